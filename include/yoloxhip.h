@@ -1,0 +1,200 @@
+/*
+ * yoloxhip.h -- C ABI of libyoloxhip.so, the MI355X (gfx950) hot path of YOLOX.
+ *
+ * The reference (pixeltable-yolox) is pure Python over PyTorch/torchvision; it has
+ * no FFI of its own.  Each entry point below replaces the library kernels the
+ * reference reaches through torch.nn / torchvision at the cited call sites, and is
+ * bound by the package's Python layer (yolox_amd/_native.py, ctypes) exactly as a
+ * maintainer would bind it from the reference.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; every buffer (including workspace) is allocated
+ *    by the caller in device memory.  Functions never allocate, free or synchronise,
+ *    so every call is legal inside hipStreamBeginCapture.
+ *  - `stream` is a hipStream_t passed as void*; work is enqueued asynchronously.
+ *  - Return 0 on success, a negative YXH_E* code otherwise; yxh_last_error() gives
+ *    a thread-local message.
+ *  - Activations are NHWC with explicit pixel stride (`cstride`, elements between
+ *    consecutive pixels) and image stride (`bstride`), so channel slices of a wider
+ *    buffer (torch.cat outputs) and nearest-x2 upsampled reads (nn.Upsample) are
+ *    addressed in place -- no concat or upsample tensor is ever materialised.
+ */
+#ifndef YOLOXHIP_H
+#define YOLOXHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YXH_ABI_VERSION 1
+
+enum yxh_status {
+    YXH_OK = 0,
+    YXH_EINVAL = -1,       /* bad shape / pointer / alignment            */
+    YXH_EHIP = -2,         /* HIP runtime error                          */
+    YXH_EUNSUPPORTED = -3  /* valid request this build does not implement */
+};
+
+enum yxh_dtype { YXH_F32 = 0, YXH_BF16 = 1, YXH_F16 = 2, YXH_U8 = 3 };
+
+enum yxh_act {
+    YXH_ACT_NONE = 0,
+    YXH_ACT_SILU = 1,         /* network_blocks.py:15-24                                  */
+    YXH_ACT_RELU = 2,
+    YXH_ACT_LRELU = 3,        /* LeakyReLU(0.1)                                            */
+    YXH_ACT_DECODE = 4,       /* eval head: ch 0-1 (v+grid)*s, 2-3 exp(v)*s, 4.. sigmoid
+                                 (yolo_head.py:185-187, 233-251)                            */
+    YXH_ACT_DECODE_TRAIN = 5  /* train head: ch 0-1, 2-3 decoded, 4.. raw logits
+                                 (yolo_head.py:213-231)                                     */
+};
+
+/* One input operand of a convolution: `channels` channels starting at `ptr`. */
+typedef struct {
+    const void* ptr;  /* element pointer to channel 0 of this slice                         */
+    int32_t channels; /* channels taken from this source                                    */
+    int32_t cstride;  /* elements between consecutive pixels                                */
+    int64_t bstride;  /* elements between consecutive images                                */
+    int32_t h, w;     /* stored spatial size                                                */
+    int32_t upsample; /* 0: pixel (y,x); 1: nearest x2, reads (y>>1, x>>1) (yolo_pafpn.py:32) */
+    int32_t reserved;
+} yxh_src;
+
+/*
+ * yxh_conv2d: Conv2d (+ folded BatchNorm) + activation (+ residual), implicit GEMM on
+ * MFMA.  Replaces BaseConv.forward (network_blocks.py:48-49, conv/bn/act), the
+ * Bottleneck residual add (:97-99), torch.cat before CspLayer.conv3 / PAFPN CSPs
+ * (network_blocks.py:182, yolo_pafpn.py:98-112) via 2 sources, nn.Upsample via
+ * src.upsample, the head's 1x1 preds + cat + sigmoid + decode (yolo_head.py:149-251)
+ * via YXH_ACT_DECODE*, and DWConv's depthwise conv (network_blocks.py:55-74) via
+ * groups == cin.
+ *
+ * weight: [cout][kh][kw][cin/groups] in `dtype`, BatchNorm already folded
+ *         (yxh_fold_bn_pack).  bias: fp32 [cout].
+ * residual (optional): same dtype as dst, added AFTER the activation.
+ * dst: `dst_dtype` (dtype or F32); for DECODE acts the pixel (b, y, x) of a level is
+ *      row b*dst_bstride + (y*out_w + x)*dst_cstride of the [B, A, 5+C] output.
+ */
+typedef struct {
+    int32_t dtype;      /* YXH_F32 / YXH_BF16 / YXH_F16: inputs, weights, MFMA operands */
+    int32_t batch;
+    int32_t in_h, in_w; /* logical input size (after upsampling)                        */
+    int32_t out_h, out_w;
+    int32_t cin, cout, kh, kw, stride, pad;
+    int32_t groups;     /* 1, or cin for depthwise                                       */
+    int32_t nsrc;       /* 1 or 2; src[0].channels + src[1].channels == cin             */
+    yxh_src src[2];
+    const void* weight;
+    const float* bias;
+    const void* residual;
+    int32_t res_cstride;
+    int32_t dst_dtype;
+    int64_t res_bstride;
+    void* dst;
+    int32_t dst_cstride;
+    int32_t act;
+    int64_t dst_bstride;
+    float decode_stride; /* level stride for DECODE acts                                */
+    int32_t decode_coff; /* position of output channel 0 in the 5+C row (0 or 5)       */
+} yxh_conv_desc;
+
+int yxh_conv2d(const yxh_conv_desc* d, void* stream);
+
+/*
+ * yxh_focus_pack: Focus space-to-depth (network_blocks.py:193-208, channel order
+ * TL, BL, TR, BR) of the network input into NHWC `dst_dtype` with 16 channels
+ * (12 used, 4 zero), consumed by the stem conv.  Accepts the reference's layout
+ * (float32 NCHW, processor.py:30-37) or NHWC uint8/bf16/f16/f32 images.
+ */
+enum yxh_layout { YXH_NCHW = 0, YXH_NHWC = 1 };
+int yxh_focus_pack(const void* img, int32_t layout, int32_t img_dtype, int32_t batch, int32_t h,
+                   int32_t w, void* dst, int32_t dst_dtype, void* stream);
+
+/*
+ * yxh_spp_maxpool: SPPBottleneck pools (network_blocks.py:129-141): reads channels
+ * [0, c) of an NHWC buffer and writes max_pool(k, stride 1, pad k/2) for k = 5, 9,
+ * 13 into channels [c, 2c), [2c, 3c), [3c, 4c) of the same buffer.
+ */
+int yxh_spp_maxpool(void* buf, int32_t dtype, int32_t batch, int32_t h, int32_t w, int32_t c,
+                    int32_t cstride, int64_t bstride, void* stream);
+
+/*
+ * yxh_fold_bn_pack: BN folding (utils/model_utils.py:33-75) + repack of an
+ * nn.Conv2d weight [cout][cin_g][kh][kw] fp32 to [cout][kh][kw][cin_pad] `dtype`
+ * (zeros in [cin_g, cin_pad), e.g. the 12 Focus channels in the 16-channel layout of
+ * yxh_focus_pack).  bn_* may be NULL (plain conv: scale 1, shift 0); conv_bias may be
+ * NULL.
+ */
+int yxh_fold_bn_pack(const float* conv_w, const float* conv_bias, const float* bn_gamma,
+                     const float* bn_beta, const float* bn_mean, const float* bn_var, float eps,
+                     int32_t cout, int32_t cin_g, int32_t kh, int32_t kw, int32_t cin_pad,
+                     int32_t dtype, void* w_out, float* b_out, void* stream);
+
+/*
+ * yxh_letterbox: preproc / ValTransform (data_augment.py:140-156, processor.py:30-37)
+ * of one uint8 HWC RGB image (device memory) into a dst_h x dst_w canvas (pad 114):
+ * out_nchw != 0 -> float32 [3][dst_h][dst_w] (the reference's tensor), else uint8
+ * [dst_h][dst_w][3] (consumed directly by yxh_focus_pack).
+ */
+int yxh_letterbox(const uint8_t* src, int32_t src_h, int32_t src_w, int32_t dst_h, int32_t dst_w,
+                  int32_t out_nchw, void* dst, void* stream);
+
+/*
+ * yxh_postprocess: utils.postprocess (utils/boxes.py:31-75) with torchvision
+ * nms / batched_nms semantics (CPU branch rule: boxes.numel() > vanilla_numel ->
+ * per-class NMS, else coordinate-offset NMS) on device.
+ *   pred      [B, A, 5+C] fp32, converted to xyxy IN PLACE (boxes.py:32-37)
+ *   det       [B, A, 7] fp32 out: rows [x1,y1,x2,y2,obj,cls_conf,cls_idx] in keep order
+ *   counts    [B] int32 out: detections per image (0 == the reference's None)
+ *   workspace >= yxh_postprocess_workspace_bytes(B, A)
+ * Candidate sets larger than 16384 per image set counts[b] = -1 (unsupported).
+ */
+size_t yxh_postprocess_workspace_bytes(int32_t batch, int32_t anchors);
+int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_classes,
+                    float conf_thre, double nms_thre, int32_t class_agnostic,
+                    int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,
+                    size_t workspace_bytes, void* stream);
+
+/*
+ * Plan execution.  A forward pass is a fixed list of ops (built once per model and
+ * input shape by the Python planner) executed back-to-back on one stream, or
+ * captured once into a hipGraph and replayed (the MI355X replacement for the
+ * reference's eager per-module dispatch).
+ */
+enum yxh_op_kind { YXH_OP_CONV = 0, YXH_OP_FOCUS = 1, YXH_OP_SPP = 2 };
+typedef struct {
+    const void* img;
+    int32_t layout, img_dtype, batch, h, w, dst_dtype;
+    void* dst;
+} yxh_focus_desc;
+typedef struct {
+    void* buf;
+    int32_t dtype, batch, h, w, c, cstride;
+    int64_t bstride;
+} yxh_spp_desc;
+typedef struct {
+    int32_t kind;
+    int32_t reserved;
+    union {
+        yxh_conv_desc conv;
+        yxh_focus_desc focus;
+        yxh_spp_desc spp;
+    } u;
+} yxh_op;
+
+int yxh_run_ops(const yxh_op* ops, int32_t n, void* stream);
+int yxh_graph_create(const yxh_op* ops, int32_t n, void* stream, void** graph_exec);
+int yxh_graph_launch(void* graph_exec, void* stream);
+int yxh_graph_destroy(void* graph_exec);
+
+int yxh_abi_version(void);
+const char* yxh_last_error(void);
+size_t yxh_sizeof_op(void);        /* ABI self-check for bindings */
+size_t yxh_sizeof_conv_desc(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YOLOXHIP_H */

@@ -1,0 +1,641 @@
+// Convolution family of the YOLOX hot path on gfx950 (MI355X).
+//
+//  conv_igemm   : NHWC implicit-GEMM Conv2d (+folded BN, act, residual, head decode)
+//                 on MFMA.  D[cout x pixels] = W[cout x K] * X[K x pixels], K ordered
+//                 (ky, kx, cin) so every 16-byte chunk of K is 8 contiguous channels
+//                 of one input pixel (bf16/f16; 4 for fp32).
+//  dwconv       : depthwise 3x3 (DWConv.dconv, nano) -- HBM-bound, VALU.
+//  focus_pack   : Focus space-to-depth of the network input into 16-ch NHWC.
+//  spp_maxpool  : SPP 5/9/13 max pools, separable, one LDS plane per 16-B chunk.
+//  fold_bn_pack : BN folding + [cout][kh][kw][cin] repack of the weights.
+//
+// Reference call sites: network_blocks.py:27-208 (BaseConv, DWConv, Bottleneck,
+// SPPBottleneck, CspLayer, Focus), yolo_pafpn.py:83-116 (cat/upsample),
+// yolo_head.py:140-251 (stems, cls/reg convs, preds, decode).
+#include <stdio.h>
+
+#include "yxh_common.hpp"
+
+namespace yxh {
+
+struct ConvParams {
+    int in_h, in_w, out_h, out_w, cin, cout, kw, stride, pad;
+    int M, ohw, taps, ncb, nsrc, src0_ch;
+    const void* sptr[2];
+    int scs[2], sw[2], sup[2];
+    long long sbs[2];
+    const void* w;
+    const float* bias;
+    const void* res;
+    int res_cs;
+    long long res_bs;
+    void* dst;
+    int dst_cs;
+    long long dst_bs;
+    int dst_f32, act, dcoff, vec_store, vec_res;
+    float dstride;
+};
+
+// ---------------------------------------------------------------- MFMA step
+// One 64-byte K slab: lane l holds row (l & 15), 16-byte chunk (l >> 4) of both
+// operands.  bf16/f16: a single 16x16x32 MFMA.  f32: four 16x16x4 MFMAs; step e
+// takes element e of every chunk, i.e. K is permuted identically for A and B.
+template <typename T> struct Mma;
+template <> struct Mma<bf16> {
+    static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                      __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+    }
+};
+template <> struct Mma<f16> {
+    static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                     __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
+    }
+};
+template <> struct Mma<float> {
+    static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+    }
+};
+
+// ---------------------------------------------------------------- epilogue
+template <typename T>
+__device__ __forceinline__ void store4(const ConvParams& p, float v[4], int n, int b, int pix, int ox,
+                                       int oy) {
+    if (p.act >= YXH_ACT_DECODE) {
+        // yolo_head.py:233-251 (eval) / :213-231 (train): fp32 output rows
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            int ch = p.dcoff + n + r;
+            if (ch < 2)
+                v[r] = (v[r] + (float)(ch == 0 ? ox : oy)) * p.dstride;
+            else if (ch < 4)
+                v[r] = expf(v[r]) * p.dstride;
+            else if (p.act == YXH_ACT_DECODE)
+                v[r] = 1.0f / (1.0f + expf(-v[r]));
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+    }
+    const bool full = n + 3 < p.cout;
+    if (p.res) {
+        const T* rp = (const T*)p.res + (long long)b * p.res_bs + (long long)pix * p.res_cs + n;
+        if (full && p.vec_res && sizeof(T) == 2) {
+            uint2 u = *(const uint2*)rp;
+            T t[4];
+            __builtin_memcpy(t, &u, 8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += to_f32(t[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (n + r < p.cout) v[r] += to_f32(rp[r]);
+        }
+    }
+    long long off = (long long)b * p.dst_bs + (long long)pix * p.dst_cs + n;
+    if (p.dst_f32) {
+        float* dp = (float*)p.dst + off;
+        if (full && p.vec_store) {
+            *(float4*)dp = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (n + r < p.cout) dp[r] = v[r];
+        }
+    } else {
+        T* dp = (T*)p.dst + off;
+        if (full && p.vec_store && sizeof(T) == 2) {
+            T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
+            uint2 u;
+            __builtin_memcpy(&u, t, 8);
+            *(uint2*)dp = u;
+        } else if (full && p.vec_store) {
+            *(float4*)dp = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (n + r < p.cout) dp[r] = from_f32<T>(v[r]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- implicit GEMM
+// Block: 256 threads = 4 waves on a WR x WC grid; tile TN output channels x TM
+// output pixels; KS 64-byte K slabs per pipeline stage.  LDS holds two stages; a
+// stage is [slab][chunk][row] of 16-byte chunks with the row index XOR-swizzled by
+// (2*chunk + slab), which makes both the ds_write_b128 of the loaders (8 lanes =
+// one row's chunks) and the ds_read_b128 fragment reads (16 rows x 1 chunk per lane
+// group) bank-conflict free.
+template <typename T, int TN, int TM, int WR, int WC, int KS>
+__global__ __launch_bounds__(256) void conv_igemm(ConvParams p) {
+    constexpr int EPC = Chunk<T>::N;
+    constexpr int CPR = 4 * KS;        // chunks per row per stage
+    constexpr int KSTAGE = CPR * EPC;  // K elements per stage
+    constexpr int RPP = 256 / CPR;     // rows per loader pass
+    constexpr int NA = (TN + RPP - 1) / RPP;
+    constexpr int NB = (TM + RPP - 1) / RPP;
+    constexpr int WTN = TN / WR, WTM = TM / WC;
+    constexpr int FR = WTN / 16, FC = WTM / 16;
+    constexpr int A_BYTES = TN * CPR * 16, B_BYTES = TM * CPR * 16;
+    constexpr int BUF = A_BYTES + B_BYTES;
+    static_assert(WR * WC == 4 && FR >= 1 && FC >= 1 && TN % 8 == 0 && TM % 16 == 0, "tile");
+    __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / WC, wc = wave % WC;
+    const int n0 = blockIdx.y * TN, m0 = blockIdx.x * TM;
+    const int cq = tid % CPR, rq = tid / CPR;
+    const int ls = cq >> 2, lc = cq & 3;  // slab / chunk of this thread's loads
+    const int coff = cq * EPC;
+
+    int bb[NB], by[NB], bx[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        int r = rq + i * RPP;
+        int m = m0 + r;
+        bool ok = r < TM && m < p.M;
+        int b = ok ? m / p.ohw : 0;
+        int rem = m - b * p.ohw;
+        int oy = rem / p.out_w, ox = rem - oy * p.out_w;
+        bb[i] = ok ? b : -1;
+        by[i] = oy * p.stride - p.pad;
+        bx[i] = ox * p.stride - p.pad;
+    }
+
+    uint4 ra[NA], rb[NB];
+    auto gload = [&](int kit) {
+        const int t = kit / p.ncb, cb = kit - t * p.ncb;
+        const int ky = t / p.kw, kx = t - ky * p.kw;
+        const int c = cb * KSTAGE + coff;
+        const bool cok = c < p.cin;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            int r = rq + i * RPP, n = n0 + r;
+            ra[i] = make_uint4(0, 0, 0, 0);
+            if (r < TN && n < p.cout && cok)
+                ra[i] = *(const uint4*)((const T*)p.w + ((long long)n * p.taps + t) * p.cin + c);
+        }
+        int s = 0, cc = c;
+        if (p.nsrc == 2 && c >= p.src0_ch) {
+            s = 1;
+            cc = c - p.src0_ch;
+        }
+        const T* sp = (const T*)p.sptr[s];
+        const int scs = p.scs[s], sw = p.sw[s], up = p.sup[s];
+        const long long sbs = p.sbs[s];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            int iy = by[i] + ky, ix = bx[i] + kx;
+            rb[i] = make_uint4(0, 0, 0, 0);
+            if (bb[i] >= 0 && cok && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w)
+                rb[i] = *(const uint4*)(sp + bb[i] * sbs +
+                                        ((long long)(iy >> up) * sw + (ix >> up)) * scs + cc);
+        }
+    };
+    auto lstore = [&](int buf) {
+        char* A = smem + buf * BUF;
+        char* B = A + A_BYTES;
+        const int sw_ = 2 * lc + ls;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            int r = rq + i * RPP;
+            if (r < TN) *(uint4*)(A + ((cq)*TN + (r ^ sw_)) * 16) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            int r = rq + i * RPP;
+            if (r < TM) *(uint4*)(B + ((cq)*TM + (r ^ sw_)) * 16) = rb[i];
+        }
+    };
+
+    f32x4 acc[FR][FC];
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int frow = lane & 15, fq = lane >> 4;
+    auto compute = [&](int buf) {
+        const char* A = smem + buf * BUF;
+        const char* B = A + A_BYTES;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int chunk = s * 4 + fq, sw_ = 2 * fq + s;
+            uint4 af[FR], bf[FC];
+#pragma unroll
+            for (int i = 0; i < FR; ++i) {
+                int row = wr * WTN + i * 16 + frow;
+                af[i] = *(const uint4*)(A + (chunk * TN + (row ^ sw_)) * 16);
+            }
+#pragma unroll
+            for (int j = 0; j < FC; ++j) {
+                int row = wc * WTM + j * 16 + frow;
+                bf[j] = *(const uint4*)(B + (chunk * TM + (row ^ sw_)) * 16);
+            }
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], af[i], bf[j]);
+        }
+    };
+
+    const int nk = p.taps * p.ncb;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int k = 0; k < nk; ++k) {
+        const int cur = k & 1;
+        if (k + 1 < nk) gload(k + 1);
+        compute(cur);
+        if (k + 1 < nk) lstore(cur ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: lane holds channels n..n+3 (rows 4*fq..) of pixel column frow
+#pragma unroll
+    for (int j = 0; j < FC; ++j) {
+        const int m = m0 + wc * WTM + j * 16 + frow;
+        if (m >= p.M) continue;
+        const int b = m / p.ohw, pix = m - b * p.ohw;
+        const int oy = pix / p.out_w, ox = pix - oy * p.out_w;
+#pragma unroll
+        for (int i = 0; i < FR; ++i) {
+            const int n = n0 + wr * WTN + i * 16 + fq * 4;
+            if (n >= p.cout) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + (n + r < p.cout ? p.bias[n + r] : 0.0f);
+            store4<T>(p, v, n, b, pix, ox, oy);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- depthwise
+template <typename T>
+__global__ __launch_bounds__(256) void dwconv(ConvParams p) {
+    constexpr int EPC = Chunk<T>::N;
+    const int nch = (p.cin + EPC - 1) / EPC;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)p.M * nch) return;
+    const int ch = (int)(idx % nch);
+    const int m = (int)(idx / nch);
+    const int b = m / p.ohw, pix = m - b * p.ohw;
+    const int oy = pix / p.out_w, ox = pix - oy * p.out_w;
+    const int c0 = ch * EPC;
+    float acc[EPC];
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) acc[e] = 0.0f;
+    const T* sp = (const T*)p.sptr[0];
+    const T* w = (const T*)p.w;
+    for (int t = 0; t < p.taps; ++t) {
+        const int ky = t / p.kw, kx = t - ky * p.kw;
+        const int iy = oy * p.stride - p.pad + ky, ix = ox * p.stride - p.pad + kx;
+        if (iy < 0 || iy >= p.in_h || ix < 0 || ix >= p.in_w) continue;
+        uint4 u = *(const uint4*)(sp + b * p.sbs[0] +
+                                  ((long long)(iy >> p.sup[0]) * p.sw[0] + (ix >> p.sup[0])) * p.scs[0] + c0);
+        T xv[EPC];
+        __builtin_memcpy(xv, &u, 16);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e)
+            if (c0 + e < p.cin) acc[e] += to_f32(xv[e]) * to_f32(w[(c0 + e) * p.taps + t]);
+    }
+    for (int q = 0; q < EPC; q += 4) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[q + r] + (c0 + q + r < p.cout ? p.bias[c0 + q + r] : 0.0f);
+        if (c0 + q < p.cout) store4<T>(p, v, c0 + q, b, pix, ox, oy);
+    }
+}
+
+// ---------------------------------------------------------------- focus pack
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void focus_pack(const TI* img, int layout, int B, int H, int W, TO* dst) {
+    const int h2 = H / 2, w2 = W / 2;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)B * h2 * w2) return;
+    const int j = (int)(idx % w2);
+    const int i = (int)((idx / w2) % h2);
+    const int b = (int)(idx / ((long long)w2 * h2));
+    TO out[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int y = 2 * i + (q & 1), x = 2 * j + (q >> 1);  // TL, BL, TR, BR
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float v = layout == YXH_NCHW ? to_f32(img[(((long long)b * 3 + c) * H + y) * W + x])
+                                         : to_f32(img[(((long long)b * H + y) * W + x) * 3 + c]);
+            out[q * 3 + c] = from_f32<TO>(v);
+        }
+    }
+#pragma unroll
+    for (int k = 12; k < 16; ++k) out[k] = from_f32<TO>(0.0f);
+    uint4* d = (uint4*)(dst + idx * 16);
+#pragma unroll
+    for (int k = 0; k < (int)(16 * sizeof(TO) / 16); ++k) {
+        uint4 u;
+        __builtin_memcpy(&u, (const char*)out + 16 * k, 16);
+        d[k] = u;
+    }
+}
+
+// ---------------------------------------------------------------- SPP
+template <typename T>
+__device__ __forceinline__ uint4 vmax(uint4 a, uint4 b) {
+    constexpr int EPC = Chunk<T>::N;
+    T x[EPC], y[EPC];
+    __builtin_memcpy(x, &a, 16);
+    __builtin_memcpy(y, &b, 16);
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) x[e] = to_f32(y[e]) > to_f32(x[e]) ? y[e] : x[e];
+    uint4 r;
+    __builtin_memcpy(&r, x, 16);
+    return r;
+}
+
+// One block per (16-byte channel chunk, image): horizontal 5/9/13 maxima into LDS,
+// then vertical.  max_pool2d pads with -inf, i.e. out-of-range taps are skipped.
+template <typename T>
+__global__ __launch_bounds__(256) void spp_maxpool(T* buf, int H, int W, int C, int cs, long long bs) {
+    constexpr int EPC = Chunk<T>::N;
+    extern __shared__ __attribute__((aligned(16))) uint4 sm[];
+    const int HW = H * W;
+    uint4* P = sm;
+    uint4* H5 = sm + HW;
+    uint4* H9 = sm + 2 * HW;
+    uint4* H13 = sm + 3 * HW;
+    const int c0 = blockIdx.x * EPC;
+    T* base = buf + blockIdx.y * bs;
+    for (int q = threadIdx.x; q < HW; q += blockDim.x) P[q] = *(const uint4*)(base + (long long)q * cs + c0);
+    __syncthreads();
+    for (int q = threadIdx.x; q < HW; q += blockDim.x) {
+        const int y = q / W, x = q - y * W;
+        uint4 m5 = P[q];
+        for (int d = 1; d <= 2; ++d) {
+            if (x - d >= 0) m5 = vmax<T>(m5, P[q - d]);
+            if (x + d < W) m5 = vmax<T>(m5, P[q + d]);
+        }
+        uint4 m9 = m5;
+        for (int d = 3; d <= 4; ++d) {
+            if (x - d >= 0) m9 = vmax<T>(m9, P[q - d]);
+            if (x + d < W) m9 = vmax<T>(m9, P[q + d]);
+        }
+        uint4 m13 = m9;
+        for (int d = 5; d <= 6; ++d) {
+            if (x - d >= 0) m13 = vmax<T>(m13, P[q - d]);
+            if (x + d < W) m13 = vmax<T>(m13, P[q + d]);
+        }
+        (void)y;
+        H5[q] = m5;
+        H9[q] = m9;
+        H13[q] = m13;
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < HW; q += blockDim.x) {
+        const int y = q / W;
+        uint4 o5 = H5[q], o9 = H9[q], o13 = H13[q];
+        for (int d = 1; d <= 6; ++d) {
+            const bool up = y - d >= 0, dn = y + d < H;
+            if (d <= 2) {
+                if (up) o5 = vmax<T>(o5, H5[q - d * W]);
+                if (dn) o5 = vmax<T>(o5, H5[q + d * W]);
+            }
+            if (d <= 4) {
+                if (up) o9 = vmax<T>(o9, H9[q - d * W]);
+                if (dn) o9 = vmax<T>(o9, H9[q + d * W]);
+            }
+            if (up) o13 = vmax<T>(o13, H13[q - d * W]);
+            if (dn) o13 = vmax<T>(o13, H13[q + d * W]);
+        }
+        T* px = base + (long long)q * cs + c0;
+        *(uint4*)(px + C) = o5;
+        *(uint4*)(px + 2 * C) = o9;
+        *(uint4*)(px + 3 * C) = o13;
+    }
+}
+
+// ---------------------------------------------------------------- BN fold + pack
+template <typename T>
+__global__ __launch_bounds__(256) void fold_bn_pack(const float* w, const float* cb, const float* g,
+                                                    const float* beta, const float* mean, const float* var,
+                                                    float eps, int cout, int cin_g, int kh, int kw,
+                                                    int cin_pad, T* wo, float* bo) {
+    const int taps = kh * kw;
+    const long long total = (long long)cout * taps * cin_pad;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int c = (int)(idx % cin_pad);
+    const int t = (int)((idx / cin_pad) % taps);
+    const int n = (int)(idx / ((long long)cin_pad * taps));
+    const float scale = g ? g[n] / sqrtf(var[n] + eps) : 1.0f;
+    const int ky = t / kw, kx = t - ky * kw;
+    float v = c < cin_g ? w[(((long long)n * cin_g + c) * kh + ky) * kw + kx] * scale : 0.0f;
+    wo[idx] = from_f32<T>(v);
+    if (t == 0 && c == 0) {
+        float b = g ? beta[n] - mean[n] * scale : 0.0f;
+        if (cb) b += cb[n] * scale;
+        bo[n] = b;
+    }
+}
+
+// ================================================================ host side
+namespace {
+
+int elem_size(int dt) { return dt == YXH_F32 ? 4 : dt == YXH_U8 ? 1 : 2; }
+
+bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
+
+template <typename T, int TN, int TM, int WR, int WC>
+int launch_igemm(const ConvParams& p, int ks, hipStream_t st) {
+    dim3 grid((p.M + TM - 1) / TM, (p.cout + TN - 1) / TN);
+    if (ks == 2)
+        hipLaunchKernelGGL((conv_igemm<T, TN, TM, WR, WC, 2>), grid, dim3(256), 0, st, p);
+    else
+        hipLaunchKernelGGL((conv_igemm<T, TN, TM, WR, WC, 1>), grid, dim3(256), 0, st, p);
+    YXH_CHECK_LAUNCH("conv_igemm launch");
+    return YXH_OK;
+}
+
+template <typename T>
+int dispatch_igemm(const ConvParams& p, int ks, hipStream_t st) {
+    if (p.cout <= 16) return launch_igemm<T, 16, 256, 1, 4>(p, ks, st);
+    if (p.cout <= 32) return launch_igemm<T, 32, 256, 1, 4>(p, ks, st);
+    if (p.cout <= 64) return launch_igemm<T, 64, 256, 1, 4>(p, ks, st);
+    if (p.cout <= 80) return launch_igemm<T, 80, 128, 1, 4>(p, ks, st);
+    return launch_igemm<T, 128, 128, 2, 2>(p, ks, st);
+}
+
+}  // namespace
+
+int conv2d(const yxh_conv_desc* d, hipStream_t st) {
+    YXH_CHECK_ARG(d, "null descriptor");
+    const int dt = d->dtype;
+    YXH_CHECK_ARG(dt == YXH_F32 || dt == YXH_BF16 || dt == YXH_F16, "conv dtype %d", dt);
+    const int es = elem_size(dt), epc = 16 / es;
+    YXH_CHECK_ARG(d->batch > 0 && d->out_h > 0 && d->out_w > 0 && d->in_h > 0 && d->in_w > 0, "empty conv");
+    YXH_CHECK_ARG(d->cin > 0 && d->cout > 0 && d->kh > 0 && d->kw > 0 && d->stride > 0 && d->pad >= 0,
+                  "bad conv geometry");
+    YXH_CHECK_ARG(d->nsrc == 1 || d->nsrc == 2, "nsrc %d", d->nsrc);
+    YXH_CHECK_ARG(d->weight && d->bias && d->dst, "null weight/bias/dst");
+    YXH_CHECK_ARG(d->dst_dtype == dt || d->dst_dtype == YXH_F32, "dst dtype %d", d->dst_dtype);
+    YXH_CHECK_ARG(d->act >= YXH_ACT_NONE && d->act <= YXH_ACT_DECODE_TRAIN, "act %d", d->act);
+    YXH_CHECK_ARG(d->act < YXH_ACT_DECODE || d->dst_dtype == YXH_F32, "decode needs an f32 dst");
+    const bool dw = d->groups != 1;
+    YXH_CHECK_ARG(!dw || (d->groups == d->cin && d->cout == d->cin && d->nsrc == 1), "groups %d", d->groups);
+    int chs = 0;
+    for (int s = 0; s < d->nsrc; ++s) {
+        const yxh_src& q = d->src[s];
+        YXH_CHECK_ARG(q.ptr && aligned16(q.ptr), "src%d null or not 16-byte aligned", s);
+        YXH_CHECK_ARG(q.channels > 0 && q.channels % epc == 0, "src%d channels %d not a multiple of %d", s,
+                      q.channels, epc);
+        YXH_CHECK_ARG(q.cstride % epc == 0 && q.bstride % epc == 0, "src%d strides not 16-byte multiples", s);
+        YXH_CHECK_ARG(q.upsample == 0 || q.upsample == 1, "upsample %d", q.upsample);
+        YXH_CHECK_ARG((q.h << q.upsample) == d->in_h && (q.w << q.upsample) == d->in_w,
+                      "src%d spatial %dx%d (up %d) vs input %dx%d", s, q.h, q.w, q.upsample, d->in_h, d->in_w);
+        chs += q.channels;
+    }
+    YXH_CHECK_ARG(chs == d->cin, "source channels %d != cin %d", chs, d->cin);
+    YXH_CHECK_ARG((d->in_h + 2 * d->pad - d->kh) / d->stride + 1 == d->out_h &&
+                      (d->in_w + 2 * d->pad - d->kw) / d->stride + 1 == d->out_w,
+                  "output size mismatch");
+    YXH_CHECK_ARG(aligned16(d->weight), "weight not 16-byte aligned");
+
+    ConvParams p{};
+    p.in_h = d->in_h; p.in_w = d->in_w; p.out_h = d->out_h; p.out_w = d->out_w;
+    p.cin = d->cin; p.cout = d->cout; p.kw = d->kw; p.stride = d->stride; p.pad = d->pad;
+    p.ohw = d->out_h * d->out_w;
+    const long long M = (long long)d->batch * p.ohw;
+    YXH_CHECK_ARG(M < (1LL << 31), "too many output pixels");
+    p.M = (int)M;
+    p.taps = d->kh * d->kw;
+    p.nsrc = d->nsrc;
+    p.src0_ch = d->src[0].channels;
+    for (int s = 0; s < d->nsrc; ++s) {
+        p.sptr[s] = d->src[s].ptr;
+        p.scs[s] = d->src[s].cstride;
+        p.sbs[s] = d->src[s].bstride;
+        p.sw[s] = d->src[s].w;
+        p.sup[s] = d->src[s].upsample;
+    }
+    p.w = d->weight;
+    p.bias = d->bias;
+    p.res = d->residual;
+    p.res_cs = d->res_cstride;
+    p.res_bs = d->res_bstride;
+    p.dst = d->dst;
+    p.dst_cs = d->dst_cstride;
+    p.dst_bs = d->dst_bstride;
+    p.dst_f32 = d->dst_dtype == YXH_F32 && dt != YXH_F32 ? 1 : (dt == YXH_F32 ? 1 : 0);
+    p.act = d->act;
+    p.dstride = d->decode_stride;
+    p.dcoff = d->decode_coff;
+    const int des = elem_size(d->dst_dtype);
+    const int vbytes = des == 4 ? 16 : 8;
+    p.vec_store = (((uintptr_t)d->dst % vbytes) == 0 && (d->dst_cstride * des) % vbytes == 0 &&
+                   (d->dst_bstride * des) % vbytes == 0)
+                      ? 1
+                      : 0;
+    p.vec_res = d->residual && ((uintptr_t)d->residual % 8) == 0 && (d->res_cstride * es) % 8 == 0 &&
+                (d->res_bstride * es) % 8 == 0;
+
+    if (dw) {
+        YXH_CHECK_ARG(d->dst_dtype == dt && d->act < YXH_ACT_DECODE, "depthwise output");
+        const long long total = M * ((d->cin + epc - 1) / epc);
+        dim3 grid((unsigned)((total + 255) / 256));
+        if (dt == YXH_BF16) hipLaunchKernelGGL(dwconv<bf16>, grid, dim3(256), 0, st, p);
+        else if (dt == YXH_F16) hipLaunchKernelGGL(dwconv<f16>, grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL(dwconv<float>, grid, dim3(256), 0, st, p);
+        YXH_CHECK_LAUNCH("dwconv launch");
+        return YXH_OK;
+    }
+
+    // K staging: two 64-byte slabs per stage when the channel structure allows it
+    const int k2 = 8 * epc;
+    int ks = (d->cin >= k2 && (d->nsrc == 1 || p.src0_ch % k2 == 0)) ? 2 : 1;
+    const int kstage = 4 * ks * epc;
+    YXH_CHECK_ARG(d->nsrc == 1 || p.src0_ch % kstage == 0, "src0 channels %d not a multiple of %d", p.src0_ch,
+                  kstage);
+    p.ncb = (d->cin + kstage - 1) / kstage;
+    if (dt == YXH_BF16) return dispatch_igemm<bf16>(p, ks, st);
+    if (dt == YXH_F16) return dispatch_igemm<f16>(p, ks, st);
+    return dispatch_igemm<float>(p, ks, st);
+}
+
+int focus_pack_launch(const void* img, int layout, int idt, int B, int H, int W, void* dst, int odt,
+                      hipStream_t st) {
+    YXH_CHECK_ARG(img && dst, "null pointer");
+    YXH_CHECK_ARG(B > 0 && H > 1 && W > 1 && H % 2 == 0 && W % 2 == 0, "image size %dx%d", H, W);
+    YXH_CHECK_ARG(layout == YXH_NCHW || layout == YXH_NHWC, "layout %d", layout);
+    YXH_CHECK_ARG(aligned16(dst), "dst not aligned");
+    const long long total = (long long)B * (H / 2) * (W / 2);
+    dim3 grid((unsigned)((total + 255) / 256));
+#define YXH_FOCUS(TI, TO) \
+    hipLaunchKernelGGL((focus_pack<TI, TO>), grid, dim3(256), 0, st, (const TI*)img, layout, B, H, W, (TO*)dst)
+#define YXH_FOCUS_OUT(TI)                          \
+    if (odt == YXH_BF16) YXH_FOCUS(TI, bf16);      \
+    else if (odt == YXH_F16) YXH_FOCUS(TI, f16);   \
+    else if (odt == YXH_F32) YXH_FOCUS(TI, float); \
+    else { set_error("focus dst dtype %d", odt); return YXH_EINVAL; }
+    if (idt == YXH_F32) { YXH_FOCUS_OUT(float) }
+    else if (idt == YXH_U8) { YXH_FOCUS_OUT(uint8_t) }
+    else if (idt == YXH_BF16) { YXH_FOCUS_OUT(bf16) }
+    else if (idt == YXH_F16) { YXH_FOCUS_OUT(f16) }
+    else { set_error("focus img dtype %d", idt); return YXH_EINVAL; }
+#undef YXH_FOCUS_OUT
+#undef YXH_FOCUS
+    YXH_CHECK_LAUNCH("focus_pack launch");
+    return YXH_OK;
+}
+
+int spp_launch(void* buf, int dt, int B, int H, int W, int C, int cs, long long bs, hipStream_t st) {
+    YXH_CHECK_ARG(buf && aligned16(buf), "spp buffer");
+    const int es = elem_size(dt), epc = 16 / es;
+    YXH_CHECK_ARG(dt == YXH_F32 || dt == YXH_BF16 || dt == YXH_F16, "spp dtype");
+    YXH_CHECK_ARG(C % epc == 0 && cs % epc == 0 && bs % epc == 0 && cs >= 4 * C, "spp channels/strides");
+    const size_t lds = (size_t)4 * H * W * 16;
+    YXH_CHECK_ARG(lds <= 160 * 1024, "spp plane %dx%d too large for LDS", H, W);
+    dim3 grid(C / epc, B);
+#define YXH_SPP(T)                                                                                       \
+    do {                                                                                                 \
+        (void)hipFuncSetAttribute((const void*)spp_maxpool<T>,                                         \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                    \
+        hipLaunchKernelGGL(spp_maxpool<T>, grid, dim3(256), lds, st, (T*)buf, H, W, C, cs, bs);          \
+    } while (0)
+    if (dt == YXH_BF16) YXH_SPP(bf16);
+    else if (dt == YXH_F16) YXH_SPP(f16);
+    else YXH_SPP(float);
+#undef YXH_SPP
+    YXH_CHECK_LAUNCH("spp launch");
+    return YXH_OK;
+}
+
+int fold_launch(const float* w, const float* cb, const float* g, const float* beta, const float* mean,
+                const float* var, float eps, int cout, int cin_g, int kh, int kw, int cin_pad, int dt, void* wo,
+                float* bo, hipStream_t st) {
+    YXH_CHECK_ARG(w && wo && bo, "null pointer");
+    YXH_CHECK_ARG(!g || (beta && mean && var), "partial BN parameters");
+    YXH_CHECK_ARG(cout > 0 && cin_g > 0 && cin_pad >= cin_g && kh > 0 && kw > 0, "fold geometry");
+    const long long total = (long long)cout * kh * kw * cin_pad;
+    dim3 grid((unsigned)((total + 255) / 256));
+    if (dt == YXH_BF16)
+        hipLaunchKernelGGL(fold_bn_pack<bf16>, grid, dim3(256), 0, st, w, cb, g, beta, mean, var, eps, cout,
+                           cin_g, kh, kw, cin_pad, (bf16*)wo, bo);
+    else if (dt == YXH_F16)
+        hipLaunchKernelGGL(fold_bn_pack<f16>, grid, dim3(256), 0, st, w, cb, g, beta, mean, var, eps, cout,
+                           cin_g, kh, kw, cin_pad, (f16*)wo, bo);
+    else if (dt == YXH_F32)
+        hipLaunchKernelGGL(fold_bn_pack<float>, grid, dim3(256), 0, st, w, cb, g, beta, mean, var, eps, cout,
+                           cin_g, kh, kw, cin_pad, (float*)wo, bo);
+    else {
+        set_error("fold dtype %d", dt);
+        return YXH_EINVAL;
+    }
+    YXH_CHECK_LAUNCH("fold launch");
+    return YXH_OK;
+}
+
+}  // namespace yxh

@@ -1,0 +1,298 @@
+// Detection post-processing on gfx950: utils.postprocess (reference
+// yolox/utils/boxes.py:31-75) with torchvision nms / batched_nms semantics.
+//
+//   pp_filter : one wave per 64 anchors; the [64 x (5+C)] fp32 tile is read
+//               coalesced into LDS (odd row stride -> conflict-free row reads),
+//               cxcywh->xyxy is written back in place (boxes.py:32-37), class max
+//               (first index, :46), score >= conf (fp32, :48) and compaction by a
+//               per-image atomic counter.  Slot order is arbitrary; everything
+//               downstream is keyed by (score desc, anchor asc) so results are
+//               deterministic.
+//   pp_sort   : one 1024-thread block per image, bitonic sort of 64-bit keys in LDS
+//               (<= 16384 candidates), sorted rows gathered, max coordinate for the
+//               coordinate-offset branch.
+//   pp_mask   : 64x64 tiles of the upper-triangular suppression matrix; lane t of a
+//               wave owns sorted box i = 64*rb + t and emits one 64-bit word per column
+//               block (the wave64 <-> 64-bit mask correspondence).
+//   pp_reduce : one wave per image walks the sorted boxes, keeps the unsuppressed
+//               ones and ORs their mask rows (greedy NMS), writing detections in keep
+//               order.
+//
+// Bit-exactness: IoU is evaluated with exactly torchvision's CPU fp32 operation
+// sequence (areas=(x2-x1)*(y2-y1); inter=w*h; inter/((a_i+a_j)-inter) > (double)thr),
+// so FP contraction is disabled for this file (and -ffp-contract=off at build).
+#pragma clang fp contract(off)
+
+#include "yxh_common.hpp"
+
+namespace yxh {
+
+constexpr int kSortCap = 16384;
+constexpr int kRow = 8;  // x1 y1 x2 y2 obj conf cls score
+
+struct PPWork {
+    int* cnt;         // [B]
+    float* maxc;      // [B]
+    int* slot_of;     // [B][A]
+    unsigned long long* key;  // [B][A]
+    float* cand;      // [B][A][8]
+    float* srt;       // [B][A][8] sorted
+    unsigned long long* mask;  // [B][cap][capw]
+    int cap, capw;
+};
+
+__device__ __forceinline__ unsigned int ordered(float f) {
+    unsigned int u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ __launch_bounds__(64) void pp_filter(float* pred, int A, int C, float conf, PPWork w) {
+    extern __shared__ float tile[];  // [64][5+C]
+    const int D = 5 + C;
+    const int b = blockIdx.y, a0 = blockIdx.x * 64, lane = threadIdx.x;
+    const int rows = min(64, A - a0);
+    float* src = pred + ((long long)b * A + a0) * D;
+    for (int q = lane; q < rows * D; q += 64) tile[q] = src[q];
+    __syncthreads();
+    if (lane < rows) {
+        float* p = tile + lane * D;
+        const float cx = p[0], cy = p[1], bw = p[2], bh = p[3];
+        const float hw = bw / 2.0f, hh = bh / 2.0f;
+        const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
+        float* g = src + lane * D;
+        g[0] = x1; g[1] = y1; g[2] = x2; g[3] = y2;
+        float best = p[5];
+        int bi = 0;
+        for (int c = 1; c < C; ++c) {
+            const float v = p[5 + c];
+            if (v > best) { best = v; bi = c; }
+        }
+        const float obj = p[4];
+        const float sc = obj * best;
+        if (sc >= conf) {
+            const int a = a0 + lane;
+            const int slot = atomicAdd(&w.cnt[b], 1);
+            w.slot_of[(long long)b * A + a] = slot;
+            w.key[(long long)b * A + slot] =
+                ((unsigned long long)(~ordered(sc)) << 32) | (unsigned int)a;
+            float* r = w.cand + ((long long)b * A + slot) * kRow;
+            *(float4*)r = make_float4(x1, y1, x2, y2);
+            *(float4*)(r + 4) = make_float4(obj, best, (float)bi, sc);
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void pp_sort(int A, PPWork w, int* counts) {
+    __shared__ unsigned long long keys[kSortCap];
+    __shared__ float red[1024 / 64];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int n = w.cnt[b];
+    if (n > kSortCap || n > w.cap) {
+        if (tid == 0) counts[b] = -1;
+        return;
+    }
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (int q = tid; q < np2; q += 1024) keys[q] = q < n ? w.key[(long long)b * A + q] : ~0ull;
+    // max coordinate over the candidates' 4 box values (batched_nms coordinate trick)
+    float m = -INFINITY;
+    for (int q = tid; q < n; q += 1024) {
+        const float4 r = *(const float4*)(w.cand + ((long long)b * A + q) * kRow);
+        m = fmaxf(m, fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w)));
+    }
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) {
+        float mm = red[0];
+        for (int i = 1; i < 16; ++i) mm = fmaxf(mm, red[i]);
+        w.maxc[b] = mm;
+    }
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int q = tid; q < np2; q += 1024) {
+                const int ixj = q ^ j;
+                if (ixj > q) {
+                    const unsigned long long x = keys[q], y = keys[ixj];
+                    const bool asc = (q & k) == 0;
+                    if ((x > y) == asc) {
+                        keys[q] = y;
+                        keys[ixj] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int q = tid; q < n; q += 1024) {
+        const int a = (int)(keys[q] & 0xffffffffu);
+        const int slot = w.slot_of[(long long)b * A + a];
+        const float* s = w.cand + ((long long)b * A + slot) * kRow;
+        float* d = w.srt + ((long long)b * A + q) * kRow;
+        *(float4*)d = *(const float4*)s;
+        *(float4*)(d + 4) = *(const float4*)(s + 4);
+    }
+}
+
+struct Box {
+    float x1, y1, x2, y2, area, cls;
+};
+
+__device__ __forceinline__ Box load_box(const float* r, int mode, float step) {
+    Box bx;
+    bx.x1 = r[0]; bx.y1 = r[1]; bx.x2 = r[2]; bx.y2 = r[3];
+    bx.cls = r[6];
+    if (mode == 1) {  // coordinate trick: boxes + idxs * (max + 1)
+        const float off = bx.cls * step;
+        bx.x1 = bx.x1 + off; bx.y1 = bx.y1 + off; bx.x2 = bx.x2 + off; bx.y2 = bx.y2 + off;
+    }
+    const float ww = bx.x2 - bx.x1;
+    const float hh = bx.y2 - bx.y1;
+    bx.area = ww * hh;
+    return bx;
+}
+
+// torchvision nms_kernel.cpp inner loop, operation for operation.
+__device__ __forceinline__ bool suppresses(const Box& i, const Box& j, double thr) {
+    const float xx1 = i.x1 < j.x1 ? j.x1 : i.x1;
+    const float yy1 = i.y1 < j.y1 ? j.y1 : i.y1;
+    const float xx2 = j.x2 < i.x2 ? j.x2 : i.x2;
+    const float yy2 = j.y2 < i.y2 ? j.y2 : i.y2;
+    const float dw = xx2 - xx1, dh = yy2 - yy1;
+    const float w = 0.0f < dw ? dw : 0.0f;
+    const float h = 0.0f < dh ? dh : 0.0f;
+    const float inter = w * h;
+    const float den = (i.area + j.area) - inter;
+    const float ovr = inter / den;
+    return (double)ovr > thr;
+}
+
+__device__ __forceinline__ int image_mode(int n, int agnostic, long long vanilla_numel) {
+    if (agnostic) return 0;
+    return (4LL * n > vanilla_numel) ? 2 : 1;
+}
+
+__global__ __launch_bounds__(64) void pp_mask(int A, double thr, int agnostic, long long vanilla_numel,
+                                              PPWork w) {
+    __shared__ Box cols[64];
+    const int b = blockIdx.y, lane = threadIdx.x;
+    const int n = w.cnt[b];
+    if (n > w.cap || n <= 0) return;
+    const int mode = image_mode(n, agnostic, vanilla_numel);
+    const float step = w.maxc[b] + 1.0f;
+    const int nb = (n + 63) / 64;
+    const long long pairs = (long long)nb * (nb + 1) / 2;
+    const float* srt = w.srt + (long long)b * A * kRow;
+    for (long long pi = blockIdx.x; pi < pairs; pi += gridDim.x) {
+        // triangular index -> (rb, cb), cb >= rb
+        int rb = 0;
+        long long rem = pi;
+        while (rem >= nb - rb) {
+            rem -= nb - rb;
+            ++rb;
+        }
+        const int cb = rb + (int)rem;
+        const int j = cb * 64 + lane;
+        __syncthreads();
+        if (j < n) cols[lane] = load_box(srt + (long long)j * kRow, mode, step);
+        __syncthreads();
+        const int i = rb * 64 + lane;
+        if (i >= n) continue;
+        const Box bi = load_box(srt + (long long)i * kRow, mode, step);
+        unsigned long long bits = 0;
+        const int jn = min(64, n - cb * 64);
+        for (int t = 0; t < jn; ++t) {
+            const int jj = cb * 64 + t;
+            if (jj <= i) continue;
+            const Box& bj = cols[t];
+            if (mode == 2 && bj.cls != bi.cls) continue;
+            if (suppresses(bi, bj, thr)) bits |= 1ull << t;
+        }
+        w.mask[((long long)b * w.cap + i) * w.capw + cb] = bits;
+    }
+}
+
+__global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int* counts) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const int n = w.cnt[b];
+    if (n > w.cap) return;  // counts[b] = -1 already
+    const int nw = (n + 63) / 64;
+    unsigned long long rm[4] = {0, 0, 0, 0};  // word lane + 64k
+    const float* srt = w.srt + (long long)b * A * kRow;
+    float* out = det + (long long)b * A * 7;
+    int nk = 0;
+    for (int i = 0; i < n; ++i) {
+        const int word = i >> 6, owner = word & 63, k = word >> 6;
+        unsigned long long v = k == 0 ? rm[0] : k == 1 ? rm[1] : k == 2 ? rm[2] : rm[3];
+        unsigned int lo = __builtin_amdgcn_readlane((unsigned int)v, owner);
+        unsigned int hi = __builtin_amdgcn_readlane((unsigned int)(v >> 32), owner);
+        const unsigned long long wv = ((unsigned long long)hi << 32) | lo;
+        if ((wv >> (i & 63)) & 1ull) continue;
+        if (lane < 7) out[(long long)nk * 7 + lane] = srt[(long long)i * kRow + lane];
+        ++nk;
+        const unsigned long long* row = w.mask + ((long long)b * w.cap + i) * w.capw;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int wd = lane + 64 * q;
+            if (wd >= word && wd < nw) rm[q] |= row[wd];
+        }
+    }
+    if (lane == 0) counts[b] = nk;
+}
+
+size_t pp_workspace(int B, int A) {
+    const size_t cap = (size_t)(A < kSortCap ? A : kSortCap);
+    const size_t capw = (cap + 63) / 64;
+    size_t s = 0;
+    auto add = [&](size_t bytes) { s += (bytes + 255) & ~(size_t)255; };
+    add(sizeof(int) * B);
+    add(sizeof(float) * B);
+    add(sizeof(int) * (size_t)B * A);
+    add(sizeof(unsigned long long) * (size_t)B * A);
+    add(sizeof(float) * kRow * (size_t)B * A);
+    add(sizeof(float) * kRow * (size_t)B * A);
+    add(sizeof(unsigned long long) * (size_t)B * cap * capw);
+    return s;
+}
+
+int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
+                float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st) {
+    YXH_CHECK_ARG(pred && det && counts, "null pointer");
+    YXH_CHECK_ARG(B > 0 && A >= 0 && C > 0, "postprocess shape B=%d A=%d C=%d", B, A, C);
+    YXH_CHECK_ARG(ws && ws_bytes >= pp_workspace(B, A), "workspace too small (%zu < %zu)", ws_bytes,
+                  pp_workspace(B, A));
+    const size_t lds = (size_t)64 * (5 + C) * sizeof(float);
+    YXH_CHECK_ARG(lds <= 64 * 1024, "too many classes for the filter tile");
+    PPWork w;
+    char* p = (char*)ws;
+    auto take = [&](size_t bytes) {
+        void* r = p;
+        p += (bytes + 255) & ~(size_t)255;
+        return r;
+    };
+    w.cap = A < kSortCap ? A : kSortCap;
+    w.capw = (w.cap + 63) / 64;
+    w.cnt = (int*)take(sizeof(int) * B);
+    w.maxc = (float*)take(sizeof(float) * B);
+    w.slot_of = (int*)take(sizeof(int) * (size_t)B * A);
+    w.key = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * A);
+    w.cand = (float*)take(sizeof(float) * kRow * (size_t)B * A);
+    w.srt = (float*)take(sizeof(float) * kRow * (size_t)B * A);
+    w.mask = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * w.cap * w.capw);
+    int rc = check_hip(hipMemsetAsync(w.cnt, 0, sizeof(int) * B, st), "memset counters");
+    if (rc) return rc;
+    rc = check_hip(hipMemsetAsync(counts, 0, sizeof(int) * B, st), "memset counts");
+    if (rc) return rc;
+    if (A == 0) return YXH_OK;
+    hipLaunchKernelGGL(pp_filter, dim3((A + 63) / 64, B), dim3(64), lds, st, pred, A, C, conf, w);
+    YXH_CHECK_LAUNCH("pp_filter");
+    hipLaunchKernelGGL(pp_sort, dim3(B), dim3(1024), 0, st, A, w, counts);
+    YXH_CHECK_LAUNCH("pp_sort");
+    hipLaunchKernelGGL(pp_mask, dim3(128, B), dim3(64), 0, st, A, nms, agnostic, vanilla_numel, w);
+    YXH_CHECK_LAUNCH("pp_mask");
+    hipLaunchKernelGGL(pp_reduce, dim3(B), dim3(64), 0, st, A, w, det, counts);
+    YXH_CHECK_LAUNCH("pp_reduce");
+    return YXH_OK;
+}
+
+}  // namespace yxh

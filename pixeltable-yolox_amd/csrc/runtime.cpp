@@ -1,0 +1,152 @@
+// C-ABI surface of libyoloxhip: argument checking, error channel, the op-list
+// executor and hipGraph capture/replay of a whole forward pass.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "yxh_common.hpp"
+
+namespace yxh {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int check_hip(hipError_t e, const char* what) {
+    if (e == hipSuccess) return YXH_OK;
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return YXH_EHIP;
+}
+
+int conv2d(const yxh_conv_desc* d, hipStream_t st);
+int focus_pack_launch(const void* img, int layout, int idt, int B, int H, int W, void* dst, int odt,
+                      hipStream_t st);
+int spp_launch(void* buf, int dt, int B, int H, int W, int C, int cs, long long bs, hipStream_t st);
+int fold_launch(const float* w, const float* cb, const float* g, const float* beta, const float* mean,
+                const float* var, float eps, int cout, int cin_g, int kh, int kw, int cin_pad, int dt, void* wo,
+                float* bo, hipStream_t st);
+size_t pp_workspace(int B, int A);
+int letterbox_launch(const uint8_t* src, int sh, int sw, int th, int tw, int out_nchw, void* dst, hipStream_t st);
+int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
+                float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st);
+
+static int run_op(const yxh_op& op, hipStream_t st) {
+    switch (op.kind) {
+        case YXH_OP_CONV:
+            return conv2d(&op.u.conv, st);
+        case YXH_OP_FOCUS: {
+            const yxh_focus_desc& f = op.u.focus;
+            return focus_pack_launch(f.img, f.layout, f.img_dtype, f.batch, f.h, f.w, f.dst, f.dst_dtype, st);
+        }
+        case YXH_OP_SPP: {
+            const yxh_spp_desc& s = op.u.spp;
+            return spp_launch(s.buf, s.dtype, s.batch, s.h, s.w, s.c, s.cstride, s.bstride, st);
+        }
+        default:
+            set_error("unknown op kind %d", op.kind);
+            return YXH_EINVAL;
+    }
+}
+
+}  // namespace yxh
+
+using namespace yxh;
+
+extern "C" {
+
+int yxh_abi_version(void) { return YXH_ABI_VERSION; }
+const char* yxh_last_error(void) { return g_err; }
+size_t yxh_sizeof_op(void) { return sizeof(yxh_op); }
+size_t yxh_sizeof_conv_desc(void) { return sizeof(yxh_conv_desc); }
+
+int yxh_conv2d(const yxh_conv_desc* d, void* stream) { return conv2d(d, (hipStream_t)stream); }
+
+int yxh_focus_pack(const void* img, int32_t layout, int32_t img_dtype, int32_t batch, int32_t h, int32_t w,
+                   void* dst, int32_t dst_dtype, void* stream) {
+    return focus_pack_launch(img, layout, img_dtype, batch, h, w, dst, dst_dtype, (hipStream_t)stream);
+}
+
+int yxh_spp_maxpool(void* buf, int32_t dtype, int32_t batch, int32_t h, int32_t w, int32_t c, int32_t cstride,
+                    int64_t bstride, void* stream) {
+    return spp_launch(buf, dtype, batch, h, w, c, cstride, bstride, (hipStream_t)stream);
+}
+
+int yxh_fold_bn_pack(const float* conv_w, const float* conv_bias, const float* bn_gamma, const float* bn_beta,
+                     const float* bn_mean, const float* bn_var, float eps, int32_t cout, int32_t cin_g, int32_t kh,
+                     int32_t kw, int32_t cin_pad, int32_t dtype, void* w_out, float* b_out, void* stream) {
+    return fold_launch(conv_w, conv_bias, bn_gamma, bn_beta, bn_mean, bn_var, eps, cout, cin_g, kh, kw, cin_pad,
+                       dtype, w_out, b_out, (hipStream_t)stream);
+}
+
+int yxh_letterbox(const uint8_t* src, int32_t src_h, int32_t src_w, int32_t dst_h, int32_t dst_w,
+                  int32_t out_nchw, void* dst, void* stream) {
+    return letterbox_launch(src, src_h, src_w, dst_h, dst_w, out_nchw, dst, (hipStream_t)stream);
+}
+
+size_t yxh_postprocess_workspace_bytes(int32_t batch, int32_t anchors) { return pp_workspace(batch, anchors); }
+
+int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_classes, float conf_thre,
+                    double nms_thre, int32_t class_agnostic, int64_t vanilla_numel, float* det, int32_t* counts,
+                    void* workspace, size_t workspace_bytes, void* stream) {
+    return postprocess(pred, batch, anchors, num_classes, conf_thre, nms_thre, class_agnostic, vanilla_numel, det,
+                       counts, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int yxh_run_ops(const yxh_op* ops, int32_t n, void* stream) {
+    YXH_CHECK_ARG(ops || n == 0, "null op list");
+    for (int i = 0; i < n; ++i) {
+        int rc = run_op(ops[i], (hipStream_t)stream);
+        if (rc) {
+            char tmp[512];
+            snprintf(tmp, sizeof(tmp), "op %d: %s", i, g_err);
+            set_error("%s", tmp);
+            return rc;
+        }
+    }
+    return YXH_OK;
+}
+
+int yxh_graph_create(const yxh_op* ops, int32_t n, void* stream, void** graph_exec) {
+    YXH_CHECK_ARG(graph_exec, "null graph_exec");
+    (void)stream;
+    hipStream_t cap;
+    int rc = check_hip(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking), "capture stream");
+    if (rc) return rc;
+    rc = check_hip(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal), "begin capture");
+    if (rc) {
+        (void)hipStreamDestroy(cap);
+        return rc;
+    }
+    int orc = yxh_run_ops(ops, n, cap);
+    hipGraph_t g = nullptr;
+    rc = check_hip(hipStreamEndCapture(cap, &g), "end capture");
+    (void)hipStreamDestroy(cap);
+    if (orc) {
+        if (g) (void)hipGraphDestroy(g);
+        return orc;
+    }
+    if (rc) return rc;
+    hipGraphExec_t ge = nullptr;
+    rc = check_hip(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0), "instantiate");
+    (void)hipGraphDestroy(g);
+    if (rc) return rc;
+    *graph_exec = (void*)ge;
+    return YXH_OK;
+}
+
+int yxh_graph_launch(void* graph_exec, void* stream) {
+    YXH_CHECK_ARG(graph_exec, "null graph");
+    return check_hip(hipGraphLaunch((hipGraphExec_t)graph_exec, (hipStream_t)stream), "graph launch");
+}
+
+int yxh_graph_destroy(void* graph_exec) {
+    if (!graph_exec) return YXH_OK;
+    return check_hip(hipGraphExecDestroy((hipGraphExec_t)graph_exec), "graph destroy");
+}
+
+}  // extern "C"

@@ -1,0 +1,53 @@
+// Shared device/host helpers for libyoloxhip (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "yoloxhip.h"
+
+namespace yxh {
+
+typedef __bf16 bf16;
+typedef _Float16 f16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// Wavefront width on CDNA4 (never 32).
+constexpr int kWave = 64;
+
+template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T)v; }
+
+// 16-byte chunk of T (8 bf16/f16, 4 f32): the unit of every global/LDS move.
+template <typename T> struct Chunk { static constexpr int N = 16 / sizeof(T); };
+
+__device__ __forceinline__ float silu(float v) { return v / (1.0f + __expf(-v)); }
+__device__ __forceinline__ float sigmoid(float v) { return 1.0f / (1.0f + __expf(-v)); }
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+    switch (act) {
+        case YXH_ACT_SILU: return silu(v);
+        case YXH_ACT_RELU: return v > 0.0f ? v : 0.0f;
+        case YXH_ACT_LRELU: return v > 0.0f ? v : 0.1f * v;
+        default: return v;
+    }
+}
+
+// Host-side error channel (thread-local message, see runtime.cpp).
+void set_error(const char* fmt, ...);
+int check_hip(hipError_t e, const char* what);
+
+}  // namespace yxh
+
+#define YXH_CHECK_ARG(cond, ...)              \
+    do {                                      \
+        if (!(cond)) {                        \
+            ::yxh::set_error(__VA_ARGS__);    \
+            return YXH_EINVAL;                \
+        }                                     \
+    } while (0)
+
+#define YXH_CHECK_LAUNCH(what) \
+    do { int _rc = ::yxh::check_hip(hipGetLastError(), what); if (_rc) return _rc; } while (0)

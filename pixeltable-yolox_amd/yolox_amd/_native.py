@@ -1,0 +1,140 @@
+"""ctypes binding of libyoloxhip.so (include/yoloxhip.h).
+
+The HIP library is the only compute path of this package: there is no CPU or
+PyTorch fallback.  If the library is missing or fails to load, every op raises.
+torch is imported first so that the library binds to the HIP runtime torch already
+loaded (both carry SONAME libamdhip64.so.7), which makes torch's stream handles and
+device pointers valid here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch  # noqa: F401  (must precede loading the HIP library)
+
+LIB_PATH = os.environ.get(
+    "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
+
+ABI_VERSION = 1
+
+# enums (yoloxhip.h)
+OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
+F32, BF16, F16, U8 = 0, 1, 2, 3
+ACT_NONE, ACT_SILU, ACT_RELU, ACT_LRELU, ACT_DECODE, ACT_DECODE_TRAIN = range(6)
+NCHW, NHWC = 0, 1
+OP_CONV, OP_FOCUS, OP_SPP = 0, 1, 2
+
+TORCH_DTYPE = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16, U8: torch.uint8}
+DTYPE_CODE = {v: k for k, v in TORCH_DTYPE.items()}
+ACT_CODE = {"silu": ACT_SILU, "relu": ACT_RELU, "lrelu": ACT_LRELU, None: ACT_NONE, "none": ACT_NONE}
+
+
+class Src(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("channels", C.c_int32), ("cstride", C.c_int32),
+                ("bstride", C.c_int64), ("h", C.c_int32), ("w", C.c_int32),
+                ("upsample", C.c_int32), ("reserved", C.c_int32)]
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [("dtype", C.c_int32), ("batch", C.c_int32), ("in_h", C.c_int32), ("in_w", C.c_int32),
+                ("out_h", C.c_int32), ("out_w", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32),
+                ("kh", C.c_int32), ("kw", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32),
+                ("groups", C.c_int32), ("nsrc", C.c_int32), ("src", Src * 2), ("weight", C.c_void_p),
+                ("bias", C.c_void_p), ("residual", C.c_void_p), ("res_cstride", C.c_int32),
+                ("dst_dtype", C.c_int32), ("res_bstride", C.c_int64), ("dst", C.c_void_p),
+                ("dst_cstride", C.c_int32), ("act", C.c_int32), ("dst_bstride", C.c_int64),
+                ("decode_stride", C.c_float), ("decode_coff", C.c_int32)]
+
+
+class FocusDesc(C.Structure):
+    _fields_ = [("img", C.c_void_p), ("layout", C.c_int32), ("img_dtype", C.c_int32), ("batch", C.c_int32),
+                ("h", C.c_int32), ("w", C.c_int32), ("dst_dtype", C.c_int32), ("dst", C.c_void_p)]
+
+
+class SppDesc(C.Structure):
+    _fields_ = [("buf", C.c_void_p), ("dtype", C.c_int32), ("batch", C.c_int32), ("h", C.c_int32),
+                ("w", C.c_int32), ("c", C.c_int32), ("cstride", C.c_int32), ("bstride", C.c_int64)]
+
+
+class _OpU(C.Union):
+    _fields_ = [("conv", ConvDesc), ("focus", FocusDesc), ("spp", SppDesc)]
+
+
+class Op(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32), ("u", _OpU)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the HIP library; raise loudly if it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"libyoloxhip.so not found at {LIB_PATH}; build it with "
+                "`make -C pixeltable-yolox_amd` (or __graft_entry__.build()). "
+                "yolox_amd has no CPU fallback.")
+        L = C.CDLL(LIB_PATH)
+        vp, i32, i64, f32, f64, sz = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_double, C.c_size_t
+        sig = {
+            "yxh_abi_version": ([], C.c_int),
+            "yxh_last_error": ([], C.c_char_p),
+            "yxh_sizeof_op": ([], sz),
+            "yxh_sizeof_conv_desc": ([], sz),
+            "yxh_conv2d": ([C.POINTER(ConvDesc), vp], C.c_int),
+            "yxh_focus_pack": ([vp, i32, i32, i32, i32, i32, vp, i32, vp], C.c_int),
+            "yxh_spp_maxpool": ([vp, i32, i32, i32, i32, i32, i32, i64, vp], C.c_int),
+            "yxh_fold_bn_pack": ([vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, i32, vp, vp, vp],
+                                 C.c_int),
+            "yxh_letterbox": ([vp, i32, i32, i32, i32, i32, vp, vp], C.c_int),
+            "yxh_postprocess_workspace_bytes": ([i32, i32], sz),
+            "yxh_postprocess": ([vp, i32, i32, i32, f32, f64, i32, i64, vp, vp, vp, sz, vp], C.c_int),
+            "yxh_run_ops": ([C.POINTER(Op), i32, vp], C.c_int),
+            "yxh_graph_create": ([C.POINTER(Op), i32, vp, C.POINTER(vp)], C.c_int),
+            "yxh_graph_launch": ([vp, vp], C.c_int),
+            "yxh_graph_destroy": ([vp], C.c_int),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        if L.yxh_abi_version() != ABI_VERSION:
+            raise NativeError(f"ABI mismatch: library {L.yxh_abi_version()} vs binding {ABI_VERSION}")
+        if L.yxh_sizeof_op() != C.sizeof(Op) or L.yxh_sizeof_conv_desc() != C.sizeof(ConvDesc):
+            raise NativeError("struct layout mismatch between yoloxhip.h and _native.py")
+        _lib = L
+    return _lib
+
+
+EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d",
+            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_fold_bn_pack", "yxh_letterbox", "yxh_postprocess_workspace_bytes",
+            "yxh_postprocess", "yxh_run_ops", "yxh_graph_create", "yxh_graph_launch", "yxh_graph_destroy"]
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != OK:
+        msg = lib().yxh_last_error().decode(errors="replace")
+        kind = {EINVAL: ValueError, EUNSUPPORTED: NotImplementedError}.get(rc, RuntimeError)
+        raise kind(f"{what}: {msg} (rc={rc})" if what else f"{msg} (rc={rc})")
+
+
+def stream_ptr(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(t: torch.Tensor, name: str = "tensor") -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be on a ROCm device (got {t.device})")

@@ -1,0 +1,393 @@
+"""Planner + executor: turns a YoloxModule into a fixed libyoloxhip op list.
+
+A plan is built once per (model, batch, input size, compute dtype, input format):
+
+* every activation is an NHWC buffer in ONE device arena (bump-allocated, 256-B
+  aligned); concatenations are buffers whose channel slices are written directly by
+  the producing convs, nearest-x2 upsampling is a strided read flag -- nothing is
+  copied between layers;
+* every conv has its BN folded into packed ``[cout][kh][kw][cin]`` weights in a
+  second arena (yxh_fold_bn_pack, re-run whenever parameters change);
+* the head's 1x1 preds write decoded fp32 rows into the [B, A, 5+C] output.
+
+The op list runs eagerly (one ctypes call, ``yxh_run_ops``) or as a captured
+hipGraph (``capture()`` / ``replay()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from . import _native as N
+
+ALIGN = 256
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+@dataclass(eq=False)
+class Buffer:
+    h: int
+    w: int
+    c: int
+    esize: int
+    offset: int = -1
+
+    @property
+    def nelem_image(self) -> int:
+        return self.h * self.w * self.c
+
+    def full(self) -> "View":
+        return View(self, 0, self.c)
+
+    def slice(self, coff: int, ch: int) -> "View":
+        if coff < 0 or coff + ch > self.c:
+            raise ValueError(f"slice [{coff}, {coff + ch}) outside buffer of {self.c} channels")
+        return View(self, coff, ch)
+
+
+@dataclass(eq=False)
+class View:
+    buf: Buffer
+    coff: int
+    ch: int
+    up: int = 0
+
+    @property
+    def lh(self) -> int:
+        return self.buf.h << self.up
+
+    @property
+    def lw(self) -> int:
+        return self.buf.w << self.up
+
+    def upsampled(self) -> "View":
+        return View(self.buf, self.coff, self.ch, self.up + 1)
+
+    def same_storage(self, other: "View") -> bool:
+        return self.buf is other.buf and self.coff == other.coff and self.ch == other.ch
+
+
+@dataclass(eq=False)
+class WeightSpec:
+    convs: list  # [(nn.Conv2d, nn.BatchNorm2d | None)], stacked along cout
+    cout: int
+    cin_g: int
+    kh: int
+    kw: int
+    cin_pad: int
+    w_off: int = -1  # bytes into weight arena
+    b_off: int = -1  # bytes into bias arena
+
+
+@dataclass(eq=False)
+class OpRec:
+    kind: int
+    args: dict = field(default_factory=dict)
+
+
+class PlanCtx:
+    def __init__(self, batch: int, dtype: torch.dtype, device: torch.device):
+        if dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            raise ValueError(f"compute dtype {dtype} not supported (float32, bfloat16, float16)")
+        self.batch = batch
+        self.dtype = dtype
+        self.dcode = N.DTYPE_CODE[dtype]
+        self.esize = torch.empty((), dtype=dtype).element_size()
+        self.epc = 16 // self.esize
+        self.device = device
+        self.buffers: list[Buffer] = []
+        self.weights: list[WeightSpec] = []
+        self.ops: list[OpRec] = []
+        self.flops = 0.0  # algorithmic multiply-adds x2 of the recorded convs
+
+    # ---------------------------------------------------------------- buffers
+    def buffer(self, h: int, w: int, c: int) -> Buffer:
+        if c % self.epc:
+            raise ValueError(f"channel count {c} not a multiple of {self.epc}")
+        b = Buffer(h, w, c, self.esize)
+        self.buffers.append(b)
+        return b
+
+    # ---------------------------------------------------------------- ops
+    def focus(self, h: int, w: int) -> View:
+        packed = self.buffer(h // 2, w // 2, 16)
+        self.ops.append(OpRec(N.OP_FOCUS, dict(dst=packed.full(), h=h, w=w)))
+        return packed.full()
+
+    def _weights(self, convs, cin_pad: int) -> WeightSpec:
+        c0 = convs[0][0]
+        spec = WeightSpec(convs, sum(c.out_channels for c, _ in convs), c0.in_channels // c0.groups,
+                          c0.kernel_size[0], c0.kernel_size[1], cin_pad)
+        self.weights.append(spec)
+        return spec
+
+    def conv(self, m, srcs: list[View], out: Optional[View] = None, residual: Optional[View] = None) -> View:
+        """A BaseConv (conv + BN + act) over 1-2 channel-concatenated sources."""
+        conv: nn.Conv2d = m.conv
+        cin = sum(s.ch for s in srcs)
+        lh, lw = srcs[0].lh, srcs[0].lw
+        if any(s.lh != lh or s.lw != lw for s in srcs):
+            raise ValueError("concatenated sources differ in spatial size")
+        groups = conv.groups
+        cin_pad = cin
+        if groups == 1:
+            if conv.in_channels > cin:
+                raise ValueError(f"conv expects {conv.in_channels} channels, got {cin}")
+            if conv.in_channels != cin and not (conv.in_channels == 12 and cin == 16):
+                raise ValueError(f"conv expects {conv.in_channels} channels, got {cin}")
+        elif groups != cin or conv.out_channels != cin:
+            raise NotImplementedError("only depthwise grouped convs are supported")
+        kh, kw = conv.kernel_size
+        sh, sw_ = conv.stride
+        ph, pw = conv.padding
+        if kh != kw or sh != sw_ or ph != pw:
+            raise NotImplementedError("square kernels/strides/padding only")
+        oh = (lh + 2 * ph - kh) // sh + 1
+        ow = (lw + 2 * pw - kw) // sw_ + 1
+        if out is None:
+            out = self.buffer(oh, ow, conv.out_channels).full()
+        if out.ch != conv.out_channels or out.lh != oh or out.lw != ow or out.up:
+            raise ValueError("output view does not match the conv")
+        spec = self._weights([(conv, m.bn)], cin_pad if groups == 1 else 1)
+        self.ops.append(OpRec(N.OP_CONV, dict(
+            srcs=list(srcs), out=out, residual=residual, spec=spec, cin=cin, cout=conv.out_channels, k=kh,
+            stride=sh, pad=ph, groups=groups, in_h=lh, in_w=lw, out_h=oh, out_w=ow,
+            act=N.ACT_CODE[getattr(m, "act_name", "silu")], dst_f32=False)))
+        self.flops += 2.0 * self.batch * oh * ow * conv.out_channels * kh * kw * (conv.in_channels // groups)
+        return out
+
+    def spp(self, cat: Buffer, hidden: int) -> None:
+        self.ops.append(OpRec(N.OP_SPP, dict(buf=cat, c=hidden)))
+
+    def head_preds(self, k: int, head, cls_feat: View, reg_feat: View, out: "OutBuffer", a_off: int,
+                   stride: int, train: bool) -> None:
+        act = N.ACT_DECODE_TRAIN if train else N.ACT_DECODE
+        h, w = cls_feat.lh, cls_feat.lw
+        for convs, feat, coff in (([(head.reg_preds[k], None), (head.obj_preds[k], None)], reg_feat, 0),
+                                  ([(head.cls_preds[k], None)], cls_feat, 5)):
+            spec = self._weights(convs, feat.ch)
+            cout = spec.cout
+            self.ops.append(OpRec(N.OP_CONV, dict(
+                srcs=[feat], out=None, head_out=(out, a_off, coff), residual=None, spec=spec, cin=feat.ch,
+                cout=cout, k=1, stride=1, pad=0, groups=1, in_h=h, in_w=w, out_h=h, out_w=w, act=act,
+                decode_stride=float(stride), decode_coff=coff, dst_f32=True)))
+            self.flops += 2.0 * self.batch * h * w * cout * feat.ch
+
+
+@dataclass(eq=False)
+class OutBuffer:
+    anchors: int
+    row: int  # 5 + C
+
+
+class Plan:
+    """A finalised op list with its arenas.  ``run(x)`` executes one forward pass."""
+
+    def __init__(self, model, batch: int, height: int, width: int, dtype: torch.dtype, device,
+                 input_layout: int = N.NCHW, input_dtype: torch.dtype = torch.float32, train: bool = False):
+        if height % 32 or width % 32:
+            raise ValueError("input size must be multiples of 32")
+        self.lib = N.lib()
+        self.batch, self.height, self.width = batch, height, width
+        self.device = torch.device(device)
+        self.input_layout = input_layout
+        self.input_dtype = input_dtype
+        self.dtype = dtype
+        head = model.head
+        self.num_classes = head.num_classes
+        ctx = PlanCtx(batch, dtype, self.device)
+        packed = ctx.focus(height, width)
+        feats = model.backbone.plan(ctx, packed)
+        anchors = sum(f.lh * f.lw for f in feats)
+        self.out_spec = OutBuffer(anchors, 5 + self.num_classes)
+        head.plan(ctx, feats, self.out_spec, train=train)
+        self.ctx = ctx
+        self.anchors = anchors
+        self.flops = ctx.flops
+        # ------------------------------------------------ arenas
+        off = 0
+        for b in ctx.buffers:
+            b.offset = off
+            off += _align(batch * b.nelem_image * b.esize)
+        self.act_bytes = off
+        self.arena = torch.empty(max(off, 1), dtype=torch.uint8, device=self.device)
+        woff = boff = 0
+        for s in ctx.weights:
+            s.w_off = woff
+            woff += _align(s.cout * s.kh * s.kw * s.cin_pad * ctx.esize)
+            s.b_off = boff
+            boff += _align(s.cout * 4)
+        self.warena = torch.empty(max(woff, 1), dtype=torch.uint8, device=self.device)
+        self.barena = torch.empty(max(boff, 1), dtype=torch.uint8, device=self.device)
+        self.output = torch.empty(batch, anchors, 5 + self.num_classes, dtype=torch.float32, device=self.device)
+        self._input_slot: Optional[torch.Tensor] = None
+        self._ops = (N.Op * len(ctx.ops))()
+        self._focus_index = None
+        self._graph = None
+        self._graph_ptrs = None
+        self._param_sig = None
+        self._model = model
+        self._encode_ops()
+
+    # -------------------------------------------------------------- encoding
+    def _ptr(self, v: View) -> int:
+        return self.arena.data_ptr() + v.buf.offset + v.coff * v.buf.esize
+
+    def _encode_ops(self) -> None:
+        ctx, B = self.ctx, self.batch
+        for i, rec in enumerate(ctx.ops):
+            op = self._ops[i]
+            op.kind = rec.kind
+            a = rec.args
+            if rec.kind == N.OP_FOCUS:
+                f = op.u.focus
+                f.layout = self.input_layout
+                f.img_dtype = N.DTYPE_CODE[self.input_dtype]
+                f.batch, f.h, f.w = B, a["h"], a["w"]
+                f.dst_dtype = ctx.dcode
+                f.dst = self._ptr(a["dst"])
+                f.img = None
+                self._focus_index = i
+            elif rec.kind == N.OP_SPP:
+                s = op.u.spp
+                buf: Buffer = a["buf"]
+                s.buf = self.arena.data_ptr() + buf.offset
+                s.dtype, s.batch, s.h, s.w, s.c = ctx.dcode, B, buf.h, buf.w, a["c"]
+                s.cstride, s.bstride = buf.c, buf.nelem_image
+            else:
+                d = op.u.conv
+                d.dtype, d.batch = ctx.dcode, B
+                d.in_h, d.in_w, d.out_h, d.out_w = a["in_h"], a["in_w"], a["out_h"], a["out_w"]
+                d.cin, d.cout, d.kh, d.kw = a["cin"], a["cout"], a["k"], a["k"]
+                d.stride, d.pad, d.groups = a["stride"], a["pad"], a["groups"]
+                d.nsrc = len(a["srcs"])
+                for j, v in enumerate(a["srcs"]):
+                    s = d.src[j]
+                    s.ptr = self._ptr(v)
+                    s.channels, s.cstride, s.bstride = v.ch, v.buf.c, v.buf.nelem_image
+                    s.h, s.w, s.upsample = v.buf.h, v.buf.w, v.up
+                spec: WeightSpec = a["spec"]
+                d.weight = self.warena.data_ptr() + spec.w_off
+                d.bias = self.barena.data_ptr() + spec.b_off
+                res = a["residual"]
+                if res is not None:
+                    d.residual = self._ptr(res)
+                    d.res_cstride, d.res_bstride = res.buf.c, res.buf.nelem_image
+                d.act = a["act"]
+                if a["dst_f32"]:
+                    out, a_off, coff = a["head_out"]
+                    row = out.row
+                    d.dst = self.output.data_ptr() + (a_off * row + coff) * 4
+                    d.dst_dtype = N.F32
+                    d.dst_cstride, d.dst_bstride = row, out.anchors * row
+                    d.decode_stride, d.decode_coff = a["decode_stride"], a["decode_coff"]
+                else:
+                    v = a["out"]
+                    d.dst = self._ptr(v)
+                    d.dst_dtype = ctx.dcode
+                    d.dst_cstride, d.dst_bstride = v.buf.c, v.buf.nelem_image
+
+    # -------------------------------------------------------------- weights
+    def _signature(self):
+        return tuple((p.data_ptr(), p._version) for p in self._model.state_dict().values())
+
+    def pack_weights(self, force: bool = False) -> None:
+        sig = self._signature()
+        if not force and sig == self._param_sig:
+            return
+        stream = N.stream_ptr(self.device)
+        dt = self.ctx.dcode
+        keep = []
+        for s in self.ctx.weights:
+            row = 0
+            for conv, bn in s.convs:
+                w = conv.weight.detach().to(self.device, torch.float32).contiguous()
+                keep.append(w)
+                args = [None, None, None, None, None]
+                if conv.bias is not None:
+                    args[0] = conv.bias.detach().to(self.device, torch.float32).contiguous()
+                if bn is not None:
+                    args[1:] = [t.detach().to(self.device, torch.float32).contiguous()
+                                for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)]
+                keep.extend(a for a in args if a is not None)
+                eps = float(bn.eps) if bn is not None else 0.0
+                ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+                wout = self.warena.data_ptr() + s.w_off + row * s.kh * s.kw * s.cin_pad * self.ctx.esize
+                bout = self.barena.data_ptr() + s.b_off + row * 4
+                N.check(self.lib.yxh_fold_bn_pack(
+                    w.data_ptr(), ptr(args[0]), ptr(args[1]), ptr(args[2]), ptr(args[3]), ptr(args[4]), eps,
+                    conv.out_channels, conv.in_channels // conv.groups, s.kh, s.kw, s.cin_pad, dt, wout, bout,
+                    stream), "fold_bn_pack")
+                row += conv.out_channels
+        torch.cuda.current_stream(self.device).synchronize()  # `keep` tensors die after this
+        del keep
+        self._param_sig = sig
+
+    # -------------------------------------------------------------- execution
+    def _bind_input(self, x: torch.Tensor) -> torch.Tensor:
+        B, H, W = self.batch, self.height, self.width
+        expect = (B, 3, H, W) if self.input_layout == N.NCHW else (B, H, W, 3)
+        if tuple(x.shape) != expect:
+            raise ValueError(f"input shape {tuple(x.shape)} != planned {expect}")
+        if x.dtype != self.input_dtype:
+            raise ValueError(f"input dtype {x.dtype} != planned {self.input_dtype}")
+        if x.device != self.device:
+            x = x.to(self.device, non_blocking=True)
+        x = x.contiguous()
+        self._ops[self._focus_index].u.focus.img = x.data_ptr()
+        return x
+
+    def run(self, x: torch.Tensor) -> torch.Tensor:
+        """Eager execution of the op list on the current stream; returns the plan's
+        output buffer [B, A, 5+C] (overwritten by the next run)."""
+        self.pack_weights()
+        x = self._bind_input(x)
+        N.check(self.lib.yxh_run_ops(self._ops, len(self._ops), N.stream_ptr(self.device)), "forward")
+        return self.output
+
+    def static_input(self) -> torch.Tensor:
+        """The fixed input buffer a captured graph reads."""
+        if self._input_slot is None:
+            shape = ((self.batch, 3, self.height, self.width) if self.input_layout == N.NCHW
+                     else (self.batch, self.height, self.width, 3))
+            self._input_slot = torch.zeros(shape, dtype=self.input_dtype, device=self.device)
+        return self._input_slot
+
+    def capture(self) -> None:
+        """Capture the whole forward into a hipGraph reading ``static_input()``."""
+        self.pack_weights()
+        self._bind_input(self.static_input())
+        if self._graph is not None:
+            N.check(self.lib.yxh_graph_destroy(self._graph))
+            self._graph = None
+        g = C.c_void_p()
+        torch.cuda.synchronize(self.device)
+        N.check(self.lib.yxh_graph_create(self._ops, len(self._ops), N.stream_ptr(self.device), C.byref(g)),
+                "graph capture")
+        self._graph = g
+
+    def replay(self) -> torch.Tensor:
+        if self._graph is None:
+            self.capture()
+        N.check(self.lib.yxh_graph_launch(self._graph, N.stream_ptr(self.device)), "graph replay")
+        return self.output
+
+    def __del__(self):
+        g = getattr(self, "_graph", None)
+        if g is not None:
+            try:
+                self.lib.yxh_graph_destroy(g)
+            except Exception:
+                pass
+
+    # -------------------------------------------------------------- reporting
+    def conv_ops(self):
+        """(index, ConvDesc) of every conv op, for per-kernel roofline accounting."""
+        return [(i, self._ops[i].u.conv) for i, r in enumerate(self.ctx.ops) if r.kind == N.OP_CONV]

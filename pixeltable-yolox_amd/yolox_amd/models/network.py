@@ -1,0 +1,252 @@
+"""YOLOX module tree: CSPDarknet backbone, PAFPN neck, decoupled head.
+
+The attribute names and parameter shapes follow the reference exactly
+(network_blocks.py, darknet.py:95-177, yolo_pafpn.py:12-116, yolo_head.py:16-138)
+so MegVii ``.pth`` checkpoints and reference state_dicts load unchanged (462 keys
+for yolox_s; tests/test_api.py checks every preset).  The modules here only own
+parameters and topology: execution is planned onto libyoloxhip ops by
+``plan(...)`` methods (engine.py) -- there is no eager PyTorch forward.
+"""
+from __future__ import annotations
+
+import math
+from typing import Sequence
+
+import torch
+import torch.nn as nn
+
+
+def _act_module(name: str) -> nn.Module:
+    # network_blocks.py:15-24
+    if name == "silu":
+        return nn.SiLU(inplace=True)
+    if name == "relu":
+        return nn.ReLU(inplace=True)
+    if name == "lrelu":
+        return nn.LeakyReLU(0.1, inplace=True)
+    raise AttributeError(f"Unsupported act type: {name}")
+
+
+class _Planned(nn.Module):
+    """Modules of this tree run only as part of a planned YoloxModule forward."""
+
+    def forward(self, *args, **kwargs):  # pragma: no cover - guard
+        raise NotImplementedError(
+            f"{type(self).__name__} is executed by the HIP plan of YoloxModule; call the YoloxModule")
+
+
+class BaseConv(_Planned):
+    """Conv2d(bias=False, same padding) -> BatchNorm2d -> activation."""
+
+    def __init__(self, in_channels, out_channels, ksize, stride, groups=1, bias=False, act="silu"):
+        super().__init__()
+        self.conv = nn.Conv2d(in_channels, out_channels, ksize, stride, (ksize - 1) // 2, groups=groups, bias=bias)
+        self.bn = nn.BatchNorm2d(out_channels)
+        self.act = _act_module(act)
+        self.act_name = act
+
+    def plan(self, ctx, srcs, out=None, residual=None):
+        return ctx.conv(self, srcs, out=out, residual=residual)
+
+
+class DWConv(_Planned):
+    """Depthwise BaseConv (groups = cin) followed by a pointwise BaseConv."""
+
+    def __init__(self, in_channels, out_channels, ksize, stride=1, act="silu"):
+        super().__init__()
+        self.dconv = BaseConv(in_channels, in_channels, ksize, stride, groups=in_channels, act=act)
+        self.pconv = BaseConv(in_channels, out_channels, 1, 1, groups=1, act=act)
+
+    def plan(self, ctx, srcs, out=None, residual=None):
+        t = ctx.conv(self.dconv, srcs)
+        return ctx.conv(self.pconv, [t], out=out, residual=residual)
+
+
+def _conv_cls(depthwise: bool):
+    return DWConv if depthwise else BaseConv
+
+
+class Bottleneck(_Planned):
+    def __init__(self, in_channels, out_channels, shortcut=True, expansion=0.5, depthwise=False, act="silu"):
+        super().__init__()
+        hidden = int(out_channels * expansion)
+        self.conv1 = BaseConv(in_channels, hidden, 1, stride=1, act=act)
+        self.conv2 = _conv_cls(depthwise)(hidden, out_channels, 3, stride=1, act=act)
+        self.use_add = shortcut and in_channels == out_channels
+
+    def plan(self, ctx, x, out):
+        """y = conv2(conv1(x)) (+ x); ``out`` may alias ``x`` (in-place residual)."""
+        t = self.conv1.plan(ctx, [x])
+        return self.conv2.plan(ctx, [t], out=out, residual=x if self.use_add else None)
+
+
+class SPPBottleneck(_Planned):
+    def __init__(self, in_channels, out_channels, kernel_sizes=(5, 9, 13), activation="silu"):
+        super().__init__()
+        hidden = in_channels // 2
+        self.conv1 = BaseConv(in_channels, hidden, 1, stride=1, act=activation)
+        self.m = nn.ModuleList([nn.MaxPool2d(kernel_size=k, stride=1, padding=k // 2) for k in kernel_sizes])
+        self.conv2 = BaseConv(hidden * (len(kernel_sizes) + 1), out_channels, 1, stride=1, act=activation)
+        if tuple(kernel_sizes) != (5, 9, 13):
+            raise NotImplementedError("the SPP kernel implements kernel_sizes (5, 9, 13)")
+
+    def plan(self, ctx, srcs, out=None):
+        hidden = self.conv1.conv.out_channels
+        src = srcs[0]
+        cat = ctx.buffer(src.lh, src.lw, 4 * hidden)
+        self.conv1.plan(ctx, srcs, out=cat.slice(0, hidden))
+        ctx.spp(cat, hidden)
+        return self.conv2.plan(ctx, [cat.full()], out=out)
+
+
+class CspLayer(_Planned):
+    """CSP bottleneck with 3 convs; the concat buffer [x_1 | x_2] is written in place."""
+
+    def __init__(self, in_channels, out_channels, n=1, shortcut=True, expansion=0.5, depthwise=False,
+                 act="silu"):
+        super().__init__()
+        hidden = int(out_channels * expansion)
+        self.conv1 = BaseConv(in_channels, hidden, 1, stride=1, act=act)
+        self.conv2 = BaseConv(in_channels, hidden, 1, stride=1, act=act)
+        self.conv3 = BaseConv(2 * hidden, out_channels, 1, stride=1, act=act)
+        self.m = nn.Sequential(*[Bottleneck(hidden, hidden, shortcut, 1.0, depthwise, act=act) for _ in range(n)])
+
+    def plan(self, ctx, srcs, out=None):
+        hidden = self.conv1.conv.out_channels
+        cat = ctx.buffer(srcs[0].lh, srcs[0].lw, 2 * hidden)
+        x1 = cat.slice(0, hidden)
+        self.conv1.plan(ctx, srcs, out=x1)
+        self.conv2.plan(ctx, srcs, out=cat.slice(hidden, hidden))
+        for b in self.m:
+            b.plan(ctx, x1, out=x1)
+        return self.conv3.plan(ctx, [cat.full()], out=out)
+
+
+class Focus(_Planned):
+    """Space-to-depth (TL, BL, TR, BR) + BaseConv; the slicing is yxh_focus_pack."""
+
+    def __init__(self, in_channels, out_channels, ksize=1, stride=1, act="silu"):
+        super().__init__()
+        self.conv = BaseConv(in_channels * 4, out_channels, ksize, stride, act=act)
+
+    def plan(self, ctx, packed):
+        return self.conv.plan(ctx, [packed])
+
+
+class CspDarknet(_Planned):
+    def __init__(self, dep_mul, wid_mul, out_features=("dark3", "dark4", "dark5"), depthwise=False, act="silu"):
+        super().__init__()
+        self.out_features = out_features
+        Conv = _conv_cls(depthwise)
+        bc = int(wid_mul * 64)
+        bd = max(round(dep_mul * 3), 1)
+        self.stem = Focus(3, bc, ksize=3, act=act)
+        self.dark2 = nn.Sequential(Conv(bc, bc * 2, 3, 2, act=act),
+                                   CspLayer(bc * 2, bc * 2, n=bd, depthwise=depthwise, act=act))
+        self.dark3 = nn.Sequential(Conv(bc * 2, bc * 4, 3, 2, act=act),
+                                   CspLayer(bc * 4, bc * 4, n=bd * 3, depthwise=depthwise, act=act))
+        self.dark4 = nn.Sequential(Conv(bc * 4, bc * 8, 3, 2, act=act),
+                                   CspLayer(bc * 8, bc * 8, n=bd * 3, depthwise=depthwise, act=act))
+        self.dark5 = nn.Sequential(Conv(bc * 8, bc * 16, 3, 2, act=act),
+                                   SPPBottleneck(bc * 16, bc * 16, activation=act),
+                                   CspLayer(bc * 16, bc * 16, n=bd, shortcut=False, depthwise=depthwise, act=act))
+
+    def plan(self, ctx, packed):
+        x = self.stem.plan(ctx, packed)
+        feats = []
+        for stage in (self.dark2, self.dark3, self.dark4, self.dark5):
+            x = stage[0].plan(ctx, [x])
+            for blk in list(stage)[1:]:
+                x = blk.plan(ctx, [x])
+            feats.append(x)
+        return feats[1], feats[2], feats[3]  # dark3, dark4, dark5
+
+
+class YoloPafpn(_Planned):
+    def __init__(self, depth=1.0, width=1.0, in_features=("dark3", "dark4", "dark5"),
+                 in_channels: Sequence[int] = (256, 512, 1024), depthwise=False, act="silu"):
+        super().__init__()
+        self.backbone = CspDarknet(depth, width, depthwise=depthwise, act=act)
+        self.in_features = in_features
+        self.in_channels = in_channels
+        Conv = _conv_cls(depthwise)
+        c0, c1, c2 = (int(c * width) for c in in_channels)
+        n = round(3 * depth)
+        self.upsample = nn.Upsample(scale_factor=2, mode="nearest")
+        self.lateral_conv0 = BaseConv(c2, c1, 1, 1, act=act)
+        self.C3_p4 = CspLayer(2 * c1, c1, n, False, depthwise=depthwise, act=act)
+        self.reduce_conv1 = BaseConv(c1, c0, 1, 1, act=act)
+        self.C3_p3 = CspLayer(2 * c0, c0, n, False, depthwise=depthwise, act=act)
+        self.bu_conv2 = Conv(c0, c0, 3, 2, act=act)
+        self.C3_n3 = CspLayer(2 * c0, c1, n, False, depthwise=depthwise, act=act)
+        self.bu_conv1 = Conv(c1, c1, 3, 2, act=act)
+        self.C3_n4 = CspLayer(2 * c1, c2, n, False, depthwise=depthwise, act=act)
+
+    def plan(self, ctx, packed):
+        """yolo_pafpn.py:83-116.  Every torch.cat is a pre-sliced buffer and every
+        upsample a strided read: fpn_out0 / fpn_out1 are written straight into the
+        right half of the bottom-up concat buffers they later join."""
+        x2, x1, x0 = self.backbone.plan(ctx, packed)
+        lat0 = self.lateral_conv0.conv.out_channels
+        red1 = self.reduce_conv1.conv.out_channels
+        bu1 = _out_channels(self.bu_conv1)
+        bu2 = _out_channels(self.bu_conv2)
+        p0 = ctx.buffer(x0.lh, x0.lw, bu1 + lat0)
+        fpn_out0 = self.lateral_conv0.plan(ctx, [x0], out=p0.slice(bu1, lat0))
+        f_out0 = self.C3_p4.plan(ctx, [fpn_out0.upsampled(), x1])
+        p1 = ctx.buffer(x1.lh, x1.lw, bu2 + red1)
+        fpn_out1 = self.reduce_conv1.plan(ctx, [f_out0], out=p1.slice(bu2, red1))
+        pan_out2 = self.C3_p3.plan(ctx, [fpn_out1.upsampled(), x2])
+        self.bu_conv2.plan(ctx, [pan_out2], out=p1.slice(0, bu2))
+        pan_out1 = self.C3_n3.plan(ctx, [p1.full()])
+        self.bu_conv1.plan(ctx, [pan_out1], out=p0.slice(0, bu1))
+        pan_out0 = self.C3_n4.plan(ctx, [p0.full()])
+        return pan_out2, pan_out1, pan_out0
+
+
+def _out_channels(m: nn.Module) -> int:
+    return m.pconv.conv.out_channels if isinstance(m, DWConv) else m.conv.out_channels
+
+
+class YoloxHead(_Planned):
+    def __init__(self, num_classes, width=1.0, strides=(8, 16, 32), in_channels=(256, 512, 1024), act="silu",
+                 depthwise=False):
+        super().__init__()
+        self.num_classes = num_classes
+        self.decode_in_inference = True
+        Conv = _conv_cls(depthwise)
+        hw_ = int(256 * width)
+        self.stems = nn.ModuleList()
+        self.cls_convs = nn.ModuleList()
+        self.reg_convs = nn.ModuleList()
+        self.cls_preds = nn.ModuleList()
+        self.reg_preds = nn.ModuleList()
+        self.obj_preds = nn.ModuleList()
+        for c in in_channels:
+            self.stems.append(BaseConv(int(c * width), hw_, 1, 1, act=act))
+            self.cls_convs.append(nn.Sequential(Conv(hw_, hw_, 3, 1, act=act), Conv(hw_, hw_, 3, 1, act=act)))
+            self.reg_convs.append(nn.Sequential(Conv(hw_, hw_, 3, 1, act=act), Conv(hw_, hw_, 3, 1, act=act)))
+            self.cls_preds.append(nn.Conv2d(hw_, num_classes, 1, 1, 0))
+            self.reg_preds.append(nn.Conv2d(hw_, 4, 1, 1, 0))
+            self.obj_preds.append(nn.Conv2d(hw_, 1, 1, 1, 0))
+        self.use_l1 = False
+        self.strides = list(strides)
+
+    def initialize_biases(self, prior_prob: float) -> None:
+        """yolo_head.py:129-138: cls/obj pred biases = -log((1 - p) / p)."""
+        v = -math.log((1 - prior_prob) / prior_prob)
+        with torch.no_grad():
+            for conv in list(self.cls_preds) + list(self.obj_preds):
+                conv.bias.fill_(v)
+
+    def plan(self, ctx, feats, out, train: bool = False):
+        """Per level: stem, 2x cls conv, 2x reg conv, then the 1x1 preds write decoded
+        rows straight into ``out`` [B, A, 5+C] (yolo_head.py:140-251)."""
+        a_off = 0
+        for k, x in enumerate(feats):
+            s = self.stems[k].plan(ctx, [x])
+            c = self.cls_convs[k][1].plan(ctx, [self.cls_convs[k][0].plan(ctx, [s])])
+            r = self.reg_convs[k][1].plan(ctx, [self.reg_convs[k][0].plan(ctx, [s])])
+            ctx.head_preds(k, self, c, r, out, a_off, self.strides[k], train)
+            a_off += x.lh * x.lw
+        return out

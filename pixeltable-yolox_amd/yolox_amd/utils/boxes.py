@@ -1,0 +1,129 @@
+"""Box utilities (reference yolox/utils/boxes.py).
+
+``postprocess`` runs on the device through ``yxh_postprocess`` (filter, stable
+score sort, torchvision nms / batched_nms).  The box-format helpers and
+``bboxes_iou`` are small tensor expressions kept with the reference's exact
+operation order (they are used on host-side targets, not on the hot path).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import _native as N
+
+__all__ = ["postprocess", "postprocess_device", "bboxes_iou", "xyxy2xywh", "xyxy2cxcywh", "cxcywh2xyxy",
+           "VANILLA_NUMEL_CPU", "VANILLA_NUMEL_CUDA"]
+
+# torchvision batched_nms branch rule: boxes.numel() above this -> per-class NMS
+VANILLA_NUMEL_CPU = 4000   # the reference CPU path (parity target)
+VANILLA_NUMEL_CUDA = 20000
+
+_workspaces: dict = {}
+
+
+def _workspace(device, B: int, A: int) -> torch.Tensor:
+    need = int(N.lib().yxh_postprocess_workspace_bytes(B, A))
+    ws = _workspaces.get(device)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=device)
+        _workspaces[device] = ws
+    return ws
+
+
+def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: float = 0.7,
+                       nms_thre: float = 0.45, class_agnostic: bool = False,
+                       vanilla_numel: int = VANILLA_NUMEL_CPU, det: Optional[torch.Tensor] = None,
+                       counts: Optional[torch.Tensor] = None):
+    """Asynchronous form: returns (det [B, A, 7], counts [B] int32) on the device,
+    nothing synchronised.  ``prediction`` (fp32, on device) becomes xyxy in place."""
+    N.require_device(prediction, "prediction")
+    if prediction.dtype != torch.float32 or not prediction.is_contiguous():
+        raise ValueError("prediction must be a contiguous float32 [B, A, 5+C] tensor")
+    B, A, D = prediction.shape
+    if D != 5 + num_classes:
+        raise ValueError(f"prediction has {D} columns, expected {5 + num_classes}")
+    dev = prediction.device
+    if det is None:
+        det = torch.empty(B, max(A, 1), 7, dtype=torch.float32, device=dev)
+    if counts is None:
+        counts = torch.empty(B, dtype=torch.int32, device=dev)
+    ws = _workspace(dev, B, A)
+    N.check(N.lib().yxh_postprocess(
+        prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre), int(bool(class_agnostic)),
+        int(vanilla_numel), det.data_ptr(), counts.data_ptr(), ws.data_ptr(), ws.numel(),
+        N.stream_ptr(dev)), "postprocess")
+    return det, counts
+
+
+def postprocess(prediction: torch.Tensor, num_classes: int, conf_thre: float = 0.7, nms_thre: float = 0.45,
+                class_agnostic: bool = False, vanilla_numel: int = VANILLA_NUMEL_CPU):
+    """utils.postprocess (boxes.py:31-75): list of [N, 7] tensors
+    (x1, y1, x2, y2, obj_conf, class_conf, class_pred) per image, or None.
+
+    Like the reference, ``prediction[..., :4]`` is rewritten to xyxy in place.  A
+    CPU tensor is processed on the device and written back.
+    """
+    host = not prediction.is_cuda
+    pred = prediction
+    if host:
+        pred = prediction.to(torch.device("cuda", torch.cuda.current_device()), torch.float32).contiguous()
+    elif prediction.dtype != torch.float32 or not prediction.is_contiguous():
+        pred = prediction.float().contiguous()
+    det, counts = postprocess_device(pred, num_classes, conf_thre, nms_thre, class_agnostic, vanilla_numel)
+    if pred is not prediction:
+        prediction.copy_(pred)
+    n = counts.cpu().tolist()
+    if any(c < 0 for c in n):
+        raise NotImplementedError("more than 16384 NMS candidates in one image")
+    out = []
+    for b, c in enumerate(n):
+        if c == 0:
+            out.append(None)
+        else:
+            d = det[b, :c]
+            out.append(d.cpu() if host else d)
+    return out
+
+
+def bboxes_iou(bboxes_a: torch.Tensor, bboxes_b: torch.Tensor, xyxy: bool = True) -> torch.Tensor:
+    """Pairwise IoU (boxes.py:78-101); raises IndexError unless boxes have 4 columns."""
+    if bboxes_a.shape[1] != 4 or bboxes_b.shape[1] != 4:
+        raise IndexError
+    a, b = bboxes_a, bboxes_b
+    if xyxy:
+        tl = torch.max(a[:, None, :2], b[:, :2])
+        br = torch.min(a[:, None, 2:], b[:, 2:])
+        area_a = torch.prod(a[:, 2:] - a[:, :2], 1)
+        area_b = torch.prod(b[:, 2:] - b[:, :2], 1)
+    else:
+        tl = torch.max(a[:, None, :2] - a[:, None, 2:] / 2, b[:, :2] - b[:, 2:] / 2)
+        br = torch.min(a[:, None, :2] + a[:, None, 2:] / 2, b[:, :2] + b[:, 2:] / 2)
+        area_a = torch.prod(a[:, 2:], 1)
+        area_b = torch.prod(b[:, 2:], 1)
+    en = (tl < br).type(tl.type()).prod(dim=2)
+    area_i = torch.prod(br - tl, 2) * en
+    return area_i / (area_a[:, None] + area_b - area_i)
+
+
+def xyxy2xywh(bboxes):
+    bboxes[:, 2] = bboxes[:, 2] - bboxes[:, 0]
+    bboxes[:, 3] = bboxes[:, 3] - bboxes[:, 1]
+    return bboxes
+
+
+def xyxy2cxcywh(bboxes):
+    bboxes[:, 2] = bboxes[:, 2] - bboxes[:, 0]
+    bboxes[:, 3] = bboxes[:, 3] - bboxes[:, 1]
+    bboxes[:, 0] = bboxes[:, 0] + bboxes[:, 2] * 0.5
+    bboxes[:, 1] = bboxes[:, 1] + bboxes[:, 3] * 0.5
+    return bboxes
+
+
+def cxcywh2xyxy(bboxes):
+    bboxes[:, 0] = bboxes[:, 0] - bboxes[:, 2] * 0.5
+    bboxes[:, 1] = bboxes[:, 1] - bboxes[:, 3] * 0.5
+    bboxes[:, 2] = bboxes[:, 0] + bboxes[:, 2]
+    bboxes[:, 3] = bboxes[:, 1] + bboxes[:, 3]
+    return bboxes

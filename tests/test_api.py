@@ -1,0 +1,119 @@
+"""Host-side API surface (no GPU): configs, module tree, loaders, planner."""
+import json
+import os
+
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+
+def test_named_configs_are_singletons_and_accept_dash():
+    from yolox_amd.config import YoloxConfig
+    a = YoloxConfig.get_named_config("yolox-s")
+    assert a is YoloxConfig.get_named_config("yolox_s")
+    assert (a.depth, a.width) == (0.33, 0.50)
+    assert YoloxConfig.get_named_config("nope") is None
+    t = YoloxConfig.get_named_config("yolox_tiny")
+    assert t.test_size == (416, 416) and t.width == 0.375
+    assert YoloxConfig.get_named_config("yolox_nano").depthwise
+
+
+def test_config_update_coercion():
+    from yolox_amd.config import named_config
+    c = named_config("yolox_s")
+    c.update({"max_epoch": "10", "test_size": "(320, 320)", "seed": "7", "nmsthre": "0.5"})
+    assert c.max_epoch == 10 and c.test_size == (320, 320) and c.seed == 7 and c.nmsthre == 0.5
+    with pytest.raises(AttributeError):
+        c.update({"bogus": "1"})
+
+
+@pytest.mark.parametrize("name", ["yolox_s", "yolox_m", "yolox_l", "yolox_x", "yolox_tiny", "yolox_nano"])
+def test_state_dict_matches_reference_checkpoint_layout(name):
+    from yolox_amd.config import named_config
+    with open(os.path.join(GOLDEN, "state_dict_shapes.json")) as f:
+        ref = {k: tuple(s) for k, s in json.load(f)[name]}
+    m = named_config(name).get_model()
+    mine = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    assert mine == ref
+
+
+def test_get_model_initialisation():
+    from yolox_amd.config import named_config
+    m = named_config("yolox_s").get_model()
+    bns = [x for x in m.modules() if isinstance(x, torch.nn.BatchNorm2d)]
+    assert bns and all(b.eps == 1e-3 and b.momentum == 0.03 for b in bns)
+    assert torch.allclose(m.head.cls_preds[0].bias, torch.full((80,), -4.59511985))
+    assert m.training
+
+
+def test_from_pretrained_errors(tmp_path):
+    from yolox_amd.models import YoloxModule
+    with pytest.raises(ValueError, match="Unknown model"):
+        YoloxModule.from_pretrained("yolox_q")
+    f = tmp_path / "w.pth"
+    f.write_bytes(b"0")
+    with pytest.raises(ValueError, match="config must be provided"):
+        YoloxModule.from_pretrained(str(f))
+    os.environ["YOLOX_HOME"] = str(tmp_path)
+    with pytest.raises(FileNotFoundError):
+        YoloxModule.from_pretrained("yolox_s")
+
+
+def test_from_pretrained_loads_local_checkpoint(tmp_path):
+    from yolox_amd.config import named_config
+    from yolox_amd.models import YoloxModule
+    from yolox_amd.weights import synthetic_state_dict
+    cfg = named_config("yolox_nano")
+    sd = synthetic_state_dict(cfg.get_model().state_dict(), seed=3)
+    torch.save({"model": sd}, tmp_path / "nano.pth")
+    m = YoloxModule.from_pretrained(str(tmp_path / "nano.pth"), named_config("yolox_nano"), device="cpu")
+    assert not m.training
+    assert torch.equal(m.state_dict()["head.cls_preds.1.weight"], sd["head.cls_preds.1.weight"])
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        m(torch.zeros(1, 3, 64, 64))
+
+
+def test_processor_rejects_bad_config():
+    from yolox_amd.models import YoloxProcessor
+    with pytest.raises(ValueError, match="string or YoloxConfig"):
+        YoloxProcessor(3)
+    assert YoloxProcessor("yolox-tiny").config.test_size == (416, 416)
+
+
+def test_bboxes_iou_matches_reference_fixture(golden):
+    from yolox_amd.utils import bboxes_iou
+    d = golden("boxes.npz")
+    t = torch.from_numpy
+    assert torch.equal(bboxes_iou(t(d["a_xyxy"]), t(d["b_xyxy"]), True), t(d["iou_xyxy"]))
+    assert torch.equal(bboxes_iou(t(d["a_c"]), t(d["b_c"]), False), t(d["iou_c"]))
+    with pytest.raises(IndexError):
+        bboxes_iou(torch.zeros(2, 3), torch.zeros(2, 4))
+
+
+@pytest.mark.parametrize("name,hw,gflop,anchors", [
+    ("yolox_s", 640, 26.69, 8400), ("yolox_tiny", 416, 6.41, 3549), ("yolox_nano", 416, 1.05, 3549),
+    ("yolox_l", 640, 155.29, 8400), ("yolox_x", 1280, 1125.64, 33600)])
+def test_planner_topology_and_flops(name, hw, gflop, anchors):
+    """The plan covers every conv of the reference (SURVEY.md Appendix A counts)."""
+    from yolox_amd.config import named_config
+    from yolox_amd.engine import OutBuffer, PlanCtx
+    m = named_config(name).get_model()
+    ctx = PlanCtx(1, torch.bfloat16, torch.device("cpu"))
+    feats = m.backbone.plan(ctx, ctx.focus(hw, hw))
+    A = sum(f.lh * f.lw for f in feats)
+    m.head.plan(ctx, feats, OutBuffer(A, 85))
+    assert A == anchors
+    assert round(ctx.flops / 1e9, 2) == gflop
+    n_bn_convs = sum(1 for x in m.modules() if x.__class__.__name__ == "BaseConv")
+    assert sum(1 for o in ctx.ops if o.kind == 0) == n_bn_convs + 6  # + (reg|obj, cls) preds x 3 levels
+
+
+def test_synthetic_weights_are_deterministic():
+    from yolox_amd.weights import synthetic_state_dict
+    shapes = {"a.conv.weight": (4, 3, 3, 3), "a.bn.weight": (4,), "head.cls_preds.0.bias": (80,)}
+    a = synthetic_state_dict(shapes, seed=1)
+    b = synthetic_state_dict(dict(reversed(list(shapes.items()))), seed=1)
+    for k in shapes:
+        assert torch.equal(a[k], b[k])
+    assert not torch.equal(a["a.conv.weight"], synthetic_state_dict(shapes, seed=2)["a.conv.weight"])

@@ -1,0 +1,85 @@
+"""Device post-processing (yxh_postprocess) vs the C oracle: bit-exact.
+
+The same fp32 [B, A, 5+C] prediction goes to both; keep indices, labels, boxes and
+confidences must be identical, as must the in-place xyxy conversion.  Covers both
+torchvision batched_nms branches (coordinate trick / per-class), class-agnostic
+NMS, empty images, all-filtered batches, score ties and dense overlaps.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(oracle, pred: np.ndarray, C: int, conf: float, nms: float, agnostic=False, vanilla=4000):
+    from yolox_amd.utils.boxes import postprocess
+    p_gpu = torch.from_numpy(pred.copy()).cuda()
+    got = postprocess(p_gpu, C, conf, nms, agnostic, vanilla_numel=vanilla)
+    p_cpu = pred.copy()
+    want = oracle.postprocess(p_cpu, C, conf, nms, agnostic, vanilla_numel=vanilla)
+    np.testing.assert_array_equal(p_gpu.cpu().numpy(), p_cpu)  # in-place xyxy
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        if w is None:
+            assert g is None
+        else:
+            assert g is not None
+            np.testing.assert_array_equal(g.cpu().numpy(), w)
+    return want
+
+
+def synthetic_pred(B, A, C, seed, dense=False):
+    rng = np.random.default_rng(seed)
+    pred = np.zeros((B, A, 5 + C), np.float32)
+    span = 60 if dense else 600
+    pred[..., 0:2] = rng.uniform(20, 20 + span, (B, A, 2))
+    pred[..., 2:4] = rng.uniform(4, 120, (B, A, 2))
+    pred[..., 4] = rng.uniform(0, 1, (B, A))
+    pred[..., 5:] = rng.uniform(0, 1, (B, A, C)) ** 3
+    return pred
+
+
+@pytest.mark.parametrize("conf", [0.01, 0.3, 0.65])
+@pytest.mark.parametrize("vanilla", [4000, 0])
+def test_reference_fixture_prediction(oracle, golden, conf, vanilla):
+    pred = golden("postprocess_pre_nms.npz")["prediction"]
+    run_both(oracle, pred, 80, conf, 0.65, vanilla=vanilla)
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("dense", [False, True])
+def test_random_predictions_both_branches(oracle, seed, dense):
+    pred = synthetic_pred(3, 2100, 80, seed, dense)
+    for conf in (0.05, 0.25):  # ~1900 / ~700 candidates: vanilla and trick branches
+        run_both(oracle, pred, 80, conf, 0.45)
+        run_both(oracle, pred, 80, conf, 0.65, agnostic=True)
+
+
+def test_full_640_anchor_set_low_conf(oracle):
+    """8400 anchors, conf 0.01: thousands of candidates (eval regime)."""
+    pred = synthetic_pred(2, 8400, 80, 7, dense=True)
+    want = run_both(oracle, pred, 80, 0.01, 0.65)
+    assert sum(len(w) for w in want if w is not None) > 100
+
+
+def test_empty_and_filtered(oracle):
+    pred = synthetic_pred(3, 336, 80, 1)
+    pred[1, :, 4] = 0.0  # image 1: nothing passes
+    run_both(oracle, pred, 80, 0.3, 0.45)
+    want = run_both(oracle, pred, 80, 1.5, 0.45)  # nothing anywhere
+    assert all(w is None for w in want)
+
+
+def test_score_ties_are_resolved_by_anchor_order(oracle):
+    pred = synthetic_pred(1, 500, 4, 3, dense=True)
+    pred[..., 4] = 0.5
+    pred[..., 5:] = 0.0
+    pred[0, :, 5 + 2] = 0.8  # every anchor: identical score, same class
+    run_both(oracle, pred, 4, 0.1, 0.3)
+    run_both(oracle, pred, 4, 0.1, 0.3, vanilla=0)
+
+
+def test_single_class_many_overlaps(oracle):
+    pred = synthetic_pred(2, 1024, 1, 5, dense=True)
+    run_both(oracle, pred, 1, 0.0, 0.5)
