@@ -80,7 +80,7 @@ __device__ __forceinline__ void store4(const ConvParams& p, float v[4], int n, i
         }
     } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+        for (int r = 0; r < 4; ++r) v[r] = apply_act<sizeof(T) == 4>(v[r], p.act);
     }
     const bool full = n + 3 < p.cout;
     if (p.res) {

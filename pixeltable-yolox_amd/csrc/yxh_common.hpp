@@ -23,12 +23,17 @@ template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T
 // 16-byte chunk of T (8 bf16/f16, 4 f32): the unit of every global/LDS move.
 template <typename T> struct Chunk { static constexpr int N = 16 / sizeof(T); };
 
-__device__ __forceinline__ float silu(float v) { return v / (1.0f + __expf(-v)); }
-__device__ __forceinline__ float sigmoid(float v) { return 1.0f / (1.0f + __expf(-v)); }
+// PRECISE: the fp32 parity path uses the correctly-rounded-ish expf; the bf16/f16
+// paths use the hardware exp2 (their outputs are rounded to 8/11 bits anyway).
+template <bool PRECISE>
+__device__ __forceinline__ float silu(float v) {
+    return v / (1.0f + (PRECISE ? expf(-v) : __expf(-v)));
+}
 
+template <bool PRECISE = false>
 __device__ __forceinline__ float apply_act(float v, int act) {
     switch (act) {
-        case YXH_ACT_SILU: return silu(v);
+        case YXH_ACT_SILU: return silu<PRECISE>(v);
         case YXH_ACT_RELU: return v > 0.0f ? v : 0.0f;
         case YXH_ACT_LRELU: return v > 0.0f ? v : 0.1f * v;
         default: return v;

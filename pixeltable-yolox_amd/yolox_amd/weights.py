@@ -51,18 +51,22 @@ def _tensor_for(key: str, shape: Sequence[int], seed: int) -> torch.Tensor:
     elif leaf == "running_var":
         a = np.ones(shape)
     elif _is_bn(key) and leaf == "weight":
-        a = rng.uniform(0.7, 1.3, shape)
+        # small gamma + positive beta keep the SiLUs near their linear range: a
+        # random BN network at init is otherwise on the chaotic side (relative
+        # perturbations grow ~7%/layer, so bf16 rounding of the weights alone would
+        # flip detections); this one is ordered like a trained net.
+        a = rng.uniform(0.4, 0.8, shape)
     elif _is_bn(key) and leaf == "bias":
-        a = rng.normal(0.0, 0.2, shape)
+        a = rng.normal(1.0, 0.5, shape)
     elif is_pred and leaf == "weight":
         fan_in = int(np.prod(shape[1:]))
-        gain = 0.08 if "reg_preds" in key else 1.0
+        gain = 0.08 if "reg_preds" in key else 4.0
         a = rng.normal(0.0, gain / math.sqrt(fan_in), shape)
     elif is_pred and leaf == "bias":
         if "cls_preds" in key:
-            a = rng.normal(-2.0, 1.0, shape)
+            a = rng.normal(-2.0, 1.5, shape)
         elif "obj_preds" in key:
-            a = rng.normal(-1.0, 0.5, shape)
+            a = rng.normal(0.0, 1.0, shape)
         else:
             a = rng.normal(0.0, 0.2, shape)
     elif len(shape) == 4:

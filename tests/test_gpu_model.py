@@ -4,9 +4,11 @@ The reference ran in the build container on seeded weights (tests/golden/
 make_golden.py); the same weights are regenerated here from the seed.
 * float32 compute: decoded [B, A, 85] within 1e-3 of the reference (north_star
   tolerance for bbox tensors; measured error is ~1e-5 relative);
-* bfloat16 / float16 compute: the bf16 rounding of 80 conv layers gives ~1e-2
-  relative differences in logits; the check is on the output scale (bf16 3e-2,
-  fp16 5e-3) plus box-level agreement of confident detections.
+* bfloat16 / float16 compute: rounding 80 layers' weights and activations to 8 / 11
+  mantissa bits.  Rounding only the WEIGHTS to bf16 in the fp32 oracle already moves
+  probabilities by up to 0.08 (p99 0.03) on these synthetic nets, so the bounds are
+  bf16: max 0.2 / p99 0.06, fp16: max 0.05 / p99 0.01 on probabilities and
+  centres within a fraction of a stride.
 """
 import numpy as np
 import pytest
@@ -40,16 +42,16 @@ def test_fp32_forward_matches_reference(golden, name, hw):
     assert np.abs(out[..., 4:] - ref[..., 4:]).max() < 1e-3
 
 
-@pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 3e-2), (torch.float16, 5e-3)])
-@pytest.mark.parametrize("name,hw", [("yolox_s", 128), ("yolox_tiny", 416), ("yolox_nano", 128)])
-def test_low_precision_forward(golden, dtype, tol, name, hw):
+@pytest.mark.parametrize("dtype,pmax,p99,xy", [(torch.bfloat16, 0.2, 0.06, 2.0), (torch.float16, 0.05, 0.01, 0.5)])
+@pytest.mark.parametrize("name,hw", [("yolox_s", 128), ("yolox_tiny", 416), ("yolox_nano", 128), ("yolox_x", 64)])
+def test_low_precision_forward(golden, dtype, pmax, p99, xy, name, hw):
     d = golden(f"fwd_{name}_{hw}.npz")
     x = torch.from_numpy(d["input_u8"]).permute(0, 3, 1, 2).float()
     out = model(name, dtype)(x).cpu().numpy()
     ref = d["output"]
-    assert np.abs(out[..., 4:] - ref[..., 4:]).max() < 10 * tol  # probabilities
-    # centres move by a fraction of the stride at most
-    assert np.abs(out[..., :2] - ref[..., :2]).max() < 8 * 10 * tol * 4
+    dp = np.abs(out[..., 4:] - ref[..., 4:])
+    assert dp.max() < pmax and np.quantile(dp, 0.99) < p99, (dp.max(), np.quantile(dp, 0.99))
+    assert np.abs(out[..., :2] - ref[..., :2]).max() < xy  # pixels (strides 8-32)
 
 
 def test_uint8_nhwc_input_and_graph_replay(golden):
