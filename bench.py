@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""Benchmark: YOLOX-s 640x640 bf16 forward + NMS images/sec (BASELINE.json metric,
+configs[1]: batch 32 per GPU, synthetic uniform [0,255] images, seeded weights).
+
+One step = one batch through the hot path: the captured hipGraph of the whole
+forward (Focus -> CSPDarknet -> PAFPN -> decoupled head with fused decode, 82
+kernels) followed by device post-processing (filter, sort, bitmask NMS) at the
+processor defaults (conf 0.5, nms 0.65).  Inputs are resident in HBM (bf16 NHWC)
+before the timed region.  With --gpus N (torchrun, one process per GPU) each rank
+runs an independent replica -- inference has no exchange step, so there is no
+collective in the data path -- and value = all images / max
+rank time.
+
+roofline: the dominant kernel family is conv_igemm (every conv of the network);
+one "launch" = one forward's conv stack, timed with HIP events on the plan's stream
+around every replay inside the timed region; achieved = algorithmic conv FLOPs per
+forward / mean forward duration, against the dense bf16 MFMA peak (2.5 PF).
+traffic: HBM bytes per forward from a rocprofv3 --pmc pass (profiles/traffic_*.json,
+FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), else null.
+cpu_baseline: the oracle (PyTorch-CPU fp32 restatement + C NMS) on a bounded
+sample, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "pixeltable-yolox_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "images/sec (fwd+NMS) YOLOX-s 640×640 bf16 @1/2/4/8 MI355X; box mAP parity"
+PEAK_BF16_TFLOPS = 2500.0  # dense MFMA, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="yolox_s")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--size", type=int, default=640)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--conf", type=float, default=0.5)
+    ap.add_argument("--nms", type=float, default=0.65)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layers", action="store_true", help="print a per-op time/roofline table to stderr")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def load_traffic(model, batch, size, dtype):
+    best = None
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "traffic_*.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if (d.get("model"), d.get("batch"), d.get("size"), d.get("dtype")) == (model, batch, size, dtype):
+            best = d
+    return best
+
+
+def layer_table(plan, iters=5):
+    """Per-op HIP-event timing of the eager op list (diagnostic; stderr)."""
+    from yolox_amd import _native as N
+    lib = N.lib()
+    st = torch.cuda.current_stream()
+    n = len(plan._ops)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+    tot = np.zeros(n)
+    for _ in range(iters):
+        ev[0].record(st)
+        for i in range(n):
+            N.check(lib.yxh_run_ops(C_op(plan, i), 1, st.cuda_stream))
+            ev[i + 1].record(st)
+        torch.cuda.synchronize()
+        tot += [ev[i].elapsed_time(ev[i + 1]) for i in range(n)]
+    tot /= iters
+    rows = []
+    for i, rec in enumerate(plan.ctx.ops):
+        a = rec.args
+        if rec.kind == N.OP_CONV:
+            flop = 2.0 * plan.batch * a["out_h"] * a["out_w"] * a["cout"] * a["k"] * a["k"] * (
+                a["cin"] // a["groups"] if a["groups"] > 1 else a["cin"])
+            if a["groups"] > 1:
+                flop = 2.0 * plan.batch * a["out_h"] * a["out_w"] * a["cout"] * a["k"] * a["k"]
+            es = plan.ctx.esize
+            byt = plan.batch * (a["in_h"] * a["in_w"] * a["cin"] // (1 if not a["srcs"][0].up else 4)
+                                + a["out_h"] * a["out_w"] * a["cout"] * (4 if a["dst_f32"] else 1)) * es
+            rows.append((i, f"conv k{a['k']}s{a['stride']} {a['cin']}->{a['cout']} @{a['out_h']}x{a['out_w']}",
+                         tot[i], flop / tot[i] / 1e9, byt / tot[i] / 1e6))
+        else:
+            rows.append((i, "focus" if rec.kind == N.OP_FOCUS else "spp", tot[i], 0.0, 0.0))
+    print(f"{'op':>3} {'layer':<40} {'ms':>8} {'TFLOP/s':>9} {'GB/s':>8}", file=sys.stderr)
+    for r in rows:
+        print(f"{r[0]:>3} {r[1]:<40} {r[2]:8.4f} {r[3]:9.1f} {r[4]:8.0f}", file=sys.stderr)
+    print(f"total {tot.sum():.3f} ms", file=sys.stderr)
+
+
+def C_op(plan, i):
+    import ctypes
+    from yolox_amd import _native as N
+    return ctypes.cast(ctypes.addressof(plan._ops) + i * ctypes.sizeof(N.Op), ctypes.POINTER(N.Op))
+
+
+def cpu_baseline(args, budget_s):
+    """Oracle forward (fp32, torch CPU) + oracle NMS on 640x640 images."""
+    import subprocess
+    from oracle import reference_cpu as O
+    from yolox_amd.weights import synthetic_images, synthetic_state_dict
+    from yolox_amd.config import named_config
+
+    lib = os.path.join(REPO, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle")], check=True, stdout=subprocess.DEVNULL)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = named_config(args.model)
+    sd = synthetic_state_dict(cfg.get_model().state_dict(), seed=0, bn_stats=cfg.name)
+    arch = O.ARCHS[args.model]
+    bs = 2
+    x = torch.from_numpy(O.letterbox_identity(synthetic_images(bs, args.size, args.size, seed=0)))
+    out = O.forward_eval(sd, arch, x)  # warm-up
+    n_img, t0 = 0, time.perf_counter()
+    while True:
+        out = O.forward_eval(sd, arch, x)
+        O.postprocess(out.numpy().copy(), 80, args.conf, args.nms)
+        n_img += bs
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n_img / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n_img} images ({args.model} {args.size}x{args.size}, batch {bs}, fp32 PyTorch-CPU "
+                      f"oracle forward + C oracle NMS conf {args.conf}) in {dt:.1f}s"}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    from yolox_amd import _native as N
+    from yolox_amd.models import YoloxModule
+    from yolox_amd.utils.boxes import postprocess_device
+    from yolox_amd.weights import synthetic_images
+
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
+    dev = torch.device("cuda", torch.cuda.current_device())
+    model = YoloxModule.synthetic(args.model, seed=0, device=dev, dtype=dtype)
+    B, S = args.batch, args.size
+    plan = model.plan_for(B, S, S, N.NHWC, dtype)
+    imgs = torch.from_numpy(synthetic_images(B, S, S, seed=1000 + rank)).to(dev)
+    plan.static_input().copy_(imgs.to(dtype))
+    plan.capture()
+    A = plan.anchors
+    det = torch.empty(B, A, 7, dtype=torch.float32, device=dev)
+    counts = torch.empty(B, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev0=None, ev1=None):
+        if ev0 is not None:
+            ev0.record(stream)
+        out = plan.replay()
+        if ev1 is not None:
+            ev1.record(stream)
+        postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if args.layers and rank == 0:
+        layer_table(plan)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(*evs[k])
+    torch.cuda.synchronize()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    dt_max = max_over_ranks(dt, world)
+    fwd_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    n_det = counts.cpu().tolist()
+
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    imgs_total = world * B * args.steps
+    value = imgs_total / dt_max
+    flops = plan.flops  # algorithmic conv FLOPs of one forward (all images of the batch)
+    achieved = flops / (fwd_ms * 1e-3) / 1e12
+    traffic = load_traffic(args.model, B, S, args.dtype)
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic uniform [0,255] images, seeded weights with calibrated BN (no checkpoints offline)",
+        "config": {
+            "workload": f"{args.model} {S}x{S} {args.dtype} batch={B}/GPU inference: forward (hipGraph) + "
+                        f"device NMS conf={args.conf} nms={args.nms} (BASELINE configs[1])",
+            "batch_per_gpu": B, "global_batch": B * world, "image_size": S,
+            "parallelism": f"replicas x{world} (no data-path collective)",
+            "input": f"{args.dtype} NHWC resident in HBM",
+        },
+        "roofline": {
+            "kernel": "conv_igemm (all conv launches of one forward; HIP events around each graph replay)",
+            "bound": "mfma",
+            "achieved": round(achieved, 2),
+            "peak": PEAK_BF16_TFLOPS if args.dtype != "fp32" else 157.3,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / (PEAK_BF16_TFLOPS if args.dtype != "fp32" else 157.3), 4),
+            "traffic": None if traffic is None else traffic["hbm_bytes_per_forward"],
+            "algorithmic_flops_per_launch": flops,
+            "forward_ms": round(fwd_ms, 4),
+        },
+        "detections_per_image_last_step": n_det[:4],
+    }
+    if traffic is not None:
+        result["roofline"]["traffic_source"] = traffic.get("source")
+    if not args.no_cpu_baseline and world == 1:
+        result["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+    else:
+        result["cpu_baseline"] = None
+    print(json.dumps(result))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
