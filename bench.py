@@ -187,6 +187,9 @@ def main():
     plan = model.plan_for(B, S, S, N.NHWC, dtype)
     imgs = torch.from_numpy(synthetic_images(B, S, S, seed=1000 + rank)).to(dev)
     plan.static_input().copy_(imgs.to(dtype))
+    t_tune = time.perf_counter()
+    plan.autotune(verbose=args.layers and rank == 0)
+    t_tune = time.perf_counter() - t_tune
     plan.capture()
     A = plan.anchors
     det = torch.empty(B, A, 7, dtype=torch.float32, device=dev)
@@ -261,6 +264,7 @@ def main():
             "forward_ms": round(fwd_ms, 4),
         },
         "detections_per_image_last_step": n_det[:4],
+        "autotune_s": round(t_tune, 2),
     }
     if traffic is not None:
         result["roofline"]["traffic_source"] = traffic.get("source")

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 1
+#define YXH_ABI_VERSION 2
 
 enum yxh_status {
     YXH_OK = 0,
@@ -98,6 +98,9 @@ typedef struct {
     int64_t dst_bstride;
     float decode_stride; /* level stride for DECODE acts                                */
     int32_t decode_coff; /* position of output channel 0 in the 5+C row (0 or 5)       */
+    int32_t tile;        /* 0: heuristic; else 2*id + (slabs-1), id in [1, 9]: explicit
+                            tile (TN x TM) chosen by the planner's on-device autotune     */
+    int32_t reserved;
 } yxh_conv_desc;
 
 int yxh_conv2d(const yxh_conv_desc* d, void* stream);

@@ -33,6 +33,7 @@ struct ConvParams {
     int dst_cs;
     long long dst_bs;
     int dst_f32, act, dcoff, vec_store, vec_res;
+    int vec16;  // dst rows 16-byte aligned and cout a chunk multiple: LDS-staged epilogue
     float dstride;
 };
 
@@ -64,8 +65,8 @@ template <> struct Mma<float> {
 
 // ---------------------------------------------------------------- epilogue
 template <typename T>
-__device__ __forceinline__ void store4(const ConvParams& p, float v[4], int n, int b, int pix, int ox,
-                                       int oy) {
+__device__ __forceinline__ void finish4(const ConvParams& p, float v[4], int n, int b, int pix, int ox,
+                                        int oy) {
     if (p.act >= YXH_ACT_DECODE) {
         // yolo_head.py:233-251 (eval) / :213-231 (train): fp32 output rows
 #pragma unroll
@@ -97,6 +98,13 @@ __device__ __forceinline__ void store4(const ConvParams& p, float v[4], int n, i
                 if (n + r < p.cout) v[r] += to_f32(rp[r]);
         }
     }
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(const ConvParams& p, float v[4], int n, int b, int pix, int ox,
+                                       int oy) {
+    finish4<T>(p, v, n, b, pix, ox, oy);
+    const bool full = n + 3 < p.cout;
     long long off = (long long)b * p.dst_bs + (long long)pix * p.dst_cs + n;
     if (p.dst_f32) {
         float* dp = (float*)p.dst + off;
@@ -256,7 +264,55 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvParams p) {
         __syncthreads();
     }
 
-    // epilogue: lane holds channels n..n+3 (rows 4*fq..) of pixel column frow
+    // epilogue: lane holds channels n..n+3 (rows 4*fq..) of pixel column frow.
+    // Staged form: bias/act/residual in registers, the [TM pixels][TN channels] tile of
+    // the output dtype goes through LDS, then whole pixel rows leave as 16-byte chunks
+    // (coalesced) instead of 8-byte lane-scattered stores.
+    constexpr int OES = sizeof(T);
+    constexpr int OROW = TN * OES + 16;  // +16 B: 16-byte aligned rows, <= 2-way write conflicts
+    constexpr bool CAN_STAGE = TM * OROW <= 2 * BUF && (TN * OES) % 16 == 0;
+    if (CAN_STAGE && p.vec16 && !p.dst_f32) {
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+            const int pl = wc * WTM + j * 16 + frow;
+            const int m = m0 + pl;
+            const int mm = m < p.M ? m : p.M - 1;
+            const int b = mm / p.ohw, pix = mm - b * p.ohw;
+            const int oy = pix / p.out_w, ox = pix - oy * p.out_w;
+#pragma unroll
+            for (int i = 0; i < FR; ++i) {
+                const int nl = wr * WTN + i * 16 + fq * 4;
+                const int n = n0 + nl;
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + (n + r < p.cout ? p.bias[n + r] : 0.0f);
+                if (m < p.M && n < p.cout) finish4<T>(p, v, n, b, pix, ox, oy);
+                T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
+                char* dstl = smem + pl * OROW + nl * OES;
+                if constexpr (OES == 2) {
+                    uint2 u;
+                    __builtin_memcpy(&u, t, 8);
+                    *(uint2*)dstl = u;
+                } else {
+                    uint4 u;
+                    __builtin_memcpy(&u, t, 16);
+                    *(uint4*)dstl = u;
+                }
+            }
+        }
+        __syncthreads();
+        constexpr int CPO = TN * OES / 16;  // 16-byte chunks per output row
+        const int ncols = min(TN, p.cout - n0) * OES / 16;
+        for (int q = tid; q < TM * CPO; q += 256) {
+            const int r = q / CPO, c = q - r * CPO;
+            const int m = m0 + r;
+            if (m >= p.M || c >= ncols) continue;
+            const int b = m / p.ohw, pix = m - b * p.ohw;
+            const uint4 u = *(const uint4*)(smem + r * OROW + c * 16);
+            *(uint4*)((char*)p.dst + ((long long)b * p.dst_bs + (long long)pix * p.dst_cs + n0) * OES + c * 16) = u;
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < FC; ++j) {
         const int m = m0 + wc * WTM + j * 16 + frow;
@@ -460,13 +516,38 @@ int launch_igemm(const ConvParams& p, int ks, hipStream_t st) {
     return YXH_OK;
 }
 
+// Tile configurations (id -> TN x TM, wave grid).  yxh_conv_desc.tile = id * 2 + (KS - 1)
+// selects one explicitly (the planner autotunes it per layer on the device); 0 picks
+// by a block-count heuristic.
+struct TileCfg { int tn, tm; };
+constexpr TileCfg kTiles[] = {{0, 0},     {16, 256}, {32, 256}, {32, 128}, {64, 256},
+                              {64, 128},  {64, 64},  {80, 128}, {128, 128}, {128, 64}};
+constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
+
 template <typename T>
-int dispatch_igemm(const ConvParams& p, int ks, hipStream_t st) {
-    if (p.cout <= 16) return launch_igemm<T, 16, 256, 1, 4>(p, ks, st);
-    if (p.cout <= 32) return launch_igemm<T, 32, 256, 1, 4>(p, ks, st);
-    if (p.cout <= 64) return launch_igemm<T, 64, 256, 1, 4>(p, ks, st);
-    if (p.cout <= 80) return launch_igemm<T, 80, 128, 1, 4>(p, ks, st);
-    return launch_igemm<T, 128, 128, 2, 2>(p, ks, st);
+int launch_tile(int id, const ConvParams& p, int ks, hipStream_t st) {
+    switch (id) {
+        case 1: return launch_igemm<T, 16, 256, 1, 4>(p, ks, st);
+        case 2: return launch_igemm<T, 32, 256, 1, 4>(p, ks, st);
+        case 3: return launch_igemm<T, 32, 128, 1, 4>(p, ks, st);
+        case 4: return launch_igemm<T, 64, 256, 1, 4>(p, ks, st);
+        case 5: return launch_igemm<T, 64, 128, 1, 4>(p, ks, st);
+        case 6: return launch_igemm<T, 64, 64, 2, 2>(p, ks, st);
+        case 7: return launch_igemm<T, 80, 128, 1, 4>(p, ks, st);
+        case 8: return launch_igemm<T, 128, 128, 2, 2>(p, ks, st);
+        case 9: return launch_igemm<T, 128, 64, 2, 2>(p, ks, st);
+        default: set_error("tile id %d", id); return YXH_EINVAL;
+    }
+}
+
+int heuristic_tile(const ConvParams& p) {
+    auto blocks = [&](int tn, int tm) { return (long long)((p.M + tm - 1) / tm) * ((p.cout + tn - 1) / tn); };
+    const long long target = 512;
+    if (p.cout <= 16) return 1;
+    if (p.cout <= 32) return blocks(32, 256) >= target ? 2 : 3;
+    if (p.cout <= 64) return blocks(64, 256) >= target ? 4 : blocks(64, 128) >= target ? 5 : 6;
+    if (p.cout <= 80) return 7;
+    return blocks(128, 128) >= target ? 8 : blocks(128, 64) >= target ? 9 : 6;
 }
 
 }  // namespace
@@ -541,6 +622,8 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
                       : 0;
     p.vec_res = d->residual && ((uintptr_t)d->residual % 8) == 0 && (d->res_cstride * es) % 8 == 0 &&
                 (d->res_bstride * es) % 8 == 0;
+    p.vec16 = d->dst_dtype == dt && ((uintptr_t)d->dst % 16) == 0 && (d->dst_cstride * des) % 16 == 0 &&
+              (d->dst_bstride * des) % 16 == 0 && (d->cout * des) % 16 == 0;
 
     if (dw) {
         YXH_CHECK_ARG(d->dst_dtype == dt && d->act < YXH_ACT_DECODE, "depthwise output");
@@ -556,13 +639,21 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     // K staging: two 64-byte slabs per stage when the channel structure allows it
     const int k2 = 8 * epc;
     int ks = (d->cin >= k2 && (d->nsrc == 1 || p.src0_ch % k2 == 0)) ? 2 : 1;
+    int tile = heuristic_tile(p);
+    if (d->tile > 0) {
+        tile = d->tile >> 1;
+        const int want_ks = (d->tile & 1) + 1;
+        YXH_CHECK_ARG(tile > 0 && tile < kNumTiles, "tile %d", d->tile);
+        YXH_CHECK_ARG(want_ks == 1 || ks == 2, "2-slab staging not possible for this conv");
+        ks = want_ks;
+    }
     const int kstage = 4 * ks * epc;
     YXH_CHECK_ARG(d->nsrc == 1 || p.src0_ch % kstage == 0, "src0 channels %d not a multiple of %d", p.src0_ch,
                   kstage);
     p.ncb = (d->cin + kstage - 1) / kstage;
-    if (dt == YXH_BF16) return dispatch_igemm<bf16>(p, ks, st);
-    if (dt == YXH_F16) return dispatch_igemm<f16>(p, ks, st);
-    return dispatch_igemm<float>(p, ks, st);
+    if (dt == YXH_BF16) return launch_tile<bf16>(tile, p, ks, st);
+    if (dt == YXH_F16) return launch_tile<f16>(tile, p, ks, st);
+    return launch_tile<float>(tile, p, ks, st);
 }
 
 int focus_pack_launch(const void* img, int layout, int idt, int B, int H, int W, void* dst, int odt,

@@ -212,30 +212,52 @@ __global__ __launch_bounds__(64) void pp_mask(int A, double thr, int agnostic, l
     }
 }
 
+// Greedy NMS over the sorted boxes, one wave per image, 64 boxes per step: the
+// removed-set words live in LDS; within a 64-box block the keep decisions are a
+// register-only scan over the block's diagonal mask words (one coalesced load),
+// then every kept lane ORs its own mask row into the later words (independent
+// loads across lanes) -- no dependent global load per kept box.
 __global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int* counts) {
+    __shared__ unsigned long long removed[kSortCap / 64];
     const int b = blockIdx.x, lane = threadIdx.x;
     const int n = w.cnt[b];
     if (n > w.cap) return;  // counts[b] = -1 already
     const int nw = (n + 63) / 64;
-    unsigned long long rm[4] = {0, 0, 0, 0};  // word lane + 64k
+    for (int q = lane; q < nw; q += 64) removed[q] = 0;
+    __syncthreads();
     const float* srt = w.srt + (long long)b * A * kRow;
+    const unsigned long long* mrow = w.mask + (long long)b * w.cap * w.capw;
     float* out = det + (long long)b * A * 7;
     int nk = 0;
-    for (int i = 0; i < n; ++i) {
-        const int word = i >> 6, owner = word & 63, k = word >> 6;
-        unsigned long long v = k == 0 ? rm[0] : k == 1 ? rm[1] : k == 2 ? rm[2] : rm[3];
-        unsigned int lo = __builtin_amdgcn_readlane((unsigned int)v, owner);
-        unsigned int hi = __builtin_amdgcn_readlane((unsigned int)(v >> 32), owner);
-        const unsigned long long wv = ((unsigned long long)hi << 32) | lo;
-        if ((wv >> (i & 63)) & 1ull) continue;
-        if (lane < 7) out[(long long)nk * 7 + lane] = srt[(long long)i * kRow + lane];
-        ++nk;
-        const unsigned long long* row = w.mask + ((long long)b * w.cap + i) * w.capw;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int wd = lane + 64 * q;
-            if (wd >= word && wd < nw) rm[q] |= row[wd];
+    for (int blk = 0; blk < nw; ++blk) {
+        const int row = blk * 64 + lane;
+        const int cnt = min(64, n - blk * 64);
+        const unsigned long long diag = row < n ? mrow[(long long)row * w.capw + blk] : 0ull;
+        unsigned long long cur = removed[blk];
+        unsigned long long kept = 0;
+        for (int t = 0; t < cnt; ++t) {
+            if (!((cur >> t) & 1ull)) {
+                kept |= 1ull << t;
+                const unsigned int lo = __builtin_amdgcn_readlane((unsigned int)diag, t);
+                const unsigned int hi = __builtin_amdgcn_readlane((unsigned int)(diag >> 32), t);
+                cur |= ((unsigned long long)hi << 32) | lo;
+            }
         }
+        const bool mine = (kept >> lane) & 1ull;
+        if (mine) {
+            const int pos = nk + __popcll(kept & ((1ull << lane) - 1ull));
+            const float* s = srt + (long long)row * kRow;
+            float* o = out + (long long)pos * 7;
+#pragma unroll
+            for (int c = 0; c < 7; ++c) o[c] = s[c];
+            const unsigned long long* mr = mrow + (long long)row * w.capw;
+            for (int q = blk + 1; q < nw; ++q) {
+                const unsigned long long v = mr[q];
+                if (v) atomicOr(&removed[q], v);
+            }
+        }
+        nk += __popcll(kept);
+        __syncthreads();
     }
     if (lane == 0) counts[b] = nk;
 }

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -45,7 +45,8 @@ class ConvDesc(C.Structure):
                 ("bias", C.c_void_p), ("residual", C.c_void_p), ("res_cstride", C.c_int32),
                 ("dst_dtype", C.c_int32), ("res_bstride", C.c_int64), ("dst", C.c_void_p),
                 ("dst_cstride", C.c_int32), ("act", C.c_int32), ("dst_bstride", C.c_int64),
-                ("decode_stride", C.c_float), ("decode_coff", C.c_int32)]
+                ("decode_stride", C.c_float), ("decode_coff", C.c_int32), ("tile", C.c_int32),
+                ("reserved", C.c_int32)]
 
 
 class FocusDesc(C.Structure):

@@ -130,20 +130,31 @@ class PlanCtx:
 
     def conv(self, m, srcs: list[View], out: Optional[View] = None, residual: Optional[View] = None) -> View:
         """A BaseConv (conv + BN + act) over 1-2 channel-concatenated sources."""
-        conv: nn.Conv2d = m.conv
+        return self.conv_multi([m], srcs, out=out, residual=residual)
+
+    def conv_multi(self, ms, srcs: list[View], out: Optional[View] = None,
+                   residual: Optional[View] = None) -> View:
+        """Several BaseConvs with the same input and geometry as ONE conv whose output
+        channels are the concatenation of theirs (weights stacked along cout): e.g.
+        CspLayer.conv1 | conv2 writing the whole concat buffer in one pass over x."""
+        convs = [m.conv for m in ms]
+        conv: nn.Conv2d = convs[0]
+        acts = {getattr(m, "act_name", "silu") for m in ms}
+        if len(acts) != 1 or any((c.kernel_size, c.stride, c.padding, c.groups, c.in_channels)
+                                 != (conv.kernel_size, conv.stride, conv.padding, conv.groups, conv.in_channels)
+                                 for c in convs):
+            raise ValueError("stacked convs must share geometry and activation")
+        cout = sum(c.out_channels for c in convs)
         cin = sum(s.ch for s in srcs)
         lh, lw = srcs[0].lh, srcs[0].lw
         if any(s.lh != lh or s.lw != lw for s in srcs):
             raise ValueError("concatenated sources differ in spatial size")
         groups = conv.groups
-        cin_pad = cin
         if groups == 1:
-            if conv.in_channels > cin:
-                raise ValueError(f"conv expects {conv.in_channels} channels, got {cin}")
             if conv.in_channels != cin and not (conv.in_channels == 12 and cin == 16):
                 raise ValueError(f"conv expects {conv.in_channels} channels, got {cin}")
-        elif groups != cin or conv.out_channels != cin:
-            raise NotImplementedError("only depthwise grouped convs are supported")
+        elif len(convs) > 1 or groups != cin or conv.out_channels != cin:
+            raise NotImplementedError("only single depthwise grouped convs are supported")
         kh, kw = conv.kernel_size
         sh, sw_ = conv.stride
         ph, pw = conv.padding
@@ -152,15 +163,15 @@ class PlanCtx:
         oh = (lh + 2 * ph - kh) // sh + 1
         ow = (lw + 2 * pw - kw) // sw_ + 1
         if out is None:
-            out = self.buffer(oh, ow, conv.out_channels).full()
-        if out.ch != conv.out_channels or out.lh != oh or out.lw != ow or out.up:
+            out = self.buffer(oh, ow, cout).full()
+        if out.ch != cout or out.lh != oh or out.lw != ow or out.up:
             raise ValueError("output view does not match the conv")
-        spec = self._weights([(conv, m.bn)], cin_pad if groups == 1 else 1)
+        spec = self._weights([(c, m.bn) for c, m in zip(convs, ms)], cin if groups == 1 else 1)
         self.ops.append(OpRec(N.OP_CONV, dict(
-            srcs=list(srcs), out=out, residual=residual, spec=spec, cin=cin, cout=conv.out_channels, k=kh,
+            srcs=list(srcs), out=out, residual=residual, spec=spec, cin=cin, cout=cout, k=kh,
             stride=sh, pad=ph, groups=groups, in_h=lh, in_w=lw, out_h=oh, out_w=ow,
-            act=N.ACT_CODE[getattr(m, "act_name", "silu")], dst_f32=False)))
-        self.flops += 2.0 * self.batch * oh * ow * conv.out_channels * kh * kw * (conv.in_channels // groups)
+            act=N.ACT_CODE[acts.pop()], dst_f32=False)))
+        self.flops += 2.0 * self.batch * oh * ow * cout * kh * kw * (conv.in_channels // groups)
         return out
 
     def spp(self, cat: Buffer, hidden: int) -> None:
@@ -185,6 +196,17 @@ class PlanCtx:
 class OutBuffer:
     anchors: int
     row: int  # 5 + C
+
+
+# tile ids of conv.hip (2 * id + slabs - 1); see yoloxhip.h yxh_conv_desc.tile
+TILE_CANDIDATES = [2 * i + k for i in range(1, 10) for k in (0, 1)]
+_TUNE_CACHE: dict = {}
+
+
+def _tune_key(d) -> tuple:
+    return (d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w, d.cin, d.cout, d.kh, d.stride, d.nsrc,
+            d.src[0].channels, d.src[0].upsample, d.src[1].upsample if d.nsrc > 1 else 0,
+            bool(d.residual), d.dst_dtype, d.dst_cstride == d.cout, d.act >= N.ACT_DECODE)
 
 
 class Plan:
@@ -386,6 +408,55 @@ class Plan:
                 self.lib.yxh_graph_destroy(g)
             except Exception:
                 pass
+
+    # -------------------------------------------------------------- autotune
+    def autotune(self, reps: int = 3, verbose: bool = False) -> dict:
+        """Pick each conv's tile (TN x TM, K slabs) by timing every variant on the
+        device with HIP events, on this plan's own buffers (after one real forward so
+        they hold realistic values).  Results are cached per layer shape for the
+        process.  In-place residual layers accumulate during tuning; the next forward
+        rewrites every buffer in order, so outputs are unaffected."""
+        self.pack_weights()
+        self._bind_input(self.static_input())
+        L, st = self.lib, N.stream_ptr(self.device)
+        N.check(L.yxh_run_ops(self._ops, len(self._ops), st), "forward")
+        stream = torch.cuda.current_stream(self.device)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        chosen = {}
+        for i, rec in enumerate(self.ctx.ops):
+            if rec.kind != N.OP_CONV or rec.args["groups"] != 1:
+                continue
+            op = self._ops[i]
+            key = _tune_key(op.u.conv)
+            if key in _TUNE_CACHE:
+                op.u.conv.tile = _TUNE_CACHE[key]
+                chosen[i] = _TUNE_CACHE[key]
+                continue
+            best = (float("inf"), 0)
+            ptr = C.pointer(op)
+            for tile in TILE_CANDIDATES:
+                op.u.conv.tile = tile
+                if L.yxh_run_ops(ptr, 1, st) != N.OK:  # variant not applicable
+                    continue
+                ev0.record(stream)
+                for _ in range(reps):
+                    L.yxh_run_ops(ptr, 1, st)
+                ev1.record(stream)
+                ev1.synchronize()
+                t = ev0.elapsed_time(ev1) / reps
+                if t < best[0]:
+                    best = (t, tile)
+            op.u.conv.tile = best[1]
+            _TUNE_CACHE[key] = best[1]
+            chosen[i] = best[1]
+            if verbose:
+                a = rec.args
+                print(f"tune op {i}: k{a['k']}s{a['stride']} {a['cin']}->{a['cout']} @{a['out_h']}x{a['out_w']}"
+                      f" -> tile {best[1] >> 1} slabs {(best[1] & 1) + 1} {best[0] * 1e3:.1f} us")
+        torch.cuda.synchronize(self.device)
+        if self._graph is not None:  # a captured graph holds the old tiles
+            self.capture()
+        return chosen
 
     # -------------------------------------------------------------- reporting
     def conv_ops(self):

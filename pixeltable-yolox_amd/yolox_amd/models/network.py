@@ -115,8 +115,8 @@ class CspLayer(_Planned):
         hidden = self.conv1.conv.out_channels
         cat = ctx.buffer(srcs[0].lh, srcs[0].lw, 2 * hidden)
         x1 = cat.slice(0, hidden)
-        self.conv1.plan(ctx, srcs, out=x1)
-        self.conv2.plan(ctx, srcs, out=cat.slice(hidden, hidden))
+        # conv1 | conv2 read the same input: one conv writes the whole [x_1 | x_2]
+        ctx.conv_multi([self.conv1, self.conv2], srcs, out=cat.full())
         for b in self.m:
             b.plan(ctx, x1, out=x1)
         return self.conv3.plan(ctx, [cat.full()], out=out)
@@ -245,8 +245,16 @@ class YoloxHead(_Planned):
         a_off = 0
         for k, x in enumerate(feats):
             s = self.stems[k].plan(ctx, [x])
-            c = self.cls_convs[k][1].plan(ctx, [self.cls_convs[k][0].plan(ctx, [s])])
-            r = self.reg_convs[k][1].plan(ctx, [self.reg_convs[k][0].plan(ctx, [s])])
+            c0, r0 = self.cls_convs[k][0], self.reg_convs[k][0]
+            if isinstance(c0, BaseConv) and isinstance(r0, BaseConv):
+                # both branch heads read the stem output: one conv writes [cls | reg]
+                hw_ = c0.conv.out_channels
+                cr = ctx.conv_multi([c0, r0], [s])
+                c, r = cr.buf.slice(0, hw_), cr.buf.slice(hw_, hw_)
+            else:
+                c, r = c0.plan(ctx, [s]), r0.plan(ctx, [s])
+            c = self.cls_convs[k][1].plan(ctx, [c])
+            r = self.reg_convs[k][1].plan(ctx, [r])
             ctx.head_preds(k, self, c, r, out, a_off, self.strides[k], train)
             a_off += x.lh * x.lw
         return out

@@ -93,3 +93,18 @@ def test_batch_size_640_shapes_and_determinism():
     b = m(x)
     assert a.shape == (2, 8400, 85) and torch.isfinite(a).all()
     assert torch.equal(a, b)
+
+
+def test_autotuned_plan_matches_default(golden):
+    """Tile choice changes only speed: the autotuned plan gives the same fp32 output
+    (up to summation-order rounding) as the heuristic one."""
+    from yolox_amd import _native as N
+    d = golden("fwd_yolox_s_128.npz")
+    m = model("yolox_s")
+    x = torch.from_numpy(d["input_u8"]).cuda()
+    plan = m.plan_for(2, 128, 128, N.NHWC, torch.uint8)
+    a = plan.run(x).clone()
+    plan.static_input().copy_(x)
+    plan.autotune(reps=1)
+    b = plan.run(x).clone()
+    assert torch.allclose(a, b, rtol=1e-4, atol=1e-4)

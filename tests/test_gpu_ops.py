@@ -74,7 +74,7 @@ def ref_conv(x, conv, bn, act):
     return {"silu": F.silu, "relu": F.relu, "lrelu": lambda t: F.leaky_relu(t, 0.1), "none": lambda t: t}[act](y)
 
 
-def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_coff=0, out_c=None):
+def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_coff=0, out_c=None, tile=0):
     """srcs: list of (nhwc tensor [B,h,w,C], coff, ch, upsample)."""
     n = N()
     B = srcs[0][0].shape[0]
@@ -105,6 +105,7 @@ def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_cof
     d.dst_dtype = n.DTYPE_CODE[out.dtype]
     d.dst_cstride, d.dst_bstride = out.shape[3], out.shape[1] * out.shape[2] * out.shape[3]
     d.act = n.ACT_CODE[act]
+    d.tile = tile
     n.check(n.lib().yxh_conv2d(ctypes.byref(d), n.stream_ptr()), "conv2d")
     torch.cuda.synchronize()
     return out
@@ -248,3 +249,27 @@ def test_letterbox_resize_cases():
     fl = F.interpolate(torch.from_numpy(b).permute(2, 0, 1)[None].float(), size=(rh, rw), mode="bilinear",
                        align_corners=False)[0].numpy()
     assert np.abs(out[:, :rh, :rw] - fl).max() <= 1.01
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_every_tile_variant(dtype):
+    """All tile configurations x K-slab counts the autotuner may pick agree."""
+    conv, bn = make_conv(64, 96, 3, 1, seed=21)
+    x = torch.randn(2, 64, 11, 13, generator=torch.Generator().manual_seed(2))
+    want = ref_conv(x, conv, bn, "silu")
+    X = nhwc(x, dtype)
+    for tid in range(1, 10):
+        for ks in (1, 2):
+            y = run_conv([(X, 0, 64, 0)], conv, bn, dtype, tile=2 * tid + ks - 1)
+            close(y.permute(0, 3, 1, 2), want, dtype)
+
+
+def test_tile_variant_rejected_when_inapplicable():
+    n = N()
+    conv, bn = make_conv(16, 32, 3, 1, seed=1)
+    x = torch.randn(1, 16, 8, 8)
+    with pytest.raises(ValueError, match="2-slab"):
+        run_conv([(nhwc(x, torch.bfloat16), 0, 16, 0)], conv, bn, torch.bfloat16, tile=2 * 2 + 1)
+    with pytest.raises(ValueError, match="tile"):
+        run_conv([(nhwc(x, torch.bfloat16), 0, 16, 0)], conv, bn, torch.bfloat16, tile=2 * 12)
+    assert n is not None
