@@ -16,6 +16,7 @@ hipGraph (``capture()`` / ``replay()``).
 from __future__ import annotations
 
 import ctypes as C
+import sys
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -452,7 +453,7 @@ class Plan:
             if verbose:
                 a = rec.args
                 print(f"tune op {i}: k{a['k']}s{a['stride']} {a['cin']}->{a['cout']} @{a['out_h']}x{a['out_w']}"
-                      f" -> tile {best[1] >> 1} slabs {(best[1] & 1) + 1} {best[0] * 1e3:.1f} us")
+                      f" -> tile {best[1] >> 1} slabs {(best[1] & 1) + 1} {best[0] * 1e3:.1f} us", file=sys.stderr)
         torch.cuda.synchronize(self.device)
         if self._graph is not None:  # a captured graph holds the old tiles
             self.capture()
