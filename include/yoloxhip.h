@@ -98,8 +98,10 @@ typedef struct {
     int64_t dst_bstride;
     float decode_stride; /* level stride for DECODE acts                                */
     int32_t decode_coff; /* position of output channel 0 in the 5+C row (0 or 5)       */
-    int32_t tile;        /* 0: heuristic; else 2*id + (slabs-1), id in [1, 9]: explicit
-                            tile (TN x TM) chosen by the planner's on-device autotune     */
+    int32_t tile;        /* 0: heuristic; else 2*id + (slabs-1): id 1-9 explicit tile
+                            (TN x TM) of the register-staged kernel, id 17-25 the same
+                            tiles on the LDS-DMA kernel; chosen by the planner's
+                            on-device autotune                                           */
     int32_t reserved;
 } yxh_conv_desc;
 
@@ -159,6 +161,24 @@ int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_cla
                     float conf_thre, double nms_thre, int32_t class_agnostic,
                     int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,
                     size_t workspace_bytes, void* stream);
+
+/*
+ * yxh_yolox_loss: YoloxHead.get_losses (yolo_head.py:253-411) with SimOTA assignment
+ * (get_assignments :420-509, get_geometry_constraint :511-540, simota_matching
+ * :542-574) and IouLoss (losses.py:13-51) for the whole batch, no host sync.
+ *   preds   [B, A, 5+C] fp32 train-mode head output: decoded cx,cy,w,h, raw obj/cls logits
+ *   origin  [B, A, 4] raw reg outputs for the L1 loss, or NULL (use_l1 = False)
+ *   labels  [B, L, 5] (cls, cx, cy, w, h), zero rows after the GTs
+ *   level_hw [nlev][2], strides [nlev]: anchor grid (anchors level-major, row-major)
+ *   out: fg_mask [B, A] u8, matched_gt [B, A] int32 (-1 = background), pred_iou [B, A],
+ *        num_fg [B] int32, losses[6] = total, 5*iou, obj, cls, l1, num_fg/max(num_gts,1)
+ */
+size_t yxh_yolox_loss_workspace_bytes(int32_t batch, int32_t anchors, int32_t max_labels);
+int yxh_yolox_loss(const float* preds, const float* origin, const float* labels, int32_t batch,
+                   int32_t anchors, int32_t num_classes, int32_t max_labels, const int32_t* level_hw,
+                   const int32_t* strides, int32_t nlevels, uint8_t* fg_mask, int32_t* matched_gt,
+                   float* pred_iou, int32_t* num_fg, float* losses, void* workspace,
+                   size_t workspace_bytes, void* stream);
 
 /*
  * Plan execution.  A forward pass is a fixed list of ops (built once per model and

@@ -296,6 +296,24 @@ def simota_assign(gt_boxes: Tensor, gt_classes: Tensor, pred_boxes: Tensor, cls_
 
 
 # ----------------------------------------------------------------- training
+def train_outputs(sd: SD, arch: Arch, x: Tensor):
+    """Train-mode head outputs (yolo_head.py:161-182, get_output_and_grid :213-231):
+    (outputs [B, A, 5+C] with decoded boxes and raw logits, origin reg [B, A, 4],
+    level sizes [(h, w)])."""
+    levels = head_raw(sd, arch, backbone(sd, arch, x, bn_train=True), bn_train=True)
+    C = arch.num_classes
+    outs, origin, hw = [], [], []
+    for (reg, obj, cls), s in zip(levels, (8, 16, 32)):
+        B, _, h, w = reg.shape
+        o = torch.cat([reg, obj, cls], 1).permute(0, 2, 3, 1).reshape(B, h * w, 5 + C)
+        gx, gy, _ = anchors_for([(h, w)], (s,))
+        grid = torch.stack([gx, gy], 1)[None]
+        outs.append(torch.cat([(o[..., :2] + grid) * s, torch.exp(o[..., 2:4]) * s, o[..., 4:]], -1))
+        origin.append(reg.permute(0, 2, 3, 1).reshape(B, h * w, 4))
+        hw.append((h, w))
+    return torch.cat(outs, 1), torch.cat(origin, 1), hw
+
+
 def forward_train(sd: SD, arch: Arch, x: Tensor, labels: Tensor, use_l1: bool = False):
     """YoloxModule.forward in train mode -> loss dict (yolox.py:76-87, yolo_head.py:161-411).
 

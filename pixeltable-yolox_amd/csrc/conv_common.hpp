@@ -1,0 +1,201 @@
+// Pieces shared by the conv kernels (conv.hip, conv_glds.hip).
+#pragma once
+
+#include "yxh_common.hpp"
+
+namespace yxh {
+
+struct ConvParams {
+    int in_h, in_w, out_h, out_w, cin, cout, kw, stride, pad;
+    int M, ohw, taps, ncb, nsrc, src0_ch;
+    const void* sptr[2];
+    int scs[2], sw[2], sup[2];
+    long long sbs[2];
+    const void* w;
+    const float* bias;
+    const void* res;
+    int res_cs;
+    long long res_bs;
+    void* dst;
+    int dst_cs;
+    long long dst_bs;
+    int dst_f32, act, dcoff, vec_store, vec_res;
+    int vec16;  // dst rows 16-byte aligned and cout a chunk multiple: LDS-staged epilogue
+    float dstride;
+};
+
+// ---------------------------------------------------------------- MFMA step
+// One 64-byte K slab: lane l holds row (l & 15), 16-byte chunk (l >> 4) of both
+// operands.  bf16/f16: a single 16x16x32 MFMA.  f32: four 16x16x4 MFMAs; step e
+// takes element e of every chunk, i.e. K is permuted identically for A and B.
+template <typename T> struct Mma;
+template <> struct Mma<bf16> {
+    static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                      __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+    }
+};
+template <> struct Mma<f16> {
+    static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                     __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
+    }
+};
+template <> struct Mma<float> {
+    static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+    }
+};
+
+// ---------------------------------------------------------------- epilogue
+template <typename T>
+__device__ __forceinline__ void finish4(const ConvParams& p, float v[4], int n, int b, int pix, int ox,
+                                        int oy) {
+    if (p.act >= YXH_ACT_DECODE) {
+        // yolo_head.py:233-251 (eval) / :213-231 (train): fp32 output rows
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            int ch = p.dcoff + n + r;
+            if (ch < 2)
+                v[r] = (v[r] + (float)(ch == 0 ? ox : oy)) * p.dstride;
+            else if (ch < 4)
+                v[r] = expf(v[r]) * p.dstride;
+            else if (p.act == YXH_ACT_DECODE)
+                v[r] = 1.0f / (1.0f + expf(-v[r]));
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = apply_act<sizeof(T) == 4>(v[r], p.act);
+    }
+    const bool full = n + 3 < p.cout;
+    if (p.res) {
+        const T* rp = (const T*)p.res + (long long)b * p.res_bs + (long long)pix * p.res_cs + n;
+        if (full && p.vec_res && sizeof(T) == 2) {
+            uint2 u = *(const uint2*)rp;
+            T t[4];
+            __builtin_memcpy(t, &u, 8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += to_f32(t[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (n + r < p.cout) v[r] += to_f32(rp[r]);
+        }
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(const ConvParams& p, float v[4], int n, int b, int pix, int ox,
+                                       int oy) {
+    finish4<T>(p, v, n, b, pix, ox, oy);
+    const bool full = n + 3 < p.cout;
+    long long off = (long long)b * p.dst_bs + (long long)pix * p.dst_cs + n;
+    if (p.dst_f32) {
+        float* dp = (float*)p.dst + off;
+        if (full && p.vec_store) {
+            *(float4*)dp = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (n + r < p.cout) dp[r] = v[r];
+        }
+    } else {
+        T* dp = (T*)p.dst + off;
+        if (full && p.vec_store && sizeof(T) == 2) {
+            T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
+            uint2 u;
+            __builtin_memcpy(&u, t, 8);
+            *(uint2*)dp = u;
+        } else if (full && p.vec_store) {
+            *(float4*)dp = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (n + r < p.cout) dp[r] = from_f32<T>(v[r]);
+        }
+    }
+}
+
+// Epilogue shared by the conv kernels: lane holds channels n..n+3 (rows 4*fq..) of
+// pixel column frow for every (i, j) fragment.  Staged form: bias/act/residual in
+// registers, the [TM pixels][TN channels] tile of the output dtype goes through LDS,
+// then whole pixel rows leave as 16-byte chunks (coalesced) instead of 8-byte
+// lane-scattered stores.  Caller guarantees all LDS reads of the K loop are done.
+template <typename T, int TN, int TM, int WR, int WC, int SMEM_BYTES>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TN / WR / 16][TM / WC / 16],
+                                              char* smem, int m0, int n0) {
+    constexpr int WTN = TN / WR, WTM = TM / WC;
+    constexpr int FR = WTN / 16, FC = WTM / 16;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / WC, wc = wave % WC;
+    const int frow = lane & 15, fq = lane >> 4;
+    constexpr int OES = sizeof(T);
+    constexpr int OROW = TN * OES + 16;  // +16 B: 16-byte aligned rows, <= 2-way write conflicts
+    constexpr bool CAN_STAGE = TM * OROW <= SMEM_BYTES && (TN * OES) % 16 == 0;
+    if (CAN_STAGE && p.vec16 && !p.dst_f32) {
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+            const int pl = wc * WTM + j * 16 + frow;
+            const int m = m0 + pl;
+            const int mm = m < p.M ? m : p.M - 1;
+            const int b = mm / p.ohw, pix = mm - b * p.ohw;
+            const int oy = pix / p.out_w, ox = pix - oy * p.out_w;
+#pragma unroll
+            for (int i = 0; i < FR; ++i) {
+                const int nl = wr * WTN + i * 16 + fq * 4;
+                const int n = n0 + nl;
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + (n + r < p.cout ? p.bias[n + r] : 0.0f);
+                if (m < p.M && n < p.cout) finish4<T>(p, v, n, b, pix, ox, oy);
+                T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
+                char* dstl = smem + pl * OROW + nl * OES;
+                if constexpr (OES == 2) {
+                    uint2 u;
+                    __builtin_memcpy(&u, t, 8);
+                    *(uint2*)dstl = u;
+                } else {
+                    uint4 u;
+                    __builtin_memcpy(&u, t, 16);
+                    *(uint4*)dstl = u;
+                }
+            }
+        }
+        __syncthreads();
+        constexpr int CPO = TN * OES / 16;  // 16-byte chunks per output row
+        const int ncols = min(TN, p.cout - n0) * OES / 16;
+        for (int q = tid; q < TM * CPO; q += 256) {
+            const int r = q / CPO, c = q - r * CPO;
+            const int m = m0 + r;
+            if (m >= p.M || c >= ncols) continue;
+            const int b = m / p.ohw, pix = m - b * p.ohw;
+            const uint4 u = *(const uint4*)(smem + r * OROW + c * 16);
+            *(uint4*)((char*)p.dst + ((long long)b * p.dst_bs + (long long)pix * p.dst_cs + n0) * OES + c * 16) = u;
+        }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < FC; ++j) {
+        const int m = m0 + wc * WTM + j * 16 + frow;
+        if (m >= p.M) continue;
+        const int b = m / p.ohw, pix = m - b * p.ohw;
+        const int oy = pix / p.out_w, ox = pix - oy * p.out_w;
+#pragma unroll
+        for (int i = 0; i < FR; ++i) {
+            const int n = n0 + wr * WTN + i * 16 + fq * 4;
+            if (n >= p.cout) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + (n + r < p.cout ? p.bias[n + r] : 0.0f);
+            store4<T>(p, v, n, b, pix, ox, oy);
+        }
+    }
+}
+
+// LDS-DMA variant (conv_glds.hip); id as in conv.hip's tile table
+int conv_glds_dispatch(int dtype, int id, const ConvParams& p, int ks, hipStream_t st);
+
+}  // namespace yxh

@@ -31,6 +31,10 @@ int fold_launch(const float* w, const float* cb, const float* g, const float* be
                 const float* var, float eps, int cout, int cin_g, int kh, int kw, int cin_pad, int dt, void* wo,
                 float* bo, hipStream_t st);
 size_t pp_workspace(int B, int A);
+size_t sim_workspace(int B, int A, int L);
+int yolox_loss(const float* preds, const float* origin, const float* labels, int B, int A, int C, int L,
+               const int* lhw, const int* strides, int nlev, uint8_t* fg, int* matched, float* piou, int* num_fg,
+               float* losses, void* ws, size_t ws_bytes, hipStream_t st);
 int letterbox_launch(const uint8_t* src, int sh, int sw, int th, int tw, int out_nchw, void* dst, hipStream_t st);
 int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
                 float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st);
@@ -95,6 +99,18 @@ int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_cla
                     void* workspace, size_t workspace_bytes, void* stream) {
     return postprocess(pred, batch, anchors, num_classes, conf_thre, nms_thre, class_agnostic, vanilla_numel, det,
                        counts, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+size_t yxh_yolox_loss_workspace_bytes(int32_t batch, int32_t anchors, int32_t max_labels) {
+    return sim_workspace(batch, anchors, max_labels);
+}
+
+int yxh_yolox_loss(const float* preds, const float* origin, const float* labels, int32_t batch, int32_t anchors,
+                   int32_t num_classes, int32_t max_labels, const int32_t* level_hw, const int32_t* strides,
+                   int32_t nlevels, uint8_t* fg_mask, int32_t* matched_gt, float* pred_iou, int32_t* num_fg,
+                   float* losses, void* workspace, size_t workspace_bytes, void* stream) {
+    return yolox_loss(preds, origin, labels, batch, anchors, num_classes, max_labels, level_hw, strides, nlevels,
+                      fg_mask, matched_gt, pred_iou, num_fg, losses, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 int yxh_run_ops(const yxh_op* ops, int32_t n, void* stream) {

@@ -103,6 +103,9 @@ def lib():
             "yxh_letterbox": ([vp, i32, i32, i32, i32, i32, vp, vp], C.c_int),
             "yxh_postprocess_workspace_bytes": ([i32, i32], sz),
             "yxh_postprocess": ([vp, i32, i32, i32, f32, f64, i32, i64, vp, vp, vp, sz, vp], C.c_int),
+            "yxh_yolox_loss_workspace_bytes": ([i32, i32, i32], sz),
+            "yxh_yolox_loss": ([vp, vp, vp, i32, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, sz, vp],
+                               C.c_int),
             "yxh_run_ops": ([C.POINTER(Op), i32, vp], C.c_int),
             "yxh_graph_create": ([C.POINTER(Op), i32, vp, C.POINTER(vp)], C.c_int),
             "yxh_graph_launch": ([vp, vp], C.c_int),
@@ -122,7 +125,7 @@ def lib():
 
 EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d",
             "yxh_focus_pack", "yxh_spp_maxpool", "yxh_fold_bn_pack", "yxh_letterbox", "yxh_postprocess_workspace_bytes",
-            "yxh_postprocess", "yxh_run_ops", "yxh_graph_create", "yxh_graph_launch", "yxh_graph_destroy"]
+            "yxh_postprocess", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_launch", "yxh_graph_destroy"]
 
 
 def check(rc: int, what: str = "") -> None:

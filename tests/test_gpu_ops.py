@@ -253,12 +253,13 @@ def test_letterbox_resize_cases():
 
 @pytest.mark.parametrize("dtype", DTYPES)
 def test_every_tile_variant(dtype):
-    """All tile configurations x K-slab counts the autotuner may pick agree."""
+    """All tile configurations x K-slab counts x both kernels (register-staged and
+    LDS-DMA) the autotuner may pick agree."""
     conv, bn = make_conv(64, 96, 3, 1, seed=21)
     x = torch.randn(2, 64, 11, 13, generator=torch.Generator().manual_seed(2))
     want = ref_conv(x, conv, bn, "silu")
     X = nhwc(x, dtype)
-    for tid in range(1, 10):
+    for tid in list(range(1, 10)) + list(range(17, 26)):
         for ks in (1, 2):
             y = run_conv([(X, 0, 64, 0)], conv, bn, dtype, tile=2 * tid + ks - 1)
             close(y.permute(0, 3, 1, 2), want, dtype)
