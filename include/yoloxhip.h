@@ -118,6 +118,29 @@ int yxh_focus_pack(const void* img, int32_t layout, int32_t img_dtype, int32_t b
                    int32_t w, void* dst, int32_t dst_dtype, void* stream);
 
 /*
+ * yxh_stem_conv: Focus + stem BaseConv fused (network_blocks.py:186-208,
+ * darknet.py:112): the 3x3 conv on the 12 space-to-depth channels evaluated as the
+ * equivalent 6x6 stride-2 pad-2 conv straight from the image (NCHW float32 or NHWC
+ * uint8/bf16/f16/f32), BN folded, activation, NHWC output [B, h/2, w/2, cout].
+ * weight/bias come from yxh_stem_pack ([round16(cout)][6][32] of `dtype`).
+ */
+typedef struct {
+    const void* img;
+    int32_t layout, img_dtype, batch, h, w;
+    int32_t dtype, cout, act;
+    const void* weight;
+    const float* bias;
+    void* dst;
+    int32_t dst_cstride;
+    int32_t reserved;
+    int64_t dst_bstride;
+} yxh_stem_desc;
+int yxh_stem_conv(const yxh_stem_desc* d, void* stream);
+int yxh_stem_pack(const float* conv_w, const float* bn_gamma, const float* bn_beta, const float* bn_mean,
+                  const float* bn_var, float eps, int32_t cout, int32_t dtype, void* w_out, float* b_out,
+                  void* stream);
+
+/*
  * yxh_spp_maxpool: SPPBottleneck pools (network_blocks.py:129-141): reads channels
  * [0, c) of an NHWC buffer and writes max_pool(k, stride 1, pad k/2) for k = 5, 9,
  * 13 into channels [c, 2c), [2c, 3c), [3c, 4c) of the same buffer.
@@ -186,7 +209,7 @@ int yxh_yolox_loss(const float* preds, const float* origin, const float* labels,
  * captured once into a hipGraph and replayed (the MI355X replacement for the
  * reference's eager per-module dispatch).
  */
-enum yxh_op_kind { YXH_OP_CONV = 0, YXH_OP_FOCUS = 1, YXH_OP_SPP = 2 };
+enum yxh_op_kind { YXH_OP_CONV = 0, YXH_OP_FOCUS = 1, YXH_OP_SPP = 2, YXH_OP_STEM = 3 };
 typedef struct {
     const void* img;
     int32_t layout, img_dtype, batch, h, w, dst_dtype;
@@ -204,6 +227,7 @@ typedef struct {
         yxh_conv_desc conv;
         yxh_focus_desc focus;
         yxh_spp_desc spp;
+        yxh_stem_desc stem;
     } u;
 } yxh_op;
 

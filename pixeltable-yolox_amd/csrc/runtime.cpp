@@ -30,6 +30,9 @@ int spp_launch(void* buf, int dt, int B, int H, int W, int C, int cs, long long 
 int fold_launch(const float* w, const float* cb, const float* g, const float* beta, const float* mean,
                 const float* var, float eps, int cout, int cin_g, int kh, int kw, int cin_pad, int dt, void* wo,
                 float* bo, hipStream_t st);
+int stem_launch(const yxh_stem_desc* d, hipStream_t st);
+int stem_pack_launch(const float* w, const float* g, const float* beta, const float* mean, const float* var,
+                     float eps, int cout, int dt, void* wo, float* bo, hipStream_t st);
 size_t pp_workspace(int B, int A);
 size_t sim_workspace(int B, int A, int L);
 int yolox_loss(const float* preds, const float* origin, const float* labels, int B, int A, int C, int L,
@@ -47,6 +50,8 @@ static int run_op(const yxh_op& op, hipStream_t st) {
             const yxh_focus_desc& f = op.u.focus;
             return focus_pack_launch(f.img, f.layout, f.img_dtype, f.batch, f.h, f.w, f.dst, f.dst_dtype, st);
         }
+        case YXH_OP_STEM:
+            return stem_launch(&op.u.stem, st);
         case YXH_OP_SPP: {
             const yxh_spp_desc& s = op.u.spp;
             return spp_launch(s.buf, s.dtype, s.batch, s.h, s.w, s.c, s.cstride, s.bstride, st);
@@ -73,6 +78,15 @@ int yxh_conv2d(const yxh_conv_desc* d, void* stream) { return conv2d(d, (hipStre
 int yxh_focus_pack(const void* img, int32_t layout, int32_t img_dtype, int32_t batch, int32_t h, int32_t w,
                    void* dst, int32_t dst_dtype, void* stream) {
     return focus_pack_launch(img, layout, img_dtype, batch, h, w, dst, dst_dtype, (hipStream_t)stream);
+}
+
+int yxh_stem_conv(const yxh_stem_desc* d, void* stream) { return stem_launch(d, (hipStream_t)stream); }
+
+int yxh_stem_pack(const float* conv_w, const float* bn_gamma, const float* bn_beta, const float* bn_mean,
+                  const float* bn_var, float eps, int32_t cout, int32_t dtype, void* w_out, float* b_out,
+                  void* stream) {
+    return stem_pack_launch(conv_w, bn_gamma, bn_beta, bn_mean, bn_var, eps, cout, dtype, w_out, b_out,
+                            (hipStream_t)stream);
 }
 
 int yxh_spp_maxpool(void* buf, int32_t dtype, int32_t batch, int32_t h, int32_t w, int32_t c, int32_t cstride,

@@ -24,7 +24,7 @@ OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
 F32, BF16, F16, U8 = 0, 1, 2, 3
 ACT_NONE, ACT_SILU, ACT_RELU, ACT_LRELU, ACT_DECODE, ACT_DECODE_TRAIN = range(6)
 NCHW, NHWC = 0, 1
-OP_CONV, OP_FOCUS, OP_SPP = 0, 1, 2
+OP_CONV, OP_FOCUS, OP_SPP, OP_STEM = 0, 1, 2, 3
 
 TORCH_DTYPE = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16, U8: torch.uint8}
 DTYPE_CODE = {v: k for k, v in TORCH_DTYPE.items()}
@@ -59,8 +59,15 @@ class SppDesc(C.Structure):
                 ("w", C.c_int32), ("c", C.c_int32), ("cstride", C.c_int32), ("bstride", C.c_int64)]
 
 
+class StemDesc(C.Structure):
+    _fields_ = [("img", C.c_void_p), ("layout", C.c_int32), ("img_dtype", C.c_int32), ("batch", C.c_int32),
+                ("h", C.c_int32), ("w", C.c_int32), ("dtype", C.c_int32), ("cout", C.c_int32), ("act", C.c_int32),
+                ("weight", C.c_void_p), ("bias", C.c_void_p), ("dst", C.c_void_p), ("dst_cstride", C.c_int32),
+                ("reserved", C.c_int32), ("dst_bstride", C.c_int64)]
+
+
 class _OpU(C.Union):
-    _fields_ = [("conv", ConvDesc), ("focus", FocusDesc), ("spp", SppDesc)]
+    _fields_ = [("conv", ConvDesc), ("focus", FocusDesc), ("spp", SppDesc), ("stem", StemDesc)]
 
 
 class Op(C.Structure):
@@ -98,6 +105,8 @@ def lib():
             "yxh_conv2d": ([C.POINTER(ConvDesc), vp], C.c_int),
             "yxh_focus_pack": ([vp, i32, i32, i32, i32, i32, vp, i32, vp], C.c_int),
             "yxh_spp_maxpool": ([vp, i32, i32, i32, i32, i32, i32, i64, vp], C.c_int),
+            "yxh_stem_conv": ([C.POINTER(StemDesc), vp], C.c_int),
+            "yxh_stem_pack": ([vp, vp, vp, vp, vp, f32, i32, i32, vp, vp, vp], C.c_int),
             "yxh_fold_bn_pack": ([vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, i32, vp, vp, vp],
                                  C.c_int),
             "yxh_letterbox": ([vp, i32, i32, i32, i32, i32, vp, vp], C.c_int),
@@ -124,7 +133,7 @@ def lib():
 
 
 EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d",
-            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_fold_bn_pack", "yxh_letterbox", "yxh_postprocess_workspace_bytes",
+            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox", "yxh_postprocess_workspace_bytes",
             "yxh_postprocess", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_launch", "yxh_graph_destroy"]
 
 

@@ -83,8 +83,16 @@ class WeightSpec:
     kh: int
     kw: int
     cin_pad: int
+    stem: bool = False  # fused Focus+stem layout [round16(cout)][6][32] (yxh_stem_pack)
     w_off: int = -1  # bytes into weight arena
     b_off: int = -1  # bytes into bias arena
+
+
+@dataclass(eq=False)
+class ImageRef:
+    """The plan's input image (bound at run time): what Focus plans from."""
+    h: int
+    w: int
 
 
 @dataclass(eq=False)
@@ -94,7 +102,7 @@ class OpRec:
 
 
 class PlanCtx:
-    def __init__(self, batch: int, dtype: torch.dtype, device: torch.device):
+    def __init__(self, batch: int, dtype: torch.dtype, device: torch.device, fuse_stem: bool = True):
         if dtype not in (torch.float32, torch.bfloat16, torch.float16):
             raise ValueError(f"compute dtype {dtype} not supported (float32, bfloat16, float16)")
         self.batch = batch
@@ -103,6 +111,7 @@ class PlanCtx:
         self.esize = torch.empty((), dtype=dtype).element_size()
         self.epc = 16 // self.esize
         self.device = device
+        self.fuse_stem = fuse_stem
         self.buffers: list[Buffer] = []
         self.weights: list[WeightSpec] = []
         self.ops: list[OpRec] = []
@@ -117,6 +126,26 @@ class PlanCtx:
         return b
 
     # ---------------------------------------------------------------- ops
+    def image(self, h: int, w: int) -> ImageRef:
+        return ImageRef(h, w)
+
+    def stem_fusable(self, m) -> bool:
+        c = m.conv
+        return (self.fuse_stem and c.in_channels == 12 and c.groups == 1 and c.kernel_size == (3, 3)
+                and c.stride == (1, 1) and c.padding == (1, 1) and c.out_channels <= 80
+                and (c.out_channels * self.esize) % 16 == 0)
+
+    def stem(self, m, img: ImageRef) -> View:
+        """Focus + its BaseConv (3x3 s1 on 12 channels) as one 6x6 s2 conv on the image."""
+        conv = m.conv
+        out = self.buffer(img.h // 2, img.w // 2, conv.out_channels)
+        spec = WeightSpec([(conv, m.bn)], conv.out_channels, 12, 3, 3, 12, stem=True)
+        self.weights.append(spec)
+        self.ops.append(OpRec(N.OP_STEM, dict(dst=out.full(), h=img.h, w=img.w, spec=spec,
+                                              act=N.ACT_CODE[getattr(m, "act_name", "silu")])))
+        self.flops += 2.0 * self.batch * out.h * out.w * conv.out_channels * 9 * 12
+        return out.full()
+
     def focus(self, h: int, w: int) -> View:
         packed = self.buffer(h // 2, w // 2, 16)
         self.ops.append(OpRec(N.OP_FOCUS, dict(dst=packed.full(), h=h, w=w)))
@@ -215,7 +244,8 @@ class Plan:
     """A finalised op list with its arenas.  ``run(x)`` executes one forward pass."""
 
     def __init__(self, model, batch: int, height: int, width: int, dtype: torch.dtype, device,
-                 input_layout: int = N.NCHW, input_dtype: torch.dtype = torch.float32, train: bool = False):
+                 input_layout: int = N.NCHW, input_dtype: torch.dtype = torch.float32, train: bool = False,
+                 fuse_stem: bool = True):
         if height % 32 or width % 32:
             raise ValueError("input size must be multiples of 32")
         self.lib = N.lib()
@@ -226,9 +256,8 @@ class Plan:
         self.dtype = dtype
         head = model.head
         self.num_classes = head.num_classes
-        ctx = PlanCtx(batch, dtype, self.device)
-        packed = ctx.focus(height, width)
-        feats = model.backbone.plan(ctx, packed)
+        ctx = PlanCtx(batch, dtype, self.device, fuse_stem=fuse_stem)
+        feats = model.backbone.plan(ctx, ctx.image(height, width))
         anchors = sum(f.lh * f.lw for f in feats)
         self.out_spec = OutBuffer(anchors, 5 + self.num_classes)
         head.plan(ctx, feats, self.out_spec, train=train)
@@ -245,15 +274,20 @@ class Plan:
         woff = boff = 0
         for s in ctx.weights:
             s.w_off = woff
-            woff += _align(s.cout * s.kh * s.kw * s.cin_pad * ctx.esize)
             s.b_off = boff
-            boff += _align(s.cout * 4)
+            if s.stem:
+                cpad = (s.cout + 15) // 16 * 16
+                woff += _align(cpad * 6 * 32 * ctx.esize)
+                boff += _align(cpad * 4)
+            else:
+                woff += _align(s.cout * s.kh * s.kw * s.cin_pad * ctx.esize)
+                boff += _align(s.cout * 4)
         self.warena = torch.empty(max(woff, 1), dtype=torch.uint8, device=self.device)
         self.barena = torch.empty(max(boff, 1), dtype=torch.uint8, device=self.device)
         self.output = torch.empty(batch, anchors, 5 + self.num_classes, dtype=torch.float32, device=self.device)
         self._input_slot: Optional[torch.Tensor] = None
         self._ops = (N.Op * len(ctx.ops))()
-        self._focus_index = None
+        self._input_index = None
         self._graph = None
         self._graph_ptrs = None
         self._param_sig = None
@@ -278,7 +312,20 @@ class Plan:
                 f.dst_dtype = ctx.dcode
                 f.dst = self._ptr(a["dst"])
                 f.img = None
-                self._focus_index = i
+                self._input_index = i
+            elif rec.kind == N.OP_STEM:
+                t = op.u.stem
+                t.layout = self.input_layout
+                t.img_dtype = N.DTYPE_CODE[self.input_dtype]
+                t.batch, t.h, t.w = B, a["h"], a["w"]
+                t.dtype, t.cout, t.act = ctx.dcode, a["spec"].cout, a["act"]
+                t.weight = self.warena.data_ptr() + a["spec"].w_off
+                t.bias = self.barena.data_ptr() + a["spec"].b_off
+                v = a["dst"]
+                t.dst = self._ptr(v)
+                t.dst_cstride, t.dst_bstride = v.buf.c, v.buf.nelem_image
+                t.img = None
+                self._input_index = i
             elif rec.kind == N.OP_SPP:
                 s = op.u.spp
                 buf: Buffer = a["buf"]
@@ -343,6 +390,14 @@ class Plan:
                 keep.extend(a for a in args if a is not None)
                 eps = float(bn.eps) if bn is not None else 0.0
                 ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+                if s.stem:
+                    if args[0] is not None:
+                        raise NotImplementedError("fused stem conv with a conv bias")
+                    N.check(self.lib.yxh_stem_pack(
+                        w.data_ptr(), ptr(args[1]), ptr(args[2]), ptr(args[3]), ptr(args[4]), eps,
+                        conv.out_channels, dt, self.warena.data_ptr() + s.w_off,
+                        self.barena.data_ptr() + s.b_off, stream), "stem_pack")
+                    continue
                 wout = self.warena.data_ptr() + s.w_off + row * s.kh * s.kw * s.cin_pad * self.ctx.esize
                 bout = self.barena.data_ptr() + s.b_off + row * 4
                 N.check(self.lib.yxh_fold_bn_pack(
@@ -365,7 +420,11 @@ class Plan:
         if x.device != self.device:
             x = x.to(self.device, non_blocking=True)
         x = x.contiguous()
-        self._ops[self._focus_index].u.focus.img = x.data_ptr()
+        op = self._ops[self._input_index]
+        if op.kind == N.OP_STEM:
+            op.u.stem.img = x.data_ptr()
+        else:
+            op.u.focus.img = x.data_ptr()
         return x
 
     def run(self, x: torch.Tensor) -> torch.Tensor:

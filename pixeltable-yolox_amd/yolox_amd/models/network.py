@@ -129,8 +129,12 @@ class Focus(_Planned):
         super().__init__()
         self.conv = BaseConv(in_channels * 4, out_channels, ksize, stride, act=act)
 
-    def plan(self, ctx, packed):
-        return self.conv.plan(ctx, [packed])
+    def plan(self, ctx, image):
+        """Fused into one 6x6 s2 conv on the image (yxh_stem_conv) when the geometry
+        allows; otherwise yxh_focus_pack + the 3x3 conv on the packed channels."""
+        if ctx.stem_fusable(self.conv):
+            return ctx.stem(self.conv, image)
+        return self.conv.plan(ctx, [ctx.focus(image.h, image.w)])
 
 
 class CspDarknet(_Planned):

@@ -108,3 +108,24 @@ def test_autotuned_plan_matches_default(golden):
     plan.autotune(reps=1)
     b = plan.run(x).clone()
     assert torch.allclose(a, b, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fused_stem_plan_matches_focus_plan(golden, dtype):
+    """The fused Focus+stem op (default) and the two-op path (yxh_focus_pack + conv)
+    give the same network output up to summation order / one rounding."""
+    from yolox_amd import _native as N
+    from yolox_amd.engine import Plan
+    d = golden("fwd_yolox_s_128.npz")
+    m = model("yolox_s", dtype)
+    x = torch.from_numpy(d["input_u8"]).cuda()
+    fused = Plan(m, 2, 128, 128, dtype, "cuda", N.NHWC, torch.uint8)
+    split = Plan(m, 2, 128, 128, dtype, "cuda", N.NHWC, torch.uint8, fuse_stem=False)
+    assert [o.kind for o in fused.ctx.ops].count(N.OP_STEM) == 1
+    assert [o.kind for o in split.ctx.ops].count(N.OP_FOCUS) == 1
+    a, b = fused.run(x).clone(), split.run(x).clone()
+    dp = (a[..., 4:] - b[..., 4:]).abs()
+    if dtype == torch.float32:
+        assert dp.max().item() < 1e-4
+    else:  # one bf16 rounding of the stem output can flip downstream roundings
+        assert dp.max().item() < 0.2 and dp.flatten().quantile(0.99).item() < 0.06

@@ -215,6 +215,45 @@ def test_focus_pack(layout, idt, dtype):
     assert got[..., 12:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("layout,idt", [("nchw", torch.float32), ("nhwc", torch.uint8), ("nhwc", torch.float16)])
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("hw,cout", [((8, 12), 32), ((70, 198), 16), ((136, 260), 24), ((66, 130), 48),
+                                     ((34, 64), 80)])
+def test_stem_conv_fused_focus(layout, idt, dtype, hw, cout):
+    """yxh_stem_conv (Focus + 3x3 BaseConv as one 6x6 s2 conv on the image) vs the
+    reference order: space-to-depth slicing, conv, BN, SiLU in fp32."""
+    n = N()
+    H, W = hw
+    es = torch.empty((), dtype=dtype).element_size()
+    if (cout * es) % 16:
+        pytest.skip("stem output rows must be whole 16-byte chunks")
+    img = torch.randint(0, 256, (2, 3, H, W)).float()
+    src = (img if layout == "nchw" else img.permute(0, 2, 3, 1)).to(DEV, idt).contiguous()
+    conv, bn = make_conv(12, cout, 3, 1, seed=cout)
+    f = lambda t: t.detach().float().contiguous().to(DEV)  # noqa: E731
+    args = [f(conv.weight), f(bn.weight), f(bn.bias), f(bn.running_mean), f(bn.running_var)]
+    cpad = (cout + 15) // 16 * 16
+    w = torch.empty(cpad * 6 * 32, dtype=dtype, device=DEV)
+    b = torch.empty(cpad, dtype=torch.float32, device=DEV)
+    n.check(n.lib().yxh_stem_pack(*[a.data_ptr() for a in args], float(bn.eps), cout, n.DTYPE_CODE[dtype],
+                                  w.data_ptr(), b.data_ptr(), n.stream_ptr()), "stem pack")
+    cs = cout + 16  # write into a wider buffer: the extra channels must stay untouched
+    dst = torch.full((2, H // 2, W // 2, cs), 7.0, dtype=dtype, device=DEV)
+    d = n.StemDesc()
+    d.img, d.layout, d.img_dtype = src.data_ptr(), n.NCHW if layout == "nchw" else n.NHWC, n.DTYPE_CODE[idt]
+    d.batch, d.h, d.w, d.dtype, d.cout, d.act = 2, H, W, n.DTYPE_CODE[dtype], cout, n.ACT_CODE["silu"]
+    d.weight, d.bias, d.dst = w.data_ptr(), b.data_ptr(), dst.data_ptr()
+    d.dst_cstride, d.dst_bstride = cs, (H // 2) * (W // 2) * cs
+    n.check(n.lib().yxh_stem_conv(ctypes.byref(d), n.stream_ptr()), "stem")
+    torch.cuda.synchronize()
+    x = torch.cat([img[..., ::2, ::2], img[..., 1::2, ::2], img[..., ::2, 1::2], img[..., 1::2, 1::2]], 1)
+    want = ref_conv(x.to(dtype).float(), conv, bn, "silu")
+    got = dst.float().cpu().permute(0, 3, 1, 2)
+    assert (got[:, cout:] == 7.0).all()
+    err = (got[:, :cout] - want).abs().max().item() / want.abs().max().item()
+    assert err < TOL[dtype], err
+
+
 def test_letterbox_identity_and_pad():
     """r == 1 (e.g. 640x480 into 640x640) is an exact copy + 114 padding."""
     from yolox_amd.models.processor import letterbox_batch
