@@ -120,13 +120,15 @@ __device__ __forceinline__ void store4(const ConvParams& p, float v[4], int n, i
 }
 
 // Epilogue shared by the conv kernels: lane holds channels n..n+3 (rows 4*fq..) of
-// pixel column frow for every (i, j) fragment.  Staged form: bias/act/residual in
-// registers, the [TM pixels][TN channels] tile of the output dtype goes through LDS,
-// then whole pixel rows leave as 16-byte chunks (coalesced) instead of 8-byte
-// lane-scattered stores.  Caller guarantees all LDS reads of the K loop are done.
-template <typename T, int TN, int TM, int WR, int WC, int SMEM_BYTES>
-__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TN / WR / 16][TM / WC / 16],
-                                              char* smem, int m0, int n0) {
+// pixel column frow for every (i, j) fragment.  `map(pl)` turns a tile-local pixel
+// index into the global output pixel m = b*ohw + pix (or -1 outside the output).
+// Staged form: bias/act/residual in registers, the [TM pixels][TN channels] tile of
+// the output dtype goes through LDS, then whole pixel rows leave as 16-byte chunks
+// (coalesced) instead of 8-byte lane-scattered stores.  Caller guarantees all LDS
+// reads of the K loop are done.
+template <typename T, int TN, int TM, int WR, int WC, int SMEM_BYTES, typename Map>
+__device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&acc)[TN / WR / 16][TM / WC / 16],
+                                                  char* smem, const Map& map, int n0) {
     constexpr int WTN = TN / WR, WTM = TM / WC;
     constexpr int FR = WTN / 16, FC = WTM / 16;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -139,8 +141,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
 #pragma unroll
         for (int j = 0; j < FC; ++j) {
             const int pl = wc * WTM + j * 16 + frow;
-            const int m = m0 + pl;
-            const int mm = m < p.M ? m : p.M - 1;
+            const int m = map(pl);
+            const int mm = m >= 0 ? m : 0;
             const int b = mm / p.ohw, pix = mm - b * p.ohw;
             const int oy = pix / p.out_w, ox = pix - oy * p.out_w;
 #pragma unroll
@@ -150,7 +152,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
                 float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + (n + r < p.cout ? p.bias[n + r] : 0.0f);
-                if (m < p.M && n < p.cout) finish4<T>(p, v, n, b, pix, ox, oy);
+                if (m >= 0 && n < p.cout) finish4<T>(p, v, n, b, pix, ox, oy);
                 T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
                 char* dstl = smem + pl * OROW + nl * OES;
                 if constexpr (OES == 2) {
@@ -169,8 +171,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
         const int ncols = min(TN, p.cout - n0) * OES / 16;
         for (int q = tid; q < TM * CPO; q += 256) {
             const int r = q / CPO, c = q - r * CPO;
-            const int m = m0 + r;
-            if (m >= p.M || c >= ncols) continue;
+            const int m = map(r);
+            if (m < 0 || c >= ncols) continue;
             const int b = m / p.ohw, pix = m - b * p.ohw;
             const uint4 u = *(const uint4*)(smem + r * OROW + c * 16);
             *(uint4*)((char*)p.dst + ((long long)b * p.dst_bs + (long long)pix * p.dst_cs + n0) * OES + c * 16) = u;
@@ -179,8 +181,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
     }
 #pragma unroll
     for (int j = 0; j < FC; ++j) {
-        const int m = m0 + wc * WTM + j * 16 + frow;
-        if (m >= p.M) continue;
+        const int m = map(wc * WTM + j * 16 + frow);
+        if (m < 0) continue;
         const int b = m / p.ohw, pix = m - b * p.ohw;
         const int oy = pix / p.out_w, ox = pix - oy * p.out_w;
 #pragma unroll
@@ -195,7 +197,19 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
     }
 }
 
+// Linear pixel tiles: tile-local pixel pl is output pixel m0 + pl.
+template <typename T, int TN, int TM, int WR, int WC, int SMEM_BYTES>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TN / WR / 16][TM / WC / 16],
+                                              char* smem, int m0, int n0) {
+    const int M = p.M;
+    conv_epilogue_map<T, TN, TM, WR, WC, SMEM_BYTES>(
+        p, acc, smem, [m0, M](int pl) { return m0 + pl < M ? m0 + pl : -1; }, n0);
+}
+
 // LDS-DMA variant (conv_glds.hip); id as in conv.hip's tile table
 int conv_glds_dispatch(int dtype, int id, const ConvParams& p, int ks, hipStream_t st);
+// Row-tiled 3x3 conv (conv_rows.hip): 2D output tiles, kx taps share one LDS row image
+int conv_rows_dispatch(int dtype, int id, const ConvParams& p, int ks, hipStream_t st);
+constexpr int kNumRowTiles = 6;
 
 }  // namespace yxh

@@ -304,6 +304,60 @@ def test_every_tile_variant(dtype):
             close(y.permute(0, 3, 1, 2), want, dtype)
 
 
+ROW_GEOMS = [  # cin, cout, s, H, W (input)
+    (64, 96, 1, 11, 13), (24, 64, 1, 83, 41), (128, 64, 1, 20, 20), (64, 128, 2, 40, 40), (32, 48, 2, 17, 35),
+    (256, 256, 1, 10, 10), (16, 5, 1, 9, 9)]
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("geom", ROW_GEOMS)
+def test_row_tiled_conv3x3(dtype, geom):
+    """conv_rows (ids 33-38): every pixel-tile shape x K-slab count, stride 1/2,
+    partial channel blocks / cout tiles / spatial tiles, vs the fp32 reference."""
+    cin, cout, s, H, W = geom
+    conv, bn = make_conv(cin, cout, 3, s, seed=cin + cout)
+    x = torch.randn(2, cin, H, W, generator=torch.Generator().manual_seed(s))
+    want = ref_conv(x, conv, bn, "silu")
+    X = nhwc(x, dtype)
+    for tid in range(33, 39):
+        for ks in (1, 2):
+            epc = 16 // torch.empty((), dtype=dtype).element_size()
+            if ks == 2 and cin < 8 * epc:
+                with pytest.raises(ValueError, match="2-slab"):
+                    run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid + ks - 1)
+                continue
+            if s == 2 and ks == 2:
+                with pytest.raises(NotImplementedError, match="stride 2"):
+                    run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid + ks - 1)
+                continue
+            y = run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid + ks - 1)
+            close(y.permute(0, 3, 1, 2), want, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_row_tiled_residual_and_strided_dst(dtype):
+    """Bottleneck form: 3x3 conv + in-place residual, output into a channel slice of a
+    wider buffer (the CSP concat)."""
+    conv, bn = make_conv(64, 64, 3, 1, seed=3)
+    x = torch.randn(2, 64, 20, 20, generator=torch.Generator().manual_seed(4))
+    r = torch.randn(2, 64, 20, 20, generator=torch.Generator().manual_seed(5))
+    want = ref_conv(x, conv, bn, "silu") + r.to(dtype).float()
+    buf = torch.zeros(2, 20, 20, 128, dtype=dtype, device=DEV)
+    buf[..., 64:] = nhwc(r, dtype)
+    for tid in (33, 34, 36):
+        buf[..., 64:] = nhwc(r, dtype)
+        y = run_conv([(nhwc(x, dtype), 0, 64, 0)], conv, bn, dtype, residual=(buf, 64), out=buf, out_coff=64,
+                     tile=2 * tid)
+        close(y[..., 64:].permute(0, 3, 1, 2), want, dtype)
+
+
+def test_row_tiled_rejects_other_geometries():
+    conv, bn = make_conv(32, 32, 1, 1, seed=1)
+    x = nhwc(torch.randn(1, 32, 8, 8), torch.bfloat16)
+    with pytest.raises(NotImplementedError, match="conv_rows"):
+        run_conv([(x, 0, 32, 0)], conv, bn, torch.bfloat16, tile=2 * 33)
+
+
 def test_tile_variant_rejected_when_inapplicable():
     n = N()
     conv, bn = make_conv(16, 32, 3, 1, seed=1)
