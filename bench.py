@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="yolox_s")
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--chunk", type=int, default=0, help="images per pass of the op list (0 = whole batch)")
     ap.add_argument("--size", type=int, default=640)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--conf", type=float, default=0.5)
@@ -103,7 +104,7 @@ def layer_table(plan, iters=5):
     from yolox_amd import _native as N
     lib = N.lib()
     st = torch.cuda.current_stream()
-    n = len(plan._ops)
+    n = plan._nops
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
     tot = np.zeros(n)
     for _ in range(iters):
@@ -118,17 +119,18 @@ def layer_table(plan, iters=5):
     for i, rec in enumerate(plan.ctx.ops):
         a = rec.args
         if rec.kind == N.OP_CONV:
-            flop = 2.0 * plan.batch * a["out_h"] * a["out_w"] * a["cout"] * a["k"] * a["k"] * (
+            flop = 2.0 * plan.chunk * a["out_h"] * a["out_w"] * a["cout"] * a["k"] * a["k"] * (
                 a["cin"] // a["groups"] if a["groups"] > 1 else a["cin"])
             if a["groups"] > 1:
-                flop = 2.0 * plan.batch * a["out_h"] * a["out_w"] * a["cout"] * a["k"] * a["k"]
+                flop = 2.0 * plan.chunk * a["out_h"] * a["out_w"] * a["cout"] * a["k"] * a["k"]
             es = plan.ctx.esize
-            byt = plan.batch * (a["in_h"] * a["in_w"] * a["cin"] // (1 if not a["srcs"][0].up else 4)
+            byt = plan.chunk * (a["in_h"] * a["in_w"] * a["cin"] // (1 if not a["srcs"][0].up else 4)
                                 + a["out_h"] * a["out_w"] * a["cout"] * (4 if a["dst_f32"] else 1)) * es
             rows.append((i, f"conv k{a['k']}s{a['stride']} {a['cin']}->{a['cout']} @{a['out_h']}x{a['out_w']}",
                          tot[i], flop / tot[i] / 1e9, byt / tot[i] / 1e6))
         else:
-            rows.append((i, "focus" if rec.kind == N.OP_FOCUS else "spp", tot[i], 0.0, 0.0))
+            rows.append((i, {N.OP_FOCUS: "focus", N.OP_SPP: "spp", N.OP_STEM: "stem (focus+conv)"}[rec.kind], tot[i],
+                         0.0, 0.0))
     print(f"{'op':>3} {'layer':<40} {'ms':>8} {'TFLOP/s':>9} {'GB/s':>8}", file=sys.stderr)
     for r in rows:
         print(f"{r[0]:>3} {r[1]:<40} {r[2]:8.4f} {r[3]:9.1f} {r[4]:8.0f}", file=sys.stderr)
@@ -184,7 +186,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     model = YoloxModule.synthetic(args.model, seed=0, device=dev, dtype=dtype)
     B, S = args.batch, args.size
-    plan = model.plan_for(B, S, S, N.NHWC, dtype)
+    plan = model.plan_for(B, S, S, N.NHWC, dtype, chunk=args.chunk or None)
     imgs = torch.from_numpy(synthetic_images(B, S, S, seed=1000 + rank)).to(dev)
     plan.static_input().copy_(imgs.to(dtype))
     t_tune = time.perf_counter()
@@ -251,6 +253,7 @@ def main():
             "batch_per_gpu": B, "global_batch": B * world, "image_size": S,
             "parallelism": f"replicas x{world} (no data-path collective)",
             "input": f"{args.dtype} NHWC resident in HBM",
+            "chunk": plan.chunk,
         },
         "roofline": {
             "kernel": "conv_igemm (all conv launches of one forward; HIP events around each graph replay)",

@@ -242,14 +242,23 @@ def _tune_key(d) -> tuple:
 
 
 class Plan:
-    """A finalised op list with its arenas.  ``run(x)`` executes one forward pass."""
+    """A finalised op list with its arenas.  ``run(x)`` executes one forward pass.
+
+    ``chunk``: the op list is planned for ``chunk`` images and executed batch/chunk
+    times back to back on the same activation arena (input and output pointers
+    advance per chunk), so each layer's output is still in the MI355X Infinity Cache
+    when the next layer reads it.  The result is identical to an unchunked plan."""
 
     def __init__(self, model, batch: int, height: int, width: int, dtype: torch.dtype, device,
                  input_layout: int = N.NCHW, input_dtype: torch.dtype = torch.float32, train: bool = False,
-                 fuse_stem: bool = True):
+                 fuse_stem: bool = True, chunk: Optional[int] = None):
         if height % 32 or width % 32:
             raise ValueError("input size must be multiples of 32")
+        chunk = chunk or batch
+        if chunk <= 0 or batch % chunk:
+            raise ValueError(f"chunk {chunk} must divide batch {batch}")
         self.lib = N.lib()
+        self.chunk, self.nchunks = chunk, batch // chunk
         self.batch, self.height, self.width = batch, height, width
         self.device = torch.device(device)
         self.input_layout = input_layout
@@ -257,19 +266,19 @@ class Plan:
         self.dtype = dtype
         head = model.head
         self.num_classes = head.num_classes
-        ctx = PlanCtx(batch, dtype, self.device, fuse_stem=fuse_stem)
+        ctx = PlanCtx(chunk, dtype, self.device, fuse_stem=fuse_stem)
         feats = model.backbone.plan(ctx, ctx.image(height, width))
         anchors = sum(f.lh * f.lw for f in feats)
         self.out_spec = OutBuffer(anchors, 5 + self.num_classes)
         head.plan(ctx, feats, self.out_spec, train=train)
         self.ctx = ctx
         self.anchors = anchors
-        self.flops = ctx.flops
+        self.flops = ctx.flops * self.nchunks
         # ------------------------------------------------ arenas
         off = 0
         for b in ctx.buffers:
             b.offset = off
-            off += _align(batch * b.nelem_image * b.esize)
+            off += _align(chunk * b.nelem_image * b.esize)
         self.act_bytes = off
         self.arena = torch.empty(max(off, 1), dtype=torch.uint8, device=self.device)
         woff = boff = 0
@@ -287,7 +296,8 @@ class Plan:
         self.barena = torch.empty(max(boff, 1), dtype=torch.uint8, device=self.device)
         self.output = torch.empty(batch, anchors, 5 + self.num_classes, dtype=torch.float32, device=self.device)
         self._input_slot: Optional[torch.Tensor] = None
-        self._ops = (N.Op * len(ctx.ops))()
+        self._nops = len(ctx.ops)
+        self._ops = (N.Op * (len(ctx.ops) * self.nchunks))()  # chunk c = ops [c*nops, (c+1)*nops)
         self._input_index = None
         self._graph = None
         self._graph_ptrs = None
@@ -300,9 +310,14 @@ class Plan:
         return self.arena.data_ptr() + v.buf.offset + v.coff * v.buf.esize
 
     def _encode_ops(self) -> None:
-        ctx, B = self.ctx, self.batch
+        for c in range(self.nchunks):
+            self._encode_chunk(c)
+
+    def _encode_chunk(self, c: int) -> None:
+        ctx, B = self.ctx, self.chunk
+        out_base = self.output.data_ptr() + c * B * self.anchors * self.out_spec.row * 4
         for i, rec in enumerate(ctx.ops):
-            op = self._ops[i]
+            op = self._ops[c * self._nops + i]
             op.kind = rec.kind
             a = rec.args
             if rec.kind == N.OP_FOCUS:
@@ -356,7 +371,7 @@ class Plan:
                 if a["dst_f32"]:
                     out, a_off, coff = a["head_out"]
                     row = out.row
-                    d.dst = self.output.data_ptr() + (a_off * row + coff) * 4
+                    d.dst = out_base + (a_off * row + coff) * 4
                     d.dst_dtype = N.F32
                     d.dst_cstride, d.dst_bstride = row, out.anchors * row
                     d.decode_stride, d.decode_coff = a["decode_stride"], a["decode_coff"]
@@ -421,11 +436,13 @@ class Plan:
         if x.device != self.device:
             x = x.to(self.device, non_blocking=True)
         x = x.contiguous()
-        op = self._ops[self._input_index]
-        if op.kind == N.OP_STEM:
-            op.u.stem.img = x.data_ptr()
-        else:
-            op.u.focus.img = x.data_ptr()
+        step = self.chunk * x[0].numel() * x.element_size()
+        for c in range(self.nchunks):
+            op = self._ops[c * self._nops + self._input_index]
+            if op.kind == N.OP_STEM:
+                op.u.stem.img = x.data_ptr() + c * step
+            else:
+                op.u.focus.img = x.data_ptr() + c * step
         return x
 
     def run(self, x: torch.Tensor) -> torch.Tensor:
@@ -481,7 +498,7 @@ class Plan:
         self.pack_weights()
         self._bind_input(self.static_input())
         L, st = self.lib, N.stream_ptr(self.device)
-        N.check(L.yxh_run_ops(self._ops, len(self._ops), st), "forward")
+        N.check(L.yxh_run_ops(self._ops, self._nops, st), "forward")
         stream = torch.cuda.current_stream(self.device)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         chosen = {}
@@ -515,6 +532,9 @@ class Plan:
                 a = rec.args
                 print(f"tune op {i}: k{a['k']}s{a['stride']} {a['cin']}->{a['cout']} @{a['out_h']}x{a['out_w']}"
                       f" -> tile {best[1] >> 1} slabs {(best[1] & 1) + 1} {best[0] * 1e3:.1f} us", file=sys.stderr)
+        for c in range(1, self.nchunks):
+            for i, t in chosen.items():
+                self._ops[c * self._nops + i].u.conv.tile = t
         torch.cuda.synchronize(self.device)
         if self._graph is not None:  # a captured graph holds the old tiles
             self.capture()
@@ -522,5 +542,5 @@ class Plan:
 
     # -------------------------------------------------------------- reporting
     def conv_ops(self):
-        """(index, ConvDesc) of every conv op, for per-kernel roofline accounting."""
+        """(index, ConvDesc) of every conv op of the first chunk, for per-kernel accounting."""
         return [(i, self._ops[i].u.conv) for i, r in enumerate(self.ctx.ops) if r.kind == N.OP_CONV]

@@ -47,17 +47,19 @@ class YoloxModule(nn.Module):
         return self.backbone.backbone.stem.conv.conv.weight.device
 
     def plan_for(self, batch: int, height: int, width: int, input_layout: int = N.NCHW,
-                 input_dtype: torch.dtype = torch.float32, dtype: Optional[torch.dtype] = None):
-        """The (cached) HIP execution plan for this input geometry."""
+                 input_dtype: torch.dtype = torch.float32, dtype: Optional[torch.dtype] = None,
+                 chunk: Optional[int] = None):
+        """The (cached) HIP execution plan for this input geometry (``chunk``: images
+        per pass of the op list, see engine.Plan)."""
         from ..engine import Plan
 
         dtype = dtype or self.compute_dtype
-        key = (batch, height, width, input_layout, input_dtype, dtype, str(self.device))
+        key = (batch, height, width, input_layout, input_dtype, dtype, str(self.device), chunk)
         plan = self._plans.get(key)
         if plan is None:
             if self.device.type != "cuda":
                 raise RuntimeError("YoloxModule runs on a ROCm device only; call .to('cuda') first")
-            plan = Plan(self, batch, height, width, dtype, self.device, input_layout, input_dtype)
+            plan = Plan(self, batch, height, width, dtype, self.device, input_layout, input_dtype, chunk=chunk)
             self._plans[key] = plan
         return plan
 

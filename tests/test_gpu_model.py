@@ -129,3 +129,23 @@ def test_fused_stem_plan_matches_focus_plan(golden, dtype):
         assert dp.max().item() < 1e-4
     else:  # one bf16 rounding of the stem output can flip downstream roundings
         assert dp.max().item() < 0.2 and dp.flatten().quantile(0.99).item() < 0.06
+
+
+def test_chunked_plan_matches_whole_batch():
+    """Executing the op list per chunk of images (Infinity-Cache-sized passes) gives
+    the whole-batch result bit for bit, eager and as a graph."""
+    from yolox_amd import _native as N
+    from yolox_amd.engine import Plan
+    from yolox_amd.weights import synthetic_images
+    m = model("yolox_s", torch.bfloat16)
+    x = torch.from_numpy(synthetic_images(4, 128, 128, seed=9)).cuda()
+    whole = Plan(m, 4, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8)
+    chunked = Plan(m, 4, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8, chunk=2)
+    assert chunked.flops == whole.flops
+    a = whole.run(x).clone()
+    b = chunked.run(x).clone()
+    assert torch.equal(a, b)
+    chunked.static_input().copy_(x)
+    assert torch.equal(chunked.replay().clone(), a)
+    with pytest.raises(ValueError, match="chunk"):
+        Plan(m, 4, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8, chunk=3)
