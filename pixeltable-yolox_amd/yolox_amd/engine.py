@@ -229,9 +229,9 @@ class OutBuffer:
 
 
 # tile codes (2 * id + slabs - 1); ids 1-9 register-staged conv_igemm, 17-25 the same
-# tiles on the LDS-DMA conv_glds kernel, 33-38 the row-tiled 3x3 conv_rows kernel
+# tiles on the LDS-DMA conv_glds kernel, 33-47 the row-tiled 3x3 conv_rows kernel
 # (yoloxhip.h yxh_conv_desc.tile)
-TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 39)) for k in (0, 1)]
+TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 48)) for k in (0, 1)]
 _TUNE_CACHE: dict = {}
 
 

@@ -319,7 +319,7 @@ def test_row_tiled_conv3x3(dtype, geom):
     x = torch.randn(2, cin, H, W, generator=torch.Generator().manual_seed(s))
     want = ref_conv(x, conv, bn, "silu")
     X = nhwc(x, dtype)
-    for tid in range(33, 39):
+    for tid in range(33, 48):
         for ks in (1, 2):
             epc = 16 // torch.empty((), dtype=dtype).element_size()
             if ks == 2 and cin < 8 * epc:
@@ -330,7 +330,12 @@ def test_row_tiled_conv3x3(dtype, geom):
                 with pytest.raises(NotImplementedError, match="stride 2"):
                     run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid + ks - 1)
                 continue
-            y = run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid + ks - 1)
+            try:
+                y = run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid + ks - 1)
+            except NotImplementedError as e:  # variant not built for this dtype / too much LDS
+                assert tid > 38 or ks == 2, e
+                assert ("bf16/f16 only" in str(e) and dtype == torch.float32) or "160 KiB" in str(e), e
+                continue
             close(y.permute(0, 3, 1, 2), want, dtype)
 
 

@@ -26,12 +26,17 @@ def run(outputs, labels, hw, origin=None):
     return {k: v.item() for k, v in losses.items()}, {k: v.cpu() for k, v in assign.items()}
 
 
-def check_image(assign, b, fg_ref, matched_ref, piou_ref, nfg_ref):
+def check_image(assign, b, fg_ref, matched_ref, piou_ref, nfg_ref, iou_rtol=0.0):
+    """Assignment exact; pred IoUs bit-exact when the head outputs are the reference's
+    own, within iou_rtol when they come from the oracle (equal to fp32 rounding)."""
     fg = assign["fg_mask"][b].numpy()
     np.testing.assert_array_equal(fg, fg_ref)
     assert int(assign["num_fg"][b]) == int(nfg_ref)
     np.testing.assert_array_equal(assign["matched_gt_inds"][b].numpy()[fg], matched_ref)
-    np.testing.assert_array_equal(assign["pred_ious"][b].numpy()[fg], piou_ref)
+    if iou_rtol:
+        np.testing.assert_allclose(assign["pred_ious"][b].numpy()[fg], piou_ref, rtol=iou_rtol, atol=0)
+    else:
+        np.testing.assert_array_equal(assign["pred_ious"][b].numpy()[fg], piou_ref)
 
 
 def test_simota_640_fixture(golden):
@@ -61,8 +66,9 @@ def test_losses_match_reference_train_step(oracle, golden, tag):
     for k, ref_k in names.items():
         assert losses[k] == pytest.approx(float(d[f"{tag}.{ref_k}"]), rel=1e-4, abs=1e-6), k
     for b in range(2):
+        # head outputs from the oracle (not bit-identical to the reference's): IoUs to 1e-6
         check_image(assign, b, d[f"{tag}.img{b}.fg_mask"], d[f"{tag}.img{b}.matched_gt_inds"],
-                    d[f"{tag}.img{b}.pred_ious"], d[f"{tag}.img{b}.num_fg"])
+                    d[f"{tag}.img{b}.pred_ious"], d[f"{tag}.img{b}.num_fg"], iou_rtol=1e-6)
 
 
 @pytest.mark.parametrize("seed", [0, 1])

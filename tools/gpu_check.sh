@@ -12,9 +12,6 @@ echo "pytest exit=$rc" >> gpurun_out/gpu_tests_$TAG.log
 # 1 = ordinary test failures; anything else (abort, segfault, timeout) ends the session
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 400 python bench.py --layers > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 1
-for bs in 8 16; do
-  timeout -k 10 300 python bench.py --batch $bs --no-cpu-baseline > gpurun_out/bench_${TAG}_bs$bs.json 2> gpurun_out/bench_${TAG}_bs$bs.err || exit 1
-done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
     -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
 echo "done rc=$?"
