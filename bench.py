@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layers", action="store_true", help="print a per-op time/roofline table to stderr")
+    ap.add_argument("--tune-file", default="", help="JSON tile choices: loaded if present (skips tuning), else written")
     return ap.parse_args()
 
 
@@ -189,9 +190,14 @@ def main():
     plan = model.plan_for(B, S, S, N.NHWC, dtype, chunk=args.chunk or None)
     imgs = torch.from_numpy(synthetic_images(B, S, S, seed=1000 + rank)).to(dev)
     plan.static_input().copy_(imgs.to(dtype))
+    from yolox_amd import engine
+    if args.tune_file and os.path.exists(args.tune_file):
+        engine.load_tune_cache(args.tune_file)
     t_tune = time.perf_counter()
     plan.autotune(verbose=args.layers and rank == 0)
     t_tune = time.perf_counter() - t_tune
+    if args.tune_file and rank == 0 and not os.path.exists(args.tune_file):
+        engine.save_tune_cache(args.tune_file)
     plan.capture()
     A = plan.anchors
     det = torch.empty(B, A, 7, dtype=torch.float32, device=dev)

@@ -100,8 +100,9 @@ typedef struct {
     int32_t decode_coff; /* position of output channel 0 in the 5+C row (0 or 5)       */
     int32_t tile;        /* 0: heuristic; else 2*id + (slabs-1): id 1-9 explicit tile
                             (TN x TM) of the register-staged kernel, id 17-25 the same
-                            tiles on the LDS-DMA kernel; chosen by the planner's
-                            on-device autotune                                           */
+                            tiles on the LDS-DMA kernel, id 33-51 the row-tiled 3x3
+                            kernel, id 65-70 the persistent streaming 1x1 kernel;
+                            chosen by the planner's on-device autotune                   */
     int32_t reserved;
 } yxh_conv_desc;
 

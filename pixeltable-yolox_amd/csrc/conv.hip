@@ -466,7 +466,7 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         tile = d->tile >> 1;
         const int want_ks = (d->tile & 1) + 1;
         YXH_CHECK_ARG((tile > 0 && tile < kNumTiles) || (tile > 16 && tile < 16 + kNumTiles) ||
-                          (tile > 32 && tile <= 32 + kNumRowTiles),
+                          (tile > 32 && tile <= 32 + kNumRowTiles) || (tile > 64 && tile <= 64 + kNumPwTiles),
                       "tile %d", d->tile);
         YXH_CHECK_ARG(want_ks == 1 || ks == 2, "2-slab staging not possible for this conv");
         ks = want_ks;
@@ -475,6 +475,7 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     YXH_CHECK_ARG(d->nsrc == 1 || p.src0_ch % kstage == 0, "src0 channels %d not a multiple of %d", p.src0_ch,
                   kstage);
     p.ncb = (d->cin + kstage - 1) / kstage;
+    if (tile > 64) return conv_pw_dispatch(dt, tile - 64, p, ks, st);
     if (tile > 32) return conv_rows_dispatch(dt, tile - 32, p, ks, st);
     if (tile > 16) return conv_glds_dispatch(dt, tile - 16, p, ks, st);
     if (dt == YXH_BF16) return launch_tile<bf16>(tile, p, ks, st);

@@ -210,6 +210,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
 int conv_glds_dispatch(int dtype, int id, const ConvParams& p, int ks, hipStream_t st);
 // Row-tiled 3x3 conv (conv_rows.hip): 2D output tiles, kx taps share one LDS row image
 int conv_rows_dispatch(int dtype, int id, const ConvParams& p, int ks, hipStream_t st);
-constexpr int kNumRowTiles = 15;
+constexpr int kNumRowTiles = 19;
+// Persistent streaming 1x1 conv (conv_pw.hip): tile ids 65..64+kNumPwTiles
+int conv_pw_dispatch(int dtype, int id, const ConvParams& p, int ks, hipStream_t st);
+constexpr int kNumPwTiles = 6;
 
 }  // namespace yxh

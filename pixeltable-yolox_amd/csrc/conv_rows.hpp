@@ -240,6 +240,10 @@ static int dispatch_shape(int id, const ConvParams& p, hipStream_t st) {
             case 13: return launch_rows<T, S, 32, 8, CH, 128, 2>(p, st);
             case 14: return launch_rows<T, S, 32, 4, CH, 128, 2>(p, st);
             case 15: return launch_rows<T, S, 16, 8, CH, 128, 2>(p, st);
+            case 16: return launch_rows<T, S, 16, 8, CH, 64, 3>(p, st);
+            case 17: return launch_rows<T, S, 32, 4, CH, 64, 3>(p, st);
+            case 18: return launch_rows<T, S, 8, 16, CH, 64, 2>(p, st);
+            case 19: return launch_rows<T, S, 64, 2, CH, 64, 2>(p, st);
             default: break;
         }
     } else if (id > 6 && id <= kNumRowTiles) {

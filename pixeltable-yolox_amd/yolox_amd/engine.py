@@ -229,10 +229,27 @@ class OutBuffer:
 
 
 # tile codes (2 * id + slabs - 1); ids 1-9 register-staged conv_igemm, 17-25 the same
-# tiles on the LDS-DMA conv_glds kernel, 33-47 the row-tiled 3x3 conv_rows kernel
+# tiles on the LDS-DMA conv_glds kernel, 33-51 the row-tiled 3x3 conv_rows kernel,
+# 65-70 the persistent streaming 1x1 conv_pw kernel
 # (yoloxhip.h yxh_conv_desc.tile)
-TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 48)) for k in (0, 1)]
+TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
+                   + list(range(65, 71)) for k in (0, 1)]
 _TUNE_CACHE: dict = {}
+
+
+def save_tune_cache(path: str) -> None:
+    """Write the per-shape tile choices (JSON) so another process can skip tuning."""
+    import json
+    with open(path, "w") as f:
+        json.dump([[list(k), v] for k, v in _TUNE_CACHE.items()], f)
+
+
+def load_tune_cache(path: str) -> int:
+    import json
+    with open(path) as f:
+        for k, v in json.load(f):
+            _TUNE_CACHE[tuple(k)] = int(v)
+    return len(_TUNE_CACHE)
 
 
 def _tune_key(d) -> tuple:

@@ -319,7 +319,7 @@ def test_row_tiled_conv3x3(dtype, geom):
     x = torch.randn(2, cin, H, W, generator=torch.Generator().manual_seed(s))
     want = ref_conv(x, conv, bn, "silu")
     X = nhwc(x, dtype)
-    for tid in range(33, 48):
+    for tid in range(33, 52):
         for ks in (1, 2):
             epc = 16 // torch.empty((), dtype=dtype).element_size()
             if ks == 2 and cin < 8 * epc:
@@ -354,6 +354,71 @@ def test_row_tiled_residual_and_strided_dst(dtype):
         y = run_conv([(nhwc(x, dtype), 0, 64, 0)], conv, bn, dtype, residual=(buf, 64), out=buf, out_coff=64,
                      tile=2 * tid)
         close(y[..., 64:].permute(0, 3, 1, 2), want, dtype)
+
+
+PW_GEOMS = [  # cin, cout, H, W
+    (32, 16, 16, 16), (64, 64, 20, 20), (96, 192, 7, 9), (256, 5, 6, 6), (128, 80, 33, 17), (512, 256, 4, 4),
+    (1024, 512, 4, 4)]
+
+
+def pw_call(fn, dtype, tid, ks):
+    """Run a conv_pw variant; returns None when it is documented as not applicable."""
+    try:
+        return fn(2 * tid + ks - 1)
+    except NotImplementedError as e:
+        msg = str(e)
+        assert "exceed" in msg or "160 KiB" in msg or (dtype == torch.float32 and "bf16/f16 only" in msg), msg
+        return None
+    except ValueError as e:
+        assert "2-slab" in str(e), e
+        return None
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("geom", PW_GEOMS)
+def test_streaming_pointwise_conv(dtype, geom):
+    """conv_pw (ids 65-70): persistent 1x1 conv with resident weights, every variant
+    x K-stage size vs the fp32 reference; at least one variant runs for bf16/f16."""
+    cin, cout, H, W = geom
+    conv, bn = make_conv(cin, cout, 1, 1, seed=cin + 3 * cout)
+    x = torch.randn(3, cin, H, W, generator=torch.Generator().manual_seed(7))
+    want = ref_conv(x, conv, bn, "silu")
+    X = nhwc(x, dtype)
+    ran = 0
+    for tid in range(65, 71):
+        for ks in (1, 2):
+            y = pw_call(lambda t: run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=t), dtype, tid, ks)
+            if y is not None:
+                close(y.permute(0, 3, 1, 2), want, dtype)
+                ran += 1
+    assert ran > 0 or dtype == torch.float32 or cin * 64 * 2 > 64 * 1024
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_streaming_pointwise_two_sources_upsample(dtype):
+    """conv_pw on the PAFPN pattern: cat([upsample(slice of a), b]) into an output slice."""
+    a_full = torch.randn(2, 192, 5, 6)
+    b = torch.randn(2, 64, 10, 12)
+    conv, bn = make_conv(128 + 64, 96, 1, 1, seed=9)
+    A, Bt = nhwc(a_full, dtype), nhwc(b, dtype)
+    ref = ref_conv(torch.cat([F.interpolate(a_full[:, 64:], scale_factor=2, mode="nearest"), b], 1), conv, bn,
+                   "silu")
+    for tid in range(65, 71):
+        for ks in (1, 2):
+            out = torch.zeros(2, 10, 12, 160, dtype=dtype, device=DEV)
+            y = pw_call(lambda t: run_conv([(A, 64, 128, 1), (Bt, 0, 64, 0)], conv, bn, dtype, out=out, out_coff=32,
+                                           tile=t), dtype, tid, ks)
+            if y is None:
+                continue
+            close(out[..., 32:128].permute(0, 3, 1, 2), ref, dtype)
+            assert out[..., :32].abs().max().item() == 0 and out[..., 128:].abs().max().item() == 0
+
+
+def test_streaming_pointwise_rejects_residual_and_3x3():
+    conv, bn = make_conv(32, 32, 3, 1, seed=1)
+    x = nhwc(torch.randn(1, 32, 8, 8), torch.bfloat16)
+    with pytest.raises(NotImplementedError, match="conv_pw"):
+        run_conv([(x, 0, 32, 0)], conv, bn, torch.bfloat16, tile=2 * 65)
 
 
 def test_row_tiled_rejects_other_geometries():

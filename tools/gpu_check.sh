@@ -11,7 +11,8 @@ rc=$?
 echo "pytest exit=$rc" >> gpurun_out/gpu_tests_$TAG.log
 # 1 = ordinary test failures; anything else (abort, segfault, timeout) ends the session
 [ $rc -le 1 ] || exit $rc
-timeout -k 10 400 python bench.py --layers > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 1
+timeout -k 10 400 python bench.py --layers --tune-file gpurun_out/tune_$TAG.json > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
-    -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
+    -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --tune-file gpurun_out/tune_$TAG.json \
+    > gpurun_out/prof_$TAG.log 2>&1
 echo "done rc=$?"
