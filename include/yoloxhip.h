@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 2
+#define YXH_ABI_VERSION 3
 
 enum yxh_status {
     YXH_OK = 0,
@@ -58,7 +58,10 @@ typedef struct {
     int32_t cstride;  /* elements between consecutive pixels                                */
     int64_t bstride;  /* elements between consecutive images                                */
     int32_t h, w;     /* stored spatial size                                                */
-    int32_t upsample; /* 0: pixel (y,x); 1: nearest x2, reads (y>>1, x>>1) (yolo_pafpn.py:32) */
+    int32_t upsample; /* 0: pixel (y,x); 1: nearest x2, reads (y>>1, x>>1) (yolo_pafpn.py:32);
+                         2: zero-inserting x2 dilation, (y,x) even -> (y>>1, x>>1), odd -> 0
+                            (the input of a stride-2 conv's data gradient; register-staged
+                            conv kernel only)                                               */
     int32_t reserved;
 } yxh_src;
 
@@ -103,8 +106,10 @@ typedef struct {
                             tiles on the LDS-DMA kernel, id 33-51 the row-tiled 3x3
                             kernel, id 65-70 the persistent streaming 1x1 kernel;
                             chosen by the planner's on-device autotune                   */
-    int32_t reserved;
+    int32_t flags;       /* YXH_CONV_ACCUMULATE: f32 dst += result (gradient accumulation) */
 } yxh_conv_desc;
+
+#define YXH_CONV_ACCUMULATE 1
 
 int yxh_conv2d(const yxh_conv_desc* d, void* stream);
 
@@ -203,6 +208,104 @@ int yxh_yolox_loss(const float* preds, const float* origin, const float* labels,
                    const int32_t* strides, int32_t nlevels, uint8_t* fg_mask, int32_t* matched_gt,
                    float* pred_iou, int32_t* num_fg, float* losses, void* workspace,
                    size_t workspace_bytes, void* stream);
+
+/* ============================================================== training
+ * The backward pass of YoloxModule (train mode): BaseConv = conv -> BatchNorm2d (batch
+ * statistics) -> act, and its gradients.  Data gradients of convolutions run on
+ * yxh_conv2d with yxh_pack_dgrad_weight's transposed, flipped weights (stride 2: the
+ * gradient source with upsample == 2) and YXH_CONV_ACCUMULATE into fp32 gradient
+ * buffers.  Views (yxh_src) give channel slices of wider buffers; `batch` images of
+ * h x w pixels each.  Activation gradients are fp32; activations are `dtype`.
+ */
+
+/* Workspace for the per-channel reductions below (channels C). */
+size_t yxh_reduce_workspace_bytes(int32_t channels);
+
+/*
+ * yxh_bn_stats: BatchNorm2d.forward in training mode (network_blocks.py:44-49,
+ * eps / momentum config.py:162-166) over the raw conv output y: per-channel mean and
+ * biased variance, stats[4][C] = mean, invstd, gamma*invstd, beta - mean*gamma*invstd;
+ * running_mean / running_var (may both be NULL) updated with `momentum` and the
+ * unbiased variance, as torch does.
+ */
+int yxh_bn_stats(int32_t dtype, int32_t batch, const yxh_src* y, const float* gamma, const float* beta,
+                 float* running_mean, float* running_var, float eps, float momentum, float* stats,
+                 void* workspace, size_t workspace_bytes, void* stream);
+
+/* out = act(y * scale + shift) (+ residual, network_blocks.py:97-99). */
+int yxh_bn_act_fwd(int32_t dtype, int32_t batch, const yxh_src* y, const float* stats, int32_t act,
+                   const yxh_src* residual, const yxh_src* out, void* stream);
+
+/*
+ * Backward of act(BN(y)): dout fp32 view -> dgamma, dbeta (fp32 [C]) and the conv
+ * output gradient dx (`dtype`, dense [batch*h*w][C]).
+ */
+int yxh_bn_act_bwd(int32_t dtype, int32_t batch, const yxh_src* y, const yxh_src* dout, const float* stats,
+                   const float* gamma, int32_t act, float* dgamma, float* dbeta, void* dx, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
+/* out[c] = sum over pixels of x[c] (bias gradients of the head's pred convs). */
+int yxh_channel_sum(int32_t dtype, int32_t batch, const yxh_src* x, float* out, void* workspace,
+                    size_t workspace_bytes, void* stream);
+
+/*
+ * yxh_conv_wgrad: weight gradient of Conv2d (autograd of network_blocks.py:48 and the
+ * head's preds, yolo_head.py:149-160) on MFMA: dw[cout][cin_store][kh][kw] (torch layout,
+ * fp32) += sum over output pixels of dy[cout] * x[cin](tap).  dw must be zeroed by the
+ * caller (split-K over pixel ranges with fp32 atomics).  src: the forward's input views
+ * (1-2 sources, nearest-x2 allowed); dy.channels >= cout, padded to 16-byte chunks.
+ */
+typedef struct {
+    int32_t dtype, batch, in_h, in_w, out_h, out_w, cin, cout, kh, kw, stride, pad;
+    int32_t nsrc, cin_store; /* cin_store <= cin: dw's input-channel extent (Focus: 12 of 16) */
+    yxh_src src[2];
+    yxh_src dy;
+    float* dw;
+    int32_t tile, reserved;  /* tile 0: default */
+} yxh_wgrad_desc;
+int yxh_conv_wgrad(const yxh_wgrad_desc* d, void* stream);
+
+/*
+ * yxh_pack_dgrad_weight: [cout][cin][kh][kw] fp32 -> [c_count][kh][kw][cout_pad] `dtype`
+ * with flipped taps for input channels [c_begin, c_begin + c_count): the weights of the
+ * data-gradient conv (zeros in [cout, cout_pad)).
+ */
+int yxh_pack_dgrad_weight(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, int32_t c_begin,
+                          int32_t c_count, int32_t cout_pad, int32_t dtype, void* out, void* stream);
+
+/*
+ * yxh_spp_bwd: SPPBottleneck concat + max_pool2d(5, 9, 13) backward
+ * (network_blocks.py:137-141): cat holds x in channels [0, c); dcat fp32 dense
+ * [batch*h*w][4c]; dx fp32 dense [batch*h*w][c] = dcat[:, :c] + pooled-argmax gradients.
+ */
+int yxh_spp_bwd(int32_t dtype, int32_t batch, const yxh_src* cat, int32_t c, const float* dcat, float* dx,
+                void* stream);
+
+/* nn.Upsample(nearest, x2) backward: dst[B,h,w,C] += 2x2 sums of g[B,2h,2w,C] (fp32). */
+int yxh_upsample_bwd(const float* g, int32_t batch, int32_t h, int32_t w, int32_t c, float* dst, void* stream);
+
+/*
+ * yxh_head_decode_train: YoloxHead.get_output_and_grid (yolo_head.py:213-231) on the
+ * raw pred-conv outputs raw[B, A, 5+C] (fp32): out = raw with ch 0-1 -> (v + grid) *
+ * stride and ch 2-3 -> exp(v) * stride.
+ */
+int yxh_head_decode_train(const float* raw, int32_t batch, int32_t anchors, int32_t num_classes,
+                          const int32_t* level_hw, const int32_t* strides, int32_t nlevels, float* out,
+                          void* stream);
+
+/*
+ * yxh_yolox_loss_bwd: gradient of losses[0] (total_loss of yxh_yolox_loss) w.r.t. the raw
+ * pred-conv outputs, given the assignment that call produced (autograd of
+ * yolo_head.py:382-402, losses.py:13-51, through the decode of :227-230).
+ * grad_total: device fp32 scalar dL/d(total_loss) (e.g. 1 or the loss scale).
+ * out (`dtype`): g_regobj [B*A][8] (ch 0-3 reg, 4 obj, 5-7 zero), g_cls [B*A][C].
+ */
+int yxh_yolox_loss_bwd(const float* preds, const float* raw, const float* labels, int32_t batch,
+                       int32_t anchors, int32_t num_classes, int32_t max_labels, const int32_t* level_hw,
+                       const int32_t* strides, int32_t nlevels, const uint8_t* fg_mask,
+                       const int32_t* matched_gt, const float* pred_iou, const int32_t* num_fg,
+                       const float* grad_total, int32_t use_l1, int32_t dtype, void* g_regobj, void* g_cls,
+                       void* stream);
 
 /*
  * Plan execution.  A forward pass is a fixed list of ops (built once per model and

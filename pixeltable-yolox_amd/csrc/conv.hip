@@ -80,13 +80,14 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvParams p) {
             cc = c - p.src0_ch;
         }
         const T* sp = (const T*)p.sptr[s];
-        const int scs = p.scs[s], sw = p.sw[s], up = p.sup[s];
+        const int scs = p.scs[s], sw = p.sw[s], up = p.sup[s] ? 1 : 0;
+        const int odd = p.sup[s] == 2 ? 1 : 0;  // zero-inserting dilation: odd positions read 0
         const long long sbs = p.sbs[s];
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
             int iy = by[i] + ky, ix = bx[i] + kx;
             rb[i] = make_uint4(0, 0, 0, 0);
-            if (bb[i] >= 0 && cok && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w)
+            if (bb[i] >= 0 && cok && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w && !((iy | ix) & odd))
                 rb[i] = *(const uint4*)(sp + bb[i] * sbs +
                                         ((long long)(iy >> up) * sw + (ix >> up)) * scs + cc);
         }
@@ -390,15 +391,19 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     const bool dw = d->groups != 1;
     YXH_CHECK_ARG(!dw || (d->groups == d->cin && d->cout == d->cin && d->nsrc == 1), "groups %d", d->groups);
     int chs = 0;
+    bool dilated = false;
     for (int s = 0; s < d->nsrc; ++s) {
         const yxh_src& q = d->src[s];
         YXH_CHECK_ARG(q.ptr && aligned16(q.ptr), "src%d null or not 16-byte aligned", s);
         YXH_CHECK_ARG(q.channels > 0 && q.channels % epc == 0, "src%d channels %d not a multiple of %d", s,
                       q.channels, epc);
         YXH_CHECK_ARG(q.cstride % epc == 0 && q.bstride % epc == 0, "src%d strides not 16-byte multiples", s);
-        YXH_CHECK_ARG(q.upsample == 0 || q.upsample == 1, "upsample %d", q.upsample);
-        YXH_CHECK_ARG((q.h << q.upsample) == d->in_h && (q.w << q.upsample) == d->in_w,
+        YXH_CHECK_ARG(q.upsample >= 0 && q.upsample <= 2, "upsample %d", q.upsample);
+        YXH_CHECK_ARG(q.upsample != 2 || !dw, "dilated source on a depthwise conv");
+        const int ush = q.upsample ? 1 : 0;
+        YXH_CHECK_ARG((q.h << ush) == d->in_h && (q.w << ush) == d->in_w,
                       "src%d spatial %dx%d (up %d) vs input %dx%d", s, q.h, q.w, q.upsample, d->in_h, d->in_w);
+        dilated |= q.upsample == 2;
         chs += q.channels;
     }
     YXH_CHECK_ARG(chs == d->cin, "source channels %d != cin %d", chs, d->cin);
@@ -433,6 +438,8 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     p.dst_cs = d->dst_cstride;
     p.dst_bs = d->dst_bstride;
     p.dst_f32 = d->dst_dtype == YXH_F32 && dt != YXH_F32 ? 1 : (dt == YXH_F32 ? 1 : 0);
+    YXH_CHECK_ARG(!(d->flags & YXH_CONV_ACCUMULATE) || d->dst_dtype == YXH_F32, "accumulate needs an f32 dst");
+    p.accum = (d->flags & YXH_CONV_ACCUMULATE) ? 1 : 0;
     p.act = d->act;
     p.dstride = d->decode_stride;
     p.dcoff = d->decode_coff;
@@ -475,6 +482,10 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     YXH_CHECK_ARG(d->nsrc == 1 || p.src0_ch % kstage == 0, "src0 channels %d not a multiple of %d", p.src0_ch,
                   kstage);
     p.ncb = (d->cin + kstage - 1) / kstage;
+    if (dilated && tile > 16) {
+        set_error("dilated (upsample == 2) sources run on the register-staged kernel only (tile ids 1-9)");
+        return YXH_EUNSUPPORTED;
+    }
     if (tile > 64) return conv_pw_dispatch(dt, tile - 64, p, ks, st);
     if (tile > 32) return conv_rows_dispatch(dt, tile - 32, p, ks, st);
     if (tile > 16) return conv_glds_dispatch(dt, tile - 16, p, ks, st);

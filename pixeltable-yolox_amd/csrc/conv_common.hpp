@@ -21,6 +21,7 @@ struct ConvParams {
     long long dst_bs;
     int dst_f32, act, dcoff, vec_store, vec_res;
     int vec16;  // dst rows 16-byte aligned and cout a chunk multiple: LDS-staged epilogue
+    int accum;  // f32 dst += result (YXH_CONV_ACCUMULATE: data-gradient accumulation)
     float dstride;
 };
 
@@ -95,6 +96,16 @@ __device__ __forceinline__ void store4(const ConvParams& p, float v[4], int n, i
     long long off = (long long)b * p.dst_bs + (long long)pix * p.dst_cs + n;
     if (p.dst_f32) {
         float* dp = (float*)p.dst + off;
+        if (p.accum) {
+            if (full && p.vec_store) {
+                const float4 o = *(const float4*)dp;
+                v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (n + r < p.cout) v[r] += dp[r];
+            }
+        }
         if (full && p.vec_store) {
             *(float4*)dp = make_float4(v[0], v[1], v[2], v[3]);
         } else {

@@ -39,6 +39,25 @@ int yolox_loss(const float* preds, const float* origin, const float* labels, int
                const int* lhw, const int* strides, int nlev, uint8_t* fg, int* matched, float* piou, int* num_fg,
                float* losses, void* ws, size_t ws_bytes, hipStream_t st);
 int letterbox_launch(const uint8_t* src, int sh, int sw, int th, int tw, int out_nchw, void* dst, hipStream_t st);
+size_t reduce_workspace(int C);
+int bn_stats(int dt, int B, const yxh_src* y, const float* gamma, const float* beta, float* rmean, float* rvar,
+             float eps, float momentum, float* stats, void* ws, size_t ws_bytes, hipStream_t st);
+int bn_act_fwd_launch(int dt, int B, const yxh_src* y, const float* stats, int act, const yxh_src* res,
+                      const yxh_src* out, hipStream_t st);
+int bn_act_bwd_launch(int dt, int B, const yxh_src* y, const yxh_src* dout, const float* stats, const float* gamma,
+                      int act, float* dgamma, float* dbeta, void* dx, void* ws, size_t ws_bytes, hipStream_t st);
+int channel_sum_launch(int dt, int B, const yxh_src* x, float* out, void* ws, size_t ws_bytes, hipStream_t st);
+int conv_wgrad_launch(const yxh_wgrad_desc* d, hipStream_t st);
+int pack_dgrad_launch(const float* w, int cout, int cin, int kh, int kw, int c_begin, int c_count, int cout_pad, int dt,
+                      void* out, hipStream_t st);
+int spp_bwd_launch(int dt, int B, const yxh_src* cat, int c, const float* dcat, float* dx, hipStream_t st);
+int upsample_bwd_launch(const float* g, int B, int h, int w, int C, float* dst, hipStream_t st);
+int head_decode_train_launch(const float* raw, int B, int A, int C, const int* lhw, const int* strides, int nlev,
+                             float* out, hipStream_t st);
+int yolox_loss_bwd(const float* preds, const float* raw, const float* labels, int B, int A, int C, int L,
+                   const int* lhw, const int* strides, int nlev, const uint8_t* fg, const int* matched,
+                   const float* piou, const int* num_fg, const float* gtot, int use_l1, int dt, void* g_ro,
+                   void* g_cls, hipStream_t st);
 int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
                 float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st);
 
@@ -125,6 +144,64 @@ int yxh_yolox_loss(const float* preds, const float* origin, const float* labels,
                    float* losses, void* workspace, size_t workspace_bytes, void* stream) {
     return yolox_loss(preds, origin, labels, batch, anchors, num_classes, max_labels, level_hw, strides, nlevels,
                       fg_mask, matched_gt, pred_iou, num_fg, losses, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+size_t yxh_reduce_workspace_bytes(int32_t channels) { return reduce_workspace(channels); }
+
+int yxh_bn_stats(int32_t dtype, int32_t batch, const yxh_src* y, const float* gamma, const float* beta,
+                 float* running_mean, float* running_var, float eps, float momentum, float* stats, void* workspace,
+                 size_t workspace_bytes, void* stream) {
+    return bn_stats(dtype, batch, y, gamma, beta, running_mean, running_var, eps, momentum, stats, workspace,
+                    workspace_bytes, (hipStream_t)stream);
+}
+
+int yxh_bn_act_fwd(int32_t dtype, int32_t batch, const yxh_src* y, const float* stats, int32_t act,
+                   const yxh_src* residual, const yxh_src* out, void* stream) {
+    return bn_act_fwd_launch(dtype, batch, y, stats, act, residual, out, (hipStream_t)stream);
+}
+
+int yxh_bn_act_bwd(int32_t dtype, int32_t batch, const yxh_src* y, const yxh_src* dout, const float* stats,
+                   const float* gamma, int32_t act, float* dgamma, float* dbeta, void* dx, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+    return bn_act_bwd_launch(dtype, batch, y, dout, stats, gamma, act, dgamma, dbeta, dx, workspace, workspace_bytes,
+                             (hipStream_t)stream);
+}
+
+int yxh_channel_sum(int32_t dtype, int32_t batch, const yxh_src* x, float* out, void* workspace,
+                    size_t workspace_bytes, void* stream) {
+    return channel_sum_launch(dtype, batch, x, out, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int yxh_conv_wgrad(const yxh_wgrad_desc* d, void* stream) { return conv_wgrad_launch(d, (hipStream_t)stream); }
+
+int yxh_pack_dgrad_weight(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, int32_t c_begin,
+                          int32_t c_count, int32_t cout_pad, int32_t dtype, void* out, void* stream) {
+    return pack_dgrad_launch(w, cout, cin, kh, kw, c_begin, c_count, cout_pad, dtype, out, (hipStream_t)stream);
+}
+
+int yxh_spp_bwd(int32_t dtype, int32_t batch, const yxh_src* cat, int32_t c, const float* dcat, float* dx,
+                void* stream) {
+    return spp_bwd_launch(dtype, batch, cat, c, dcat, dx, (hipStream_t)stream);
+}
+
+int yxh_upsample_bwd(const float* g, int32_t batch, int32_t h, int32_t w, int32_t c, float* dst, void* stream) {
+    return upsample_bwd_launch(g, batch, h, w, c, dst, (hipStream_t)stream);
+}
+
+int yxh_head_decode_train(const float* raw, int32_t batch, int32_t anchors, int32_t num_classes,
+                          const int32_t* level_hw, const int32_t* strides, int32_t nlevels, float* out, void* stream) {
+    return head_decode_train_launch(raw, batch, anchors, num_classes, level_hw, strides, nlevels, out,
+                                    (hipStream_t)stream);
+}
+
+int yxh_yolox_loss_bwd(const float* preds, const float* raw, const float* labels, int32_t batch, int32_t anchors,
+                       int32_t num_classes, int32_t max_labels, const int32_t* level_hw, const int32_t* strides,
+                       int32_t nlevels, const uint8_t* fg_mask, const int32_t* matched_gt, const float* pred_iou,
+                       const int32_t* num_fg, const float* grad_total, int32_t use_l1, int32_t dtype, void* g_regobj,
+                       void* g_cls, void* stream) {
+    return yolox_loss_bwd(preds, raw, labels, batch, anchors, num_classes, max_labels, level_hw, strides, nlevels,
+                          fg_mask, matched_gt, pred_iou, num_fg, grad_total, use_l1, dtype, g_regobj, g_cls,
+                          (hipStream_t)stream);
 }
 
 int yxh_run_ops(const yxh_op* ops, int32_t n, void* stream) {

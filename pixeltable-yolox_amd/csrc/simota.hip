@@ -332,8 +332,118 @@ __global__ void sim_finalize(const float* partial, int nparts, const int* num_fg
     losses[5] = d / fmaxf(ngt, 1.0f);      // num_fg / max(num_gts, 1)
 }
 
+
+// get_output_and_grid (yolo_head.py:213-231) on raw pred-conv outputs
+__global__ __launch_bounds__(256) void head_decode_train(const float* raw, int B, int A, int D, SimGeom geo,
+                                                        float* out) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)B * A * D) return;
+    const int ch = (int)(idx % D);
+    const int a = (int)((idx / D) % A);
+    float v = raw[idx];
+    if (ch < 4) {
+        float xs, ys, st;
+        anchor_geom(geo, a, xs, ys, st);
+        v = ch < 2 ? (v + (ch == 0 ? xs : ys)) * st : expf(v) * st;
+    }
+    out[idx] = v;
+}
+
+__device__ __forceinline__ float tie_w(float a, float b, bool want_greater) {
+    // torch.maximum / minimum backward: full gradient to the selected input, half on ties
+    if (a == b) return 0.5f;
+    return (want_greater ? a > b : a < b) ? 1.0f : 0.0f;
+}
+
+__device__ __forceinline__ float sgn(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
+
+// d total_loss / d raw outputs (autograd of yolo_head.py:382-402 + losses.py:13-51 through
+// the decode of :227-230); one thread per anchor.
+template <typename T>
+__global__ __launch_bounds__(256) void sim_loss_bwd(const float* preds, const float* raw, const float* labels, int B,
+                                                    int A, int C, int L, SimGeom geo, const uint8_t* fg,
+                                                    const int* matched, const float* piou, const int* num_fg,
+                                                    const float* gtot, int use_l1, T* g_ro, T* g_cls) {
+    const int b = blockIdx.y, a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= A) return;
+    int nfg = 0;
+    for (int q = 0; q < B; ++q) nfg += num_fg[q];
+    const float gs = gtot[0] / fmaxf((float)nfg, 1.0f);
+    const long long row = (long long)b * A + a;
+    const int D = 5 + C;
+    const float* p = preds + row * D;
+    const float* r = raw + row * D;
+    const bool f = fg[row];
+    float gr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    gr[4] = (sig(r[4]) - (f ? 1.0f : 0.0f)) * gs;
+    T* gc = g_cls + row * C;
+    if (!f) {
+        for (int c = 0; c < C; ++c) gc[c] = from_f32<T>(0.0f);
+    } else {
+        const int g = matched[row];
+        const float* gt = labels + ((long long)b * L + g) * 5;
+        const int k = (int)gt[0];
+        const float t = piou[row];
+        for (int c = 0; c < C; ++c) gc[c] = from_f32<T>((sig(r[5 + c]) - (c == k ? t : 0.0f)) * gs);
+        // IoU loss (reg_weight 5): L = 1 - iou^2
+        const float px = p[0], py = p[1], pw = p[2], ph = p[3];
+        const float atx = px - pw / 2, btx = gt[1] - gt[3] / 2, aty = py - ph / 2, bty = gt[2] - gt[4] / 2;
+        const float abx = px + pw / 2, bbx = gt[1] + gt[3] / 2, aby = py + ph / 2, bby = gt[2] + gt[4] / 2;
+        const float tlx = fmaxf(atx, btx), tly = fmaxf(aty, bty), brx = fminf(abx, bbx), bry = fminf(aby, bby);
+        const float en = (tlx < brx && tly < bry) ? 1.0f : 0.0f;
+        const float dxx = brx - tlx, dyy = bry - tly;
+        const float ai = (dxx * dyy) * en;
+        const float ap = pw * ph, ag = gt[3] * gt[4];
+        const float u = ((ap + ag) - ai) + 1e-16f;
+        const float io = ai / u;
+        const float gi = 5.0f * gs * (-2.0f * io);
+        const float gu = -gi * ai / (u * u);
+        const float gai = gi / u - gu;
+        const float gap = gu;
+        const float gdx = gai * en * dyy, gdy = gai * en * dxx;
+        const float gtlx = -gdx * tie_w(atx, btx, true), gbrx = gdx * tie_w(abx, bbx, false);
+        const float gtly = -gdy * tie_w(aty, bty, true), gbry = gdy * tie_w(aby, bby, false);
+        const float gpx = gtlx + gbrx, gpy = gtly + gbry;
+        const float gpw = 0.5f * (gbrx - gtlx) + gap * ph;
+        const float gph = 0.5f * (gbry - gtly) + gap * pw;
+        float xs, ys, st;
+        anchor_geom(geo, a, xs, ys, st);
+        gr[0] = gpx * st;
+        gr[1] = gpy * st;
+        gr[2] = gpw * st * expf(r[2]);
+        gr[3] = gph * st * expf(r[3]);
+        if (use_l1) {
+            const float t0 = gt[1] / st - xs, t1 = gt[2] / st - ys;
+            const float t2 = logf(gt[3] / st + 1e-8f), t3 = logf(gt[4] / st + 1e-8f);
+            gr[0] += sgn(r[0] - t0) * gs;
+            gr[1] += sgn(r[1] - t1) * gs;
+            gr[2] += sgn(r[2] - t2) * gs;
+            gr[3] += sgn(r[3] - t3) * gs;
+        }
+    }
+    T o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = from_f32<T>(gr[q]);
+    T* go = g_ro + row * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) go[q] = o[q];
+}
+
 // ------------------------------------------------------------------ host
 static size_t al(size_t n) { return (n + 255) & ~(size_t)255; }
+
+static SimGeom make_geom(const int* lhw, const int* strides, int nlev) {
+    SimGeom geo{};
+    geo.nlev = nlev;
+    geo.off[0] = 0;
+    for (int l = 0; l < nlev; ++l) {
+        geo.lh[l] = lhw[2 * l];
+        geo.lw[l] = lhw[2 * l + 1];
+        geo.stride[l] = strides[l];
+        geo.off[l + 1] = geo.off[l] + geo.lh[l] * geo.lw[l];
+    }
+    return geo;
+}
 
 size_t sim_workspace(int B, int A, int L) {
     const int nblk = (A + 255) / 256;
@@ -348,15 +458,7 @@ int yolox_loss(const float* preds, const float* origin, const float* labels, int
     YXH_CHECK_ARG(preds && labels && fg && matched && piou && num_fg && losses && lhw && strides, "null pointer");
     YXH_CHECK_ARG(B > 0 && A > 0 && C > 0 && L > 0 && nlev > 0 && nlev <= 4, "shape B=%d A=%d C=%d L=%d", B, A, C, L);
     YXH_CHECK_ARG(ws && ws_bytes >= sim_workspace(B, A, L), "workspace too small");
-    SimGeom geo{};
-    geo.nlev = nlev;
-    geo.off[0] = 0;
-    for (int l = 0; l < nlev; ++l) {
-        geo.lh[l] = lhw[2 * l];
-        geo.lw[l] = lhw[2 * l + 1];
-        geo.stride[l] = strides[l];
-        geo.off[l + 1] = geo.off[l] + geo.lh[l] * geo.lw[l];
-    }
+    SimGeom geo = make_geom(lhw, strides, nlev);
     YXH_CHECK_ARG(geo.off[nlev] == A, "level sizes sum to %d, not A=%d", geo.off[nlev], A);
     char* p = (char*)ws;
     auto take = [&](size_t bytes) {
@@ -394,6 +496,45 @@ int yolox_loss(const float* preds, const float* origin, const float* labels, int
     hipLaunchKernelGGL(sim_finalize, dim3(1), dim3(64), 0, st, w.partial, B * nblk, num_fg, labels, B, L,
                        origin ? 1 : 0, losses);
     YXH_CHECK_LAUNCH("sim_finalize");
+    return YXH_OK;
+}
+
+
+int head_decode_train_launch(const float* raw, int B, int A, int C, const int* lhw, const int* strides, int nlev,
+                             float* out, hipStream_t st) {
+    YXH_CHECK_ARG(raw && out && lhw && strides, "null pointer");
+    YXH_CHECK_ARG(B > 0 && A > 0 && C > 0 && nlev > 0 && nlev <= 4, "shape");
+    SimGeom geo = make_geom(lhw, strides, nlev);
+    YXH_CHECK_ARG(geo.off[nlev] == A, "level sizes sum to %d, not A=%d", geo.off[nlev], A);
+    const long long total = (long long)B * A * (5 + C);
+    hipLaunchKernelGGL(head_decode_train, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, raw, B, A, 5 + C,
+                       geo, out);
+    YXH_CHECK_LAUNCH("head_decode_train");
+    return YXH_OK;
+}
+
+int yolox_loss_bwd(const float* preds, const float* raw, const float* labels, int B, int A, int C, int L,
+                   const int* lhw, const int* strides, int nlev, const uint8_t* fg, const int* matched,
+                   const float* piou, const int* num_fg, const float* gtot, int use_l1, int dt, void* g_ro,
+                   void* g_cls, hipStream_t st) {
+    YXH_CHECK_ARG(preds && raw && labels && fg && matched && piou && num_fg && gtot && g_ro && g_cls && lhw && strides,
+                  "null pointer");
+    YXH_CHECK_ARG(B > 0 && A > 0 && C > 0 && L > 0 && nlev > 0 && nlev <= 4, "shape");
+    SimGeom geo = make_geom(lhw, strides, nlev);
+    YXH_CHECK_ARG(geo.off[nlev] == A, "level sizes sum to %d, not A=%d", geo.off[nlev], A);
+    dim3 grid((A + 255) / 256, B);
+#define YXH_LB(T)                                                                                                    \
+    hipLaunchKernelGGL(sim_loss_bwd<T>, grid, dim3(256), 0, st, preds, raw, labels, B, A, C, L, geo, fg, matched,  \
+                       piou, num_fg, gtot, use_l1, (T*)g_ro, (T*)g_cls)
+    if (dt == YXH_BF16) YXH_LB(bf16);
+    else if (dt == YXH_F16) YXH_LB(f16);
+    else if (dt == YXH_F32) YXH_LB(float);
+    else {
+        set_error("loss_bwd dtype %d", dt);
+        return YXH_EINVAL;
+    }
+#undef YXH_LB
+    YXH_CHECK_LAUNCH("sim_loss_bwd");
     return YXH_OK;
 }
 

@@ -1,0 +1,830 @@
+// Training-side kernels of the YOLOX hot path on gfx950 (MI355X): everything the
+// backward pass of YoloxModule needs besides the data-gradient convolutions (those
+// run on the forward conv kernels with transposed/flipped weights, yxh_pack_dgrad_weight,
+// and a zero-dilated source for stride 2).
+//
+//  bn_stats        : BatchNorm2d training statistics (network_blocks.py:44-49 BaseConv.bn,
+//                    eps/momentum from config.py:162-166): per-channel shifted sums in a
+//                    fixed-order two-stage reduction, then mean / invstd / folded
+//                    scale+shift and the running-stat update (unbiased var, momentum).
+//  bn_act_fwd      : y*scale+shift -> act (SiLU/ReLU/LReLU) (+ Bottleneck residual,
+//                    network_blocks.py:97-99) into a channel-slice view.
+//  bn_act_bwd      : act' and BatchNorm backward: dgamma = sum dz*xhat, dbeta = sum dz,
+//                    dx = gamma*invstd*(dz - dbeta/M - xhat*dgamma/M).
+//  conv_wgrad      : dW[n][c][ky][kx] = sum_pixels dY[n] * X[c](tap) on MFMA: both
+//                    operands are pixel-major (NHWC), so the loader transposes 16-byte
+//                    chunks in registers (v_perm) and the LDS image is the forward
+//                    kernel's [K chunk][row] layout with K = pixels; split over pixel
+//                    ranges, fp32 atomics into the weight gradient.
+//  spp_bwd         : max_pool2d(5/9/13, s1) backward (first max in row-major scan, as
+//                    torch) + the identity branch of SPPBottleneck's concat.
+//  upsample_bwd    : nn.Upsample(nearest x2) backward (2x2 sums), accumulated.
+//  channel_sum     : bias gradients of the head's pred convs.
+#include "conv_common.hpp"
+
+namespace yxh {
+
+// A strided NHWC view (yxh_src): pixel m = b*HW + pix -> b*bs + pix*cs elements.
+struct TView {
+    const void* ptr;
+    int C, cs, HW;
+    long long bs;
+};
+
+__device__ __forceinline__ long long vofs(const TView& v, int m) {
+    const int b = m / v.HW, pix = m - b * v.HW;
+    return (long long)b * v.bs + (long long)pix * v.cs;
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void load_f(const T* p, float (&o)[N]) {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int q = 0; q < N; q += 4) {
+            const float4 u = *(const float4*)(p + q);
+            o[q] = u.x; o[q + 1] = u.y; o[q + 2] = u.z; o[q + 3] = u.w;
+        }
+    } else {
+        static_assert(N % 8 == 0, "16-bit chunks");
+#pragma unroll
+        for (int q = 0; q < N; q += 8) {
+            const uint4 u = *(const uint4*)(p + q);
+            T t[8];
+            __builtin_memcpy(t, &u, 16);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[q + e] = to_f32(t[e]);
+        }
+    }
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void store_f(T* p, const float (&o)[N]) {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int q = 0; q < N; q += 4) *(float4*)(p + q) = make_float4(o[q], o[q + 1], o[q + 2], o[q + 3]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < N; q += 8) {
+            T t[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) t[e] = from_f32<T>(o[q + e]);
+            uint4 u;
+            __builtin_memcpy(&u, t, 16);
+            *(uint4*)(p + q) = u;
+        }
+    }
+}
+
+// d act(z) / dz
+template <bool PRECISE>
+__device__ __forceinline__ float act_grad(float z, int act) {
+    switch (act) {
+        case YXH_ACT_SILU: {
+            const float s = 1.0f / (1.0f + (PRECISE ? expf(-z) : __expf(-z)));
+            return s * (1.0f + z * (1.0f - s));
+        }
+        case YXH_ACT_RELU: return z > 0.0f ? 1.0f : 0.0f;
+        case YXH_ACT_LRELU: return z > 0.0f ? 1.0f : 0.1f;
+        default: return 1.0f;
+    }
+}
+
+// ------------------------------------------------------------------ reductions
+// Stage 1: block b reduces rows [b*rpb, (b+1)*rpb) into partial[b][2][C].
+// Thread = (row lane, channel chunk of EPC channels); rows stride by the row lanes.
+enum { RED_STATS = 0, RED_BWD = 1, RED_SUM = 2 };
+
+struct RedArgs {
+    TView x;          // activation (T): y for STATS/BWD, x for SUM
+    TView g;          // fp32 gradient (BWD)
+    const float* st;  // stats [4][C] = mean, invstd, scale, shift (BWD)
+    int act, M, rpb;
+    float* partial;
+};
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void chan_reduce(RedArgs a) {
+    constexpr int EPC = Chunk<T>::N;
+    __shared__ float red[2][256 * EPC];
+    const int C = a.x.C, nch = C / EPC;
+    const int tid = threadIdx.x;
+    const int q = tid % nch, rl = tid / nch, rpi = 256 / nch;
+    float s1[EPC], s2[EPC], sh[EPC];
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) s1[e] = s2[e] = sh[e] = 0.0f;
+    const int c0 = q * EPC;
+    const T* xp = (const T*)a.x.ptr;
+    if (MODE == RED_STATS && rl < rpi) {
+        load_f<T, EPC>(xp + c0, sh);  // shift = pixel 0 (cancellation guard)
+        if (blockIdx.x == 0 && rl == 0)
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) a.partial[(long long)gridDim.x * 2 * C + c0 + e] = sh[e];
+    }
+    float sc[EPC], sf[EPC], mu[EPC], is[EPC];
+    if (MODE == RED_BWD) {
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+            mu[e] = a.st[c0 + e];
+            is[e] = a.st[C + c0 + e];
+            sc[e] = a.st[2 * C + c0 + e];
+            sf[e] = a.st[3 * C + c0 + e];
+        }
+    }
+    const int r0 = blockIdx.x * a.rpb, r1 = min(a.M, r0 + a.rpb);
+    if (rl < rpi) {
+        for (int r = r0 + rl; r < r1; r += rpi) {
+            float v[EPC];
+            load_f<T, EPC>(xp + vofs(a.x, r) + c0, v);
+            if (MODE == RED_STATS) {
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) {
+                    const float d = v[e] - sh[e];
+                    s1[e] += d;
+                    s2[e] += d * d;
+                }
+            } else if (MODE == RED_SUM) {
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) s1[e] += v[e];
+            } else {
+                float gv[EPC];
+                load_f<float, EPC>((const float*)a.g.ptr + vofs(a.g, r) + c0, gv);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) {
+                    const float z = v[e] * sc[e] + sf[e];
+                    const float dz = gv[e] * act_grad<sizeof(T) == 4>(z, a.act);
+                    s1[e] += dz;
+                    s2[e] += dz * ((v[e] - mu[e]) * is[e]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+        red[0][tid * EPC + e] = s1[e];
+        red[1][tid * EPC + e] = s2[e];
+    }
+    __syncthreads();
+    // thread t < C sums channel t over the row lanes (fixed order: deterministic)
+    for (int c = tid; c < C; c += 256) {
+        const int qq = c / EPC, e = c - qq * EPC;
+        float t1 = 0.0f, t2 = 0.0f;
+        for (int l = 0; l < rpi; ++l) {
+            t1 += red[0][(l * nch + qq) * EPC + e];
+            t2 += red[1][(l * nch + qq) * EPC + e];
+        }
+        a.partial[((long long)blockIdx.x * 2) * C + c] = t1;
+        a.partial[((long long)blockIdx.x * 2 + 1) * C + c] = t2;
+    }
+}
+
+struct FinArgs {
+    const float* partial;  // [nblk][2][C] (+ [C] shift row for STATS)
+    int nblk, C, M, mode;
+    const float *gamma, *beta;
+    float *rmean, *rvar;
+    float eps, momentum;
+    float* stats;        // STATS out [4][C] = mean, invstd, scale, shift
+    float *out0, *out1;  // BWD: dgamma, dbeta; SUM: out0
+};
+
+__global__ __launch_bounds__(256) void chan_finalize(FinArgs f) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= f.C) return;
+    double t1 = 0.0, t2 = 0.0;
+    for (int b = 0; b < f.nblk; ++b) {
+        t1 += f.partial[((long long)b * 2) * f.C + c];
+        t2 += f.partial[((long long)b * 2 + 1) * f.C + c];
+    }
+    if (f.mode == RED_STATS) {
+        const double m1 = t1 / f.M;
+        const double mean = (double)f.partial[(long long)f.nblk * 2 * f.C + c] + m1;
+        double var = t2 / f.M - m1 * m1;
+        if (var < 0) var = 0;
+        const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+        const float g = f.gamma ? f.gamma[c] : 1.0f, be = f.beta ? f.beta[c] : 0.0f;
+        const float scale = g * invstd;
+        f.stats[c] = (float)mean;
+        f.stats[f.C + c] = invstd;
+        f.stats[2 * f.C + c] = scale;
+        f.stats[3 * f.C + c] = be - (float)mean * scale;
+        if (f.rmean) {
+            const float mo = f.momentum;
+            f.rmean[c] = (1.0f - mo) * f.rmean[c] + mo * (float)mean;
+            const double unb = f.M > 1 ? var * f.M / (f.M - 1) : var;
+            f.rvar[c] = (1.0f - mo) * f.rvar[c] + mo * (float)unb;
+        }
+    } else if (f.mode == RED_BWD) {
+        f.out0[c] = (float)t2;  // dgamma = sum dz * xhat
+        f.out1[c] = (float)t1;  // dbeta = sum dz
+    } else {
+        f.out0[c] = (float)t1;
+    }
+}
+
+// ------------------------------------------------------------------ elementwise
+template <typename T>
+__global__ __launch_bounds__(256) void bn_act_fwd(TView y, const float* st, int act, TView res, TView out, int M) {
+    constexpr int EPC = Chunk<T>::N;
+    const int C = y.C, nch = C / EPC;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)M * nch) return;
+    const int m = (int)(idx / nch), c0 = (int)(idx - (long long)m * nch) * EPC;
+    float v[EPC];
+    load_f<T, EPC>((const T*)y.ptr + vofs(y, m) + c0, v);
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) v[e] = apply_act<sizeof(T) == 4>(v[e] * st[2 * C + c0 + e] + st[3 * C + c0 + e], act);
+    if (res.ptr) {
+        float r[EPC];
+        load_f<T, EPC>((const T*)res.ptr + vofs(res, m) + c0, r);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) v[e] += r[e];
+    }
+    store_f<T, EPC>((T*)out.ptr + vofs(out, m) + c0, v);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_act_bwd_apply(TView y, TView g, const float* st, const float* gamma,
+                                                       const float* dgamma, const float* dbeta, int act, int M,
+                                                       T* dx) {
+    constexpr int EPC = Chunk<T>::N;
+    const int C = y.C, nch = C / EPC;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)M * nch) return;
+    const int m = (int)(idx / nch), c0 = (int)(idx - (long long)m * nch) * EPC;
+    float v[EPC], gv[EPC], o[EPC];
+    load_f<T, EPC>((const T*)y.ptr + vofs(y, m) + c0, v);
+    load_f<float, EPC>((const float*)g.ptr + vofs(g, m) + c0, gv);
+    const float inv_m = 1.0f / (float)M;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+        const int c = c0 + e;
+        const float mu = st[c], is = st[C + c];
+        const float z = v[e] * st[2 * C + c] + st[3 * C + c];
+        const float dz = gv[e] * act_grad<sizeof(T) == 4>(z, act);
+        const float xh = (v[e] - mu) * is;
+        const float gm = gamma ? gamma[c] : 1.0f;
+        o[e] = (gm * is) * ((dz - dbeta[c] * inv_m) - xh * (dgamma[c] * inv_m));
+    }
+    store_f<T, EPC>(dx + (long long)m * C + c0, o);
+}
+
+// ------------------------------------------------------------------ weight gradient
+struct WgradParams {
+    int in_h, in_w, out_h, out_w, cin, cout, kh, kw, stride, pad, ohw, M;
+    int nsrc, src0_ch;
+    const void* sptr[2];
+    int scs[2], sw[2], sup[2];
+    long long sbs[2];
+    const void* dy;
+    int dycs;
+    long long dybs;
+    float* dw;
+    int cin_store;
+    int sps, nst;  // stages per split, total pixel stages
+    int ntc;       // channel tiles per tap
+};
+
+// In-register transpose of an EPC x EPC block of T: a[e] = EPC channels of pixel e ->
+// a[j] = EPC pixels of channel j.
+__device__ __forceinline__ void transpose_chunks(uint4 (&a)[8]) {  // 16-bit elements
+    uint32_t w[8][4];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        w[e][0] = a[e].x; w[e][1] = a[e].y; w[e][2] = a[e].z; w[e][3] = a[e].w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = __builtin_amdgcn_perm(w[2 * q + 1][j >> 1], w[2 * q][j >> 1], sel);
+        a[j] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+__device__ __forceinline__ void transpose_chunks(uint4 (&a)[4]) {  // 32-bit elements
+    uint4 b[4];
+    b[0] = make_uint4(a[0].x, a[1].x, a[2].x, a[3].x);
+    b[1] = make_uint4(a[0].y, a[1].y, a[2].y, a[3].y);
+    b[2] = make_uint4(a[0].z, a[1].z, a[2].z, a[3].z);
+    b[3] = make_uint4(a[0].w, a[1].w, a[2].w, a[3].w);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = b[j];
+}
+
+template <typename T, int TN, int TM, int WR, int WC, int KS>
+__global__ __launch_bounds__(256) void conv_wgrad(WgradParams p) {
+    constexpr int EPC = Chunk<T>::N;
+    constexpr int CPR = 4 * KS;           // 16-byte chunks (of EPC pixels) per row per stage
+    constexpr int KP = CPR * EPC;         // pixels per stage
+    constexpr int NA = (TN / EPC) * CPR;  // transpose items: A = dY rows (cout)
+    constexpr int NB = (TM / EPC) * CPR;  //                  B = X rows (cin of the tap)
+    constexpr int NIT = (NA + NB + 255) / 256;
+    constexpr int WTN = TN / WR, WTM = TM / WC;
+    constexpr int FR = WTN / 16, FC = WTM / 16;
+    constexpr int A_BYTES = TN * CPR * 16, B_BYTES = TM * CPR * 16;
+    constexpr int BUF = A_BYTES + B_BYTES;
+    static_assert(WR * WC == 4 && FR >= 1 && FC >= 1, "tile");
+    __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / WC, wc = wave % WC;
+    const int n0 = blockIdx.y * TN;
+    const int tap = blockIdx.z / p.ntc, c0 = (blockIdx.z - tap * p.ntc) * TM;
+    const int ky = tap / p.kw, kx = tap - ky * p.kw;
+    const int st0 = blockIdx.x * p.sps, st1 = min(p.nst, st0 + p.sps);
+
+    uint4 rg[NIT][EPC];
+    auto gload = [&](int stg) {
+        const int pbase = stg * KP;
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            const int it = tid + 256 * i;
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) rg[i][e] = make_uint4(0, 0, 0, 0);
+            if (it < NA) {
+                const int ci = it % (TN / EPC), pc = it / (TN / EPC);
+                const int n = n0 + ci * EPC;
+                if (n < p.cout) {
+#pragma unroll
+                    for (int e = 0; e < EPC; ++e) {
+                        const int m = pbase + pc * EPC + e;
+                        if (m < p.M) {
+                            const int b = m / p.ohw, pix = m - b * p.ohw;
+                            rg[i][e] = *(const uint4*)((const T*)p.dy + (long long)b * p.dybs +
+                                                       (long long)pix * p.dycs + n);
+                        }
+                    }
+                }
+            } else if (it < NA + NB) {
+                const int jt = it - NA;
+                const int ci = jt % (TM / EPC), pc = jt / (TM / EPC);
+                int c = c0 + ci * EPC;
+                if (c < p.cin) {
+                    int s = 0;
+                    if (p.nsrc == 2 && c >= p.src0_ch) {
+                        s = 1;
+                        c -= p.src0_ch;
+                    }
+                    const T* sp = (const T*)p.sptr[s];
+                    const int up = p.sup[s];
+#pragma unroll
+                    for (int e = 0; e < EPC; ++e) {
+                        const int m = pbase + pc * EPC + e;
+                        if (m < p.M) {
+                            const int b = m / p.ohw, pix = m - b * p.ohw;
+                            const int oy = pix / p.out_w, ox = pix - oy * p.out_w;
+                            const int iy = oy * p.stride - p.pad + ky, ix = ox * p.stride - p.pad + kx;
+                            if (iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w)
+                                rg[i][e] = *(const uint4*)(sp + (long long)b * p.sbs[s] +
+                                                           ((long long)(iy >> up) * p.sw[s] + (ix >> up)) * p.scs[s] +
+                                                           c);
+                        }
+                    }
+                }
+            }
+        }
+    };
+    auto lstore = [&](int buf) {
+        char* A = smem + buf * BUF;
+        char* B = A + A_BYTES;
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            const int it = tid + 256 * i;
+            if (it >= NA + NB) continue;
+            transpose_chunks(rg[i]);
+            const bool isa = it < NA;
+            const int jt = isa ? it : it - NA;
+            const int rows = isa ? TN : TM;
+            const int ci = jt % (rows / EPC), pc = jt / (rows / EPC);
+            const int sw_ = 2 * (pc & 3) + (pc >> 2);
+            char* base = isa ? A : B;
+#pragma unroll
+            for (int j = 0; j < EPC; ++j) {
+                const int r = ci * EPC + j;
+                *(uint4*)(base + (pc * rows + (r ^ sw_)) * 16) = rg[i][j];
+            }
+        }
+    };
+
+    f32x4 acc[FR][FC];
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int frow = lane & 15, fq = lane >> 4;
+    auto compute = [&](int buf) {
+        const char* A = smem + buf * BUF;
+        const char* B = A + A_BYTES;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int chunk = s * 4 + fq, sw_ = 2 * fq + s;
+            uint4 af[FR], bf[FC];
+#pragma unroll
+            for (int i = 0; i < FR; ++i) af[i] = *(const uint4*)(A + (chunk * TN + ((wr * WTN + i * 16 + frow) ^ sw_)) * 16);
+#pragma unroll
+            for (int j = 0; j < FC; ++j) bf[j] = *(const uint4*)(B + (chunk * TM + ((wc * WTM + j * 16 + frow) ^ sw_)) * 16);
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], af[i], bf[j]);
+        }
+    };
+
+    if (st0 < st1) {
+        gload(st0);
+        lstore(0);
+        __syncthreads();
+        for (int k = st0; k < st1; ++k) {
+            const int cur = (k - st0) & 1;
+            if (k + 1 < st1) gload(k + 1);
+            compute(cur);
+            if (k + 1 < st1) lstore(cur ^ 1);
+            __syncthreads();
+        }
+    }
+    // dW (torch layout [cout][cin_store][kh][kw]) += acc
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+            const int c = c0 + wc * WTM + j * 16 + frow;
+            if (c >= p.cin_store) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n0 + wr * WTN + i * 16 + fq * 4 + r;
+                if (n < p.cout)
+                    atomicAdd(p.dw + (((long long)n * p.cin_store + c) * p.kh + ky) * p.kw + kx, acc[i][j][r]);
+            }
+        }
+}
+
+// dgrad weights: w [cout][cin][kh][kw] fp32 -> [c_count][kh][kw][cout_pad] of T, taps
+// flipped (ky -> kh-1-ky), input channels [c_begin, c_begin + c_count).
+template <typename T>
+__global__ __launch_bounds__(256) void pack_dgrad(const float* w, int cout, int cin, int kh, int kw, int c_begin,
+                                                  int c_count, int cout_pad, T* out) {
+    const long long total = (long long)c_count * kh * kw * cout_pad;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int n = (int)(idx % cout_pad);
+    const int t = (int)((idx / cout_pad) % (kh * kw));
+    const int c = (int)(idx / ((long long)cout_pad * kh * kw));
+    const int ky = t / kw, kx = t - ky * kw;
+    float v = 0.0f;
+    if (n < cout) v = w[(((long long)n * cin + c_begin + c) * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx)];
+    out[idx] = from_f32<T>(v);
+}
+
+// ------------------------------------------------------------------ SPP / upsample backward
+// One thread per (pixel, channel) of the SPP input x (channels [0, c) of `cat`):
+// every pool output whose window holds this pixel checks whether its argmax (first
+// maximum, row-major scan, -inf padding) is this pixel.  dx = dcat[:, :c] + those.
+template <typename T>
+__global__ __launch_bounds__(256) void spp_bwd(TView cat, int H, int W, int c, const float* dcat, float* dx,
+                                               int B) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long total = (long long)B * H * W * c;
+    if (idx >= total) return;
+    const int ch = (int)(idx % c);
+    const long long m = idx / c;
+    const int b = (int)(m / (H * W)), pix = (int)(m - (long long)b * H * W);
+    const int y = pix / W, x = pix - y * W;
+    const T* xb = (const T*)cat.ptr + (long long)b * cat.bs;
+    const float* db = dcat + (long long)b * H * W * 4 * c;
+    float g = db[(long long)pix * 4 * c + ch];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int r = 2 + 2 * k;  // 5, 9, 13
+        for (int oy = max(0, y - r); oy <= min(H - 1, y + r); ++oy)
+            for (int ox = max(0, x - r); ox <= min(W - 1, x + r); ++ox) {
+                // argmax of output (oy, ox)'s window
+                float best = -INFINITY;
+                int by = -1, bx = -1;
+                for (int iy = max(0, oy - r); iy <= min(H - 1, oy + r); ++iy)
+                    for (int ix = max(0, ox - r); ix <= min(W - 1, ox + r); ++ix) {
+                        const float v = to_f32(xb[((long long)iy * W + ix) * cat.cs + ch]);
+                        if (v > best || by < 0) {
+                            best = v;
+                            by = iy;
+                            bx = ix;
+                        }
+                    }
+                if (by == y && bx == x) g += db[((long long)oy * W + ox) * 4 * c + (k + 1) * c + ch];
+            }
+    }
+    dx[m * c + ch] = g;
+}
+
+__global__ __launch_bounds__(256) void upsample_bwd(const float* g, int B, int h, int w, int C, float* dst) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int nc4 = C / 4;
+    if (idx >= (long long)B * h * w * nc4) return;
+    const int c = (int)(idx % nc4) * 4;
+    const long long m = idx / nc4;
+    const int b = (int)(m / ((long long)h * w)), pix = (int)(m - (long long)b * h * w);
+    const int y = pix / w, x = pix - y * w;
+    const float* gb = g + (long long)b * 4 * h * w * C;
+    float4 s = *(float4*)(dst + m * C + c);
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+            const float4 u = *(const float4*)(gb + ((long long)(2 * y + dy) * 2 * w + 2 * x + dx) * C + c);
+            s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
+        }
+    *(float4*)(dst + m * C + c) = s;
+}
+
+// ================================================================== host
+namespace {
+
+int esz(int dt) { return dt == YXH_F32 ? 4 : 2; }
+
+TView tview(const yxh_src* s, int C) {
+    TView v;
+    v.ptr = s ? s->ptr : nullptr;
+    v.C = C;
+    v.cs = s ? s->cstride : 0;
+    v.HW = s ? s->h * s->w : 1;
+    v.bs = s ? s->bstride : 0;
+    return v;
+}
+
+bool a16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int check_view(const yxh_src* s, int dt, const char* what) {
+    YXH_CHECK_ARG(s && s->ptr, "%s: null view", what);
+    const int epc = 16 / esz(dt);
+    YXH_CHECK_ARG(a16(s->ptr) && s->channels > 0 && s->channels % epc == 0 && s->cstride % epc == 0 &&
+                      s->bstride % epc == 0 && s->h > 0 && s->w > 0,
+                  "%s: view not 16-byte aligned / chunked (channels %d, cstride %d)", what, s->channels, s->cstride);
+    return YXH_OK;
+}
+
+constexpr int kRedMaxBlocks = 1024;
+
+int red_blocks(int M, int C, int dt, int* rpb) {
+    const int nch = C / (16 / esz(dt));
+    const int rpi = nch >= 256 ? 1 : 256 / nch;
+    int nblk = (int)(((long long)M + rpi * 16 - 1) / (rpi * 16));  // ~16 rows per thread
+    nblk = nblk < 1 ? 1 : (nblk > kRedMaxBlocks ? kRedMaxBlocks : nblk);
+    *rpb = (M + nblk - 1) / nblk;
+    return (M + *rpb - 1) / *rpb;
+}
+
+template <int MODE>
+int launch_reduce(int dt, const RedArgs& a, int nblk, hipStream_t st) {
+    if (dt == YXH_BF16) hipLaunchKernelGGL((chan_reduce<bf16, MODE>), dim3(nblk), dim3(256), 0, st, a);
+    else if (dt == YXH_F16) hipLaunchKernelGGL((chan_reduce<f16, MODE>), dim3(nblk), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((chan_reduce<float, MODE>), dim3(nblk), dim3(256), 0, st, a);
+    YXH_CHECK_LAUNCH("chan_reduce");
+    return YXH_OK;
+}
+
+}  // namespace
+
+size_t reduce_workspace(int C) { return (size_t)(kRedMaxBlocks * 2 + 1) * C * sizeof(float); }
+
+namespace {
+
+int run_reduce(int mode, int dt, int B, const yxh_src* x, const yxh_src* g, const float* stats, int act,
+               void* ws, size_t ws_bytes, FinArgs f, hipStream_t st) {
+    const int C = x->channels;
+    YXH_CHECK_ARG(B > 0, "batch %d", B);
+    YXH_CHECK_ARG(C / (16 / esz(dt)) <= 256, "reduction: %d channels exceed one block's chunks", C);
+    YXH_CHECK_ARG(ws && ws_bytes >= reduce_workspace(C), "reduction workspace too small");
+    RedArgs a{};
+    a.x = tview(x, C);
+    a.g = tview(g, C);
+    a.st = stats;
+    a.act = act;
+    const long long M = (long long)B * x->h * x->w;
+    YXH_CHECK_ARG(M < (1LL << 31), "too many pixels");
+    a.M = (int)M;
+    const int nblk = red_blocks(a.M, C, dt, &a.rpb);
+    a.partial = (float*)ws;
+    int rc = mode == RED_STATS ? launch_reduce<RED_STATS>(dt, a, nblk, st)
+             : mode == RED_BWD ? launch_reduce<RED_BWD>(dt, a, nblk, st)
+                               : launch_reduce<RED_SUM>(dt, a, nblk, st);
+    if (rc) return rc;
+    f.partial = (const float*)ws;
+    f.nblk = nblk;
+    f.C = C;
+    f.M = a.M;
+    f.mode = mode;
+    hipLaunchKernelGGL(chan_finalize, dim3((C + 255) / 256), dim3(256), 0, st, f);
+    YXH_CHECK_LAUNCH("chan_finalize");
+    return YXH_OK;
+}
+
+}  // namespace
+
+int bn_stats(int dt, int B, const yxh_src* y, const float* gamma, const float* beta, float* rmean, float* rvar,
+             float eps, float momentum, float* stats, void* ws, size_t ws_bytes, hipStream_t st) {
+    if (int rc = check_view(y, dt, "bn_stats y")) return rc;
+    YXH_CHECK_ARG(stats, "bn_stats: null stats");
+    YXH_CHECK_ARG(!rmean == !rvar, "running mean/var must both be given or both NULL");
+    FinArgs f{};
+    f.gamma = gamma;
+    f.beta = beta;
+    f.rmean = rmean;
+    f.rvar = rvar;
+    f.eps = eps;
+    f.momentum = momentum;
+    f.stats = stats;
+    return run_reduce(RED_STATS, dt, B, y, nullptr, nullptr, 0, ws, ws_bytes, f, st);
+}
+
+int bn_act_fwd_launch(int dt, int B, const yxh_src* y, const float* stats, int act, const yxh_src* res,
+                      const yxh_src* out, hipStream_t st) {
+    if (int rc = check_view(y, dt, "bn_act_fwd y")) return rc;
+    if (int rc = check_view(out, dt, "bn_act_fwd out")) return rc;
+    if (res && res->ptr)
+        if (int rc = check_view(res, dt, "bn_act_fwd residual")) return rc;
+    const int C = y->channels;
+    YXH_CHECK_ARG(out->channels == C && out->h == y->h && out->w == y->w, "bn_act_fwd: out view shape");
+    YXH_CHECK_ARG(!res || !res->ptr || (res->channels == C && res->h == y->h && res->w == y->w),
+                  "bn_act_fwd: residual view shape");
+    YXH_CHECK_ARG(stats && B > 0, "bn_act_fwd: stats / batch");
+    const long long M = (long long)B * y->h * y->w;
+    const long long total = M * (C / (16 / esz(dt)));
+    TView r = tview(res && res->ptr ? res : nullptr, C);
+    dim3 grid((unsigned)((total + 255) / 256));
+#define YXH_BNF(T) hipLaunchKernelGGL(bn_act_fwd<T>, grid, dim3(256), 0, st, tview(y, C), stats, act, r, tview(out, C), (int)M)
+    if (dt == YXH_BF16) YXH_BNF(bf16);
+    else if (dt == YXH_F16) YXH_BNF(f16);
+    else YXH_BNF(float);
+#undef YXH_BNF
+    YXH_CHECK_LAUNCH("bn_act_fwd");
+    return YXH_OK;
+}
+
+int bn_act_bwd_launch(int dt, int B, const yxh_src* y, const yxh_src* dout, const float* stats, const float* gamma,
+                      int act, float* dgamma, float* dbeta, void* dx, void* ws, size_t ws_bytes, hipStream_t st) {
+    if (int rc = check_view(y, dt, "bn_act_bwd y")) return rc;
+    if (int rc = check_view(dout, YXH_F32, "bn_act_bwd dout")) return rc;
+    const int C = y->channels;
+    YXH_CHECK_ARG(dout->channels == C && dout->h == y->h && dout->w == y->w, "bn_act_bwd: dout view shape");
+    YXH_CHECK_ARG(stats && dgamma && dbeta && dx && a16(dx), "bn_act_bwd: null / unaligned outputs");
+    FinArgs f{};
+    f.out0 = dgamma;
+    f.out1 = dbeta;
+    if (int rc = run_reduce(RED_BWD, dt, B, y, dout, stats, act, ws, ws_bytes, f, st)) return rc;
+    const long long M = (long long)B * y->h * y->w;
+    const long long total = M * (C / (16 / esz(dt)));
+    dim3 grid((unsigned)((total + 255) / 256));
+#define YXH_BNB(T)                                                                                                 \
+    hipLaunchKernelGGL(bn_act_bwd_apply<T>, grid, dim3(256), 0, st, tview(y, C), tview(dout, C), stats, gamma,   \
+                       dgamma, dbeta, act, (int)M, (T*)dx)
+    if (dt == YXH_BF16) YXH_BNB(bf16);
+    else if (dt == YXH_F16) YXH_BNB(f16);
+    else YXH_BNB(float);
+#undef YXH_BNB
+    YXH_CHECK_LAUNCH("bn_act_bwd_apply");
+    return YXH_OK;
+}
+
+int channel_sum_launch(int dt, int B, const yxh_src* x, float* out, void* ws, size_t ws_bytes, hipStream_t st) {
+    if (int rc = check_view(x, dt, "channel_sum x")) return rc;
+    YXH_CHECK_ARG(out, "channel_sum: null out");
+    FinArgs f{};
+    f.out0 = out;
+    return run_reduce(RED_SUM, dt, B, x, nullptr, nullptr, 0, ws, ws_bytes, f, st);
+}
+
+namespace {
+
+template <typename T, int TN, int TM, int WR, int WC, int KS>
+int launch_wgrad_t(WgradParams p, hipStream_t st) {
+    constexpr int EPC = Chunk<T>::N;
+    constexpr int KP = 4 * KS * EPC;
+    const int ntn = (p.cout + TN - 1) / TN;
+    p.ntc = (p.cin + TM - 1) / TM;
+    const int ntap = p.kh * p.kw;
+    p.nst = (p.M + KP - 1) / KP;
+    // ~2 blocks per CU over the whole grid; at least 8 stages per split
+    const long long tiles = (long long)ntn * ntap * p.ntc;
+    long long splits = (512 + tiles - 1) / tiles;
+    const long long max_splits = (p.nst + 7) / 8;
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    p.sps = (int)((p.nst + splits - 1) / splits);
+    splits = (p.nst + p.sps - 1) / p.sps;
+    YXH_CHECK_ARG(ntap * p.ntc < 65536 && ntn < 65536, "wgrad grid");
+    hipLaunchKernelGGL((conv_wgrad<T, TN, TM, WR, WC, KS>), dim3((unsigned)splits, ntn, ntap * p.ntc), dim3(256), 0,
+                       st, p);
+    YXH_CHECK_LAUNCH("conv_wgrad");
+    return YXH_OK;
+}
+
+template <typename T>
+int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
+    // default: 64 x 64 (cout x cin), 2 x 2 waves; 4 slabs (bf16: 128 pixels) per stage
+    switch (tile) {
+        case 0:
+        case 1: return sizeof(T) == 4 ? launch_wgrad_t<T, 64, 64, 2, 2, 2>(p, st) : launch_wgrad_t<T, 64, 64, 2, 2, 4>(p, st);
+        case 2: return launch_wgrad_t<T, 128, 128, 2, 2, 2>(p, st);
+        case 3: return launch_wgrad_t<T, 32, 64, 1, 4, 2>(p, st);
+        case 4: return launch_wgrad_t<T, 16, 64, 1, 4, 2>(p, st);
+        default: set_error("wgrad tile %d", tile); return YXH_EINVAL;
+    }
+}
+
+}  // namespace
+
+int conv_wgrad_launch(const yxh_wgrad_desc* d, hipStream_t st) {
+    YXH_CHECK_ARG(d, "null descriptor");
+    const int dt = d->dtype;
+    YXH_CHECK_ARG(dt == YXH_F32 || dt == YXH_BF16 || dt == YXH_F16, "wgrad dtype %d", dt);
+    const int epc = 16 / esz(dt);
+    YXH_CHECK_ARG(d->batch > 0 && d->cin > 0 && d->cout > 0 && d->kh > 0 && d->kw > 0 && d->stride > 0,
+                  "wgrad geometry");
+    YXH_CHECK_ARG((d->in_h + 2 * d->pad - d->kh) / d->stride + 1 == d->out_h &&
+                      (d->in_w + 2 * d->pad - d->kw) / d->stride + 1 == d->out_w,
+                  "wgrad output size mismatch");
+    YXH_CHECK_ARG(d->nsrc == 1 || d->nsrc == 2, "nsrc %d", d->nsrc);
+    int chs = 0;
+    for (int s = 0; s < d->nsrc; ++s) {
+        const yxh_src& q = d->src[s];
+        YXH_CHECK_ARG(q.ptr && a16(q.ptr) && q.channels % epc == 0 && q.cstride % epc == 0 && q.bstride % epc == 0,
+                      "wgrad src%d alignment / channels", s);
+        YXH_CHECK_ARG(q.upsample == 0 || q.upsample == 1, "wgrad src%d upsample %d", s, q.upsample);
+        YXH_CHECK_ARG((q.h << q.upsample) == d->in_h && (q.w << q.upsample) == d->in_w, "wgrad src%d spatial", s);
+        chs += q.channels;
+    }
+    YXH_CHECK_ARG(chs == d->cin, "wgrad source channels %d != cin %d", chs, d->cin);
+    const yxh_src& g = d->dy;
+    YXH_CHECK_ARG(g.ptr && a16(g.ptr) && g.channels % epc == 0 && g.channels >= d->cout && g.cstride % epc == 0 &&
+                      g.bstride % epc == 0 && g.h == d->out_h && g.w == d->out_w && g.upsample == 0,
+                  "wgrad dy view (channels %d must cover cout %d in %d-element chunks)", g.channels, d->cout, epc);
+    YXH_CHECK_ARG(d->dw && d->cin_store > 0 && d->cin_store <= d->cin, "wgrad dw / cin_store");
+    WgradParams p{};
+    p.in_h = d->in_h; p.in_w = d->in_w; p.out_h = d->out_h; p.out_w = d->out_w;
+    p.cin = d->cin; p.cout = d->cout; p.kh = d->kh; p.kw = d->kw; p.stride = d->stride; p.pad = d->pad;
+    p.ohw = d->out_h * d->out_w;
+    const long long M = (long long)d->batch * p.ohw;
+    YXH_CHECK_ARG(M < (1LL << 31), "too many pixels");
+    p.M = (int)M;
+    p.nsrc = d->nsrc;
+    p.src0_ch = d->src[0].channels;
+    for (int s = 0; s < d->nsrc; ++s) {
+        p.sptr[s] = d->src[s].ptr;
+        p.scs[s] = d->src[s].cstride;
+        p.sbs[s] = d->src[s].bstride;
+        p.sw[s] = d->src[s].w;
+        p.sup[s] = d->src[s].upsample;
+    }
+    p.dy = g.ptr;
+    p.dycs = g.cstride;
+    p.dybs = g.bstride;
+    p.dw = d->dw;
+    p.cin_store = d->cin_store;
+    if (dt == YXH_BF16) return wgrad_tile<bf16>(d->tile, p, st);
+    if (dt == YXH_F16) return wgrad_tile<f16>(d->tile, p, st);
+    return wgrad_tile<float>(d->tile, p, st);
+}
+
+int pack_dgrad_launch(const float* w, int cout, int cin, int kh, int kw, int c_begin, int c_count, int cout_pad, int dt,
+                      void* out, hipStream_t st) {
+    YXH_CHECK_ARG(w && out && a16(out), "pack_dgrad: null / unaligned");
+    YXH_CHECK_ARG(cout > 0 && cin > 0 && kh > 0 && kw > 0 && c_begin >= 0 && c_count > 0 && c_begin + c_count <= cin &&
+                      cout_pad >= cout,
+                  "pack_dgrad geometry");
+    const long long total = (long long)c_count * kh * kw * cout_pad;
+    dim3 grid((unsigned)((total + 255) / 256));
+    if (dt == YXH_BF16) hipLaunchKernelGGL(pack_dgrad<bf16>, grid, dim3(256), 0, st, w, cout, cin, kh, kw, c_begin, c_count, cout_pad, (bf16*)out);
+    else if (dt == YXH_F16) hipLaunchKernelGGL(pack_dgrad<f16>, grid, dim3(256), 0, st, w, cout, cin, kh, kw, c_begin, c_count, cout_pad, (f16*)out);
+    else if (dt == YXH_F32) hipLaunchKernelGGL(pack_dgrad<float>, grid, dim3(256), 0, st, w, cout, cin, kh, kw, c_begin, c_count, cout_pad, (float*)out);
+    else {
+        set_error("pack_dgrad dtype %d", dt);
+        return YXH_EINVAL;
+    }
+    YXH_CHECK_LAUNCH("pack_dgrad");
+    return YXH_OK;
+}
+
+int spp_bwd_launch(int dt, int B, const yxh_src* cat, int c, const float* dcat, float* dx, hipStream_t st) {
+    YXH_CHECK_ARG(cat && cat->ptr && dcat && dx && B > 0 && c > 0 && cat->cstride >= 4 * c, "spp_bwd arguments");
+    const long long total = (long long)B * cat->h * cat->w * c;
+    dim3 grid((unsigned)((total + 255) / 256));
+    TView v = tview(cat, c);
+#define YXH_SPPB(T) hipLaunchKernelGGL(spp_bwd<T>, grid, dim3(256), 0, st, v, cat->h, cat->w, c, dcat, dx, B)
+    if (dt == YXH_BF16) YXH_SPPB(bf16);
+    else if (dt == YXH_F16) YXH_SPPB(f16);
+    else YXH_SPPB(float);
+#undef YXH_SPPB
+    YXH_CHECK_LAUNCH("spp_bwd");
+    return YXH_OK;
+}
+
+int upsample_bwd_launch(const float* g, int B, int h, int w, int C, float* dst, hipStream_t st) {
+    YXH_CHECK_ARG(g && dst && a16(g) && a16(dst) && B > 0 && h > 0 && w > 0 && C > 0 && C % 4 == 0,
+                  "upsample_bwd arguments");
+    const long long total = (long long)B * h * w * (C / 4);
+    hipLaunchKernelGGL(upsample_bwd, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, g, B, h, w, C, dst);
+    YXH_CHECK_LAUNCH("upsample_bwd");
+    return YXH_OK;
+}
+
+}  // namespace yxh

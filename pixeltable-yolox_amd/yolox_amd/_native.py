@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -46,7 +46,18 @@ class ConvDesc(C.Structure):
                 ("dst_dtype", C.c_int32), ("res_bstride", C.c_int64), ("dst", C.c_void_p),
                 ("dst_cstride", C.c_int32), ("act", C.c_int32), ("dst_bstride", C.c_int64),
                 ("decode_stride", C.c_float), ("decode_coff", C.c_int32), ("tile", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("flags", C.c_int32)]
+
+
+CONV_ACCUMULATE = 1
+
+
+class WgradDesc(C.Structure):
+    _fields_ = [("dtype", C.c_int32), ("batch", C.c_int32), ("in_h", C.c_int32), ("in_w", C.c_int32),
+                ("out_h", C.c_int32), ("out_w", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32),
+                ("kh", C.c_int32), ("kw", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32),
+                ("nsrc", C.c_int32), ("cin_store", C.c_int32), ("src", Src * 2), ("dy", Src),
+                ("dw", C.c_void_p), ("tile", C.c_int32), ("reserved", C.c_int32)]
 
 
 class FocusDesc(C.Structure):
@@ -115,6 +126,19 @@ def lib():
             "yxh_yolox_loss_workspace_bytes": ([i32, i32, i32], sz),
             "yxh_yolox_loss": ([vp, vp, vp, i32, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, sz, vp],
                                C.c_int),
+            "yxh_reduce_workspace_bytes": ([i32], sz),
+            "yxh_bn_stats": ([i32, i32, C.POINTER(Src), vp, vp, vp, vp, f32, f32, vp, vp, sz, vp], C.c_int),
+            "yxh_bn_act_fwd": ([i32, i32, C.POINTER(Src), vp, i32, C.POINTER(Src), C.POINTER(Src), vp], C.c_int),
+            "yxh_bn_act_bwd": ([i32, i32, C.POINTER(Src), C.POINTER(Src), vp, vp, i32, vp, vp, vp, vp, sz, vp],
+                               C.c_int),
+            "yxh_channel_sum": ([i32, i32, C.POINTER(Src), vp, vp, sz, vp], C.c_int),
+            "yxh_conv_wgrad": ([C.POINTER(WgradDesc), vp], C.c_int),
+            "yxh_pack_dgrad_weight": ([vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp], C.c_int),
+            "yxh_spp_bwd": ([i32, i32, C.POINTER(Src), i32, vp, vp, vp], C.c_int),
+            "yxh_upsample_bwd": ([vp, i32, i32, i32, i32, vp, vp], C.c_int),
+            "yxh_head_decode_train": ([vp, i32, i32, i32, vp, vp, i32, vp, vp], C.c_int),
+            "yxh_yolox_loss_bwd": ([vp, vp, vp, i32, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, i32, i32, vp,
+                                    vp, vp], C.c_int),
             "yxh_run_ops": ([C.POINTER(Op), i32, vp], C.c_int),
             "yxh_graph_create": ([C.POINTER(Op), i32, vp, C.POINTER(vp)], C.c_int),
             "yxh_graph_launch": ([vp, vp], C.c_int),
@@ -134,7 +158,10 @@ def lib():
 
 EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d",
             "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox", "yxh_postprocess_workspace_bytes",
-            "yxh_postprocess", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_launch", "yxh_graph_destroy"]
+            "yxh_postprocess", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create",
+            "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
+            "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_spp_bwd",
+            "yxh_upsample_bwd", "yxh_head_decode_train", "yxh_yolox_loss_bwd"]
 
 
 def check(rc: int, what: str = "") -> None:

@@ -30,8 +30,9 @@ def yolox_losses(outputs: torch.Tensor, labels: torch.Tensor, level_hw: Sequence
     labels = labels.to(dev, torch.float32).contiguous()
     if origin_reg is not None:
         origin_reg = origin_reg.to(dev, torch.float32).contiguous()
-    hw = torch.tensor([v for h, w in level_hw for v in (h, w)], dtype=torch.int32, device=dev)
-    st = torch.tensor(list(strides), dtype=torch.int32, device=dev)
+    # level geometry is read on the host by the launcher (host arrays, not device memory)
+    hw = torch.tensor([v for h, w in level_hw for v in (h, w)], dtype=torch.int32)
+    st = torch.tensor(list(strides), dtype=torch.int32)
     fg = torch.empty(B, A, dtype=torch.uint8, device=dev)
     matched = torch.empty(B, A, dtype=torch.int32, device=dev)
     piou = torch.empty(B, A, dtype=torch.float32, device=dev)

@@ -65,9 +65,14 @@ class YoloxModule(nn.Module):
 
     def forward(self, x, targets=None):
         if self.training:
-            # SimOTA assignment / losses / backward are the next rows of the hot path
-            # (DESIGN.md §Scope); the eval path below is the graded inference path.
-            raise NotImplementedError("training forward is not implemented yet in yolox_amd")
+            # yolox.py:76-87: loss dict; BN batch statistics, on-device SimOTA, HIP
+            # reverse pass behind total_loss.backward() (yolox_amd/train.py)
+            assert targets is not None
+            from ..train import train_forward
+
+            if self.device.type != "cuda":
+                raise RuntimeError("YoloxModule runs on a ROCm device only; call .to('cuda') first")
+            return train_forward(self, x, targets)
         if x.dim() != 4 or x.shape[1] != 3:
             raise ValueError(f"expected [B, 3, H, W] images, got {tuple(x.shape)}")
         B, _, H, W = x.shape

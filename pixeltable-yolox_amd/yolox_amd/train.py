@@ -1,0 +1,520 @@
+"""Training step of YoloxModule on libyoloxhip.
+
+Reference: ``YoloxModule.forward(x, targets)`` in train mode (yolox/models/yolox.py:72-92)
+-> backbone (darknet.py:95-177, yolo_pafpn.py:83-116) -> ``YoloxHead.forward`` training
+branch (yolo_head.py:161-182, get_output_and_grid :213-231) -> ``get_losses`` (:253-411)
+and ``loss.backward()`` (trainer.py:112).
+
+Every BaseConv runs as conv (MFMA, raw output) -> BatchNorm2d batch statistics
+(yxh_bn_stats, running stats updated like torch) -> BN+act apply (+ Bottleneck
+residual); the head's preds write raw rows of [B, A, 5+C]; decode, SimOTA and the losses
+run on the device without a host sync.  The forward records a tape of backward
+closures; ``backward`` replays it in reverse:
+
+* act + BN backward (yxh_bn_act_bwd) -> dgamma / dbeta straight into the gradient
+  buffer, conv-output gradient in the compute dtype;
+* weight gradient (yxh_conv_wgrad, MFMA, split over pixels);
+* data gradient = a forward conv with transposed, flipped weights
+  (yxh_pack_dgrad_weight; stride 2 via a zero-dilated source) accumulating into the
+  fp32 gradient of each input view; nearest-x2 sources through yxh_upsample_bwd;
+* SPP max-pool backward (yxh_spp_bwd), residuals as plain adds.
+
+Parameter gradients land in one flat fp32 buffer (``GradBuffer``) whose slices become
+``param.grad``; a data-parallel reducer (yolox_amd.dp) can all-reduce it in buckets as
+the reverse pass completes them (``on_param_ready``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Callable, Optional, Sequence
+
+import torch
+import torch.nn as nn
+
+from . import _native as N
+from .models.losses import LOSS_KEYS
+from .models.network import (BaseConv, Bottleneck, CspDarknet, CspLayer, DWConv, Focus, SPPBottleneck,
+                             YoloPafpn, YoloxHead)
+
+MAX_CHANNELS = 4096  # reduction workspace sizing (yolox_x: 1280)
+
+
+class Act:
+    """An NHWC activation: channels [coff, coff + ch) of storage ``t`` [B, h, w, Ct]."""
+
+    __slots__ = ("t", "coff", "ch", "h", "w", "grad", "needs_grad")
+
+    def __init__(self, t: torch.Tensor, coff: int, ch: int, needs_grad: bool = True):
+        self.t, self.coff, self.ch = t, coff, ch
+        self.h, self.w = t.shape[1], t.shape[2]
+        self.grad: Optional[torch.Tensor] = None
+        self.needs_grad = needs_grad
+
+    def src(self, up: int = 0) -> N.Src:
+        s = N.Src()
+        s.ptr = self.t.data_ptr() + self.coff * self.t.element_size()
+        s.channels, s.cstride = self.ch, self.t.shape[3]
+        s.bstride = self.h * self.w * self.t.shape[3]
+        s.h, s.w, s.upsample = self.h, self.w, up
+        return s
+
+    def ensure_grad(self) -> torch.Tensor:
+        if self.grad is None:
+            self.grad = torch.zeros(self.t.shape[0], self.h, self.w, self.ch, dtype=torch.float32,
+                                    device=self.t.device)
+        return self.grad
+
+
+def dense_src(t: torch.Tensor, up: int = 0) -> N.Src:
+    """View of a dense [B, h, w, C] tensor."""
+    s = N.Src()
+    s.ptr = t.data_ptr()
+    s.channels = s.cstride = t.shape[3]
+    s.bstride = t.shape[1] * t.shape[2] * t.shape[3]
+    s.h, s.w, s.upsample = t.shape[1], t.shape[2], up
+    return s
+
+
+class GradBuffer:
+    """One flat fp32 buffer holding every parameter gradient, parameters in reverse
+    registration order (roughly the order the reverse pass finishes them)."""
+
+    def __init__(self, params: Sequence[nn.Parameter], device):
+        self.params = list(params)[::-1]
+        self.offsets = {}
+        off = 0
+        for p in self.params:
+            self.offsets[id(p)] = off
+            off += p.numel()
+        self.numel = off
+        self.flat = torch.zeros(off, dtype=torch.float32, device=device)
+        self.views = {id(p): self.flat[self.offsets[id(p)]:self.offsets[id(p)] + p.numel()].view_as(p)
+                      for p in self.params}
+
+    def of(self, p: nn.Parameter) -> torch.Tensor:
+        return self.views[id(p)]
+
+    def begin(self) -> Optional[torch.Tensor]:
+        """Zero the buffer for a new reverse pass; returns what param.grad held if the
+        gradients already live here (torch accumulates across backward calls)."""
+        held = any(p.grad is not None and p.grad.data_ptr() == self.views[id(p)].data_ptr() for p in self.params)
+        prev = self.flat.clone() if held else None
+        self.flat.zero_()
+        return prev
+
+    def publish(self, prev: Optional[torch.Tensor]) -> None:
+        if prev is not None:
+            self.flat.add_(prev)
+        for p in self.params:
+            g = self.views[id(p)]
+            if p.grad is None:
+                p.grad = g
+            elif p.grad.data_ptr() != g.data_ptr():
+                p.grad.add_(g)
+
+
+class TrainGraph:
+    """Executes one training forward (recording the tape) and its backward."""
+
+    def __init__(self, model, dtype: torch.dtype):
+        if dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            raise ValueError(f"compute dtype {dtype} not supported")
+        self.model = model
+        self.dtype = dtype
+        self.dcode = N.DTYPE_CODE[dtype]
+        self.device = model.device
+        self.lib = N.lib()
+        self.esize = torch.empty((), dtype=dtype).element_size()
+        self.grads = GradBuffer(model.parameters(), self.device)
+        self.ws = torch.empty(int(self.lib.yxh_reduce_workspace_bytes(MAX_CHANNELS)), dtype=torch.uint8,
+                              device=self.device)
+        self.zero_bias = torch.zeros(MAX_CHANNELS, dtype=torch.float32, device=self.device)
+        self.tape: list[Callable[[], None]] = []
+        self.on_param_ready: Optional[Callable[[nn.Parameter], None]] = None
+        self._fwd_w: dict = {}
+        self.grad_total = torch.ones((), dtype=torch.float32, device=self.device)
+
+    # ------------------------------------------------------------ helpers
+    @property
+    def stream(self) -> int:
+        return N.stream_ptr(self.device)
+
+    def _chk(self, rc, what):
+        N.check(rc, what)
+
+    def _ready(self, *params) -> None:
+        if self.on_param_ready is not None:
+            for p in params:
+                self.on_param_ready(p)
+
+    def _fwd_weight(self, conv: nn.Conv2d, cin_pad: int):
+        """conv.weight -> [cout][kh][kw][cin_pad] compute dtype (+ fp32 bias)."""
+        kh, kw = conv.kernel_size
+        w = self._fwd_w.get(id(conv))
+        if w is None:
+            w = (torch.empty(conv.out_channels * kh * kw * cin_pad, dtype=self.dtype, device=self.device),
+                 torch.empty(conv.out_channels, dtype=torch.float32, device=self.device))
+            self._fwd_w[id(conv)] = w
+        wt = conv.weight.detach()
+        if wt.dtype != torch.float32:
+            raise ValueError("training keeps fp32 master weights; the compute dtype comes from autocast")
+        b = conv.bias.detach() if conv.bias is not None else None
+        self._chk(self.lib.yxh_fold_bn_pack(
+            wt.data_ptr(), b.data_ptr() if b is not None else None, None, None, None, None, 0.0,
+            conv.out_channels, conv.in_channels // conv.groups, kh, kw, cin_pad, self.dcode, w[0].data_ptr(),
+            w[1].data_ptr(), self.stream), "pack weights")
+        return w
+
+    def _conv(self, srcs: list, cin: int, cout: int, k: int, stride: int, pad: int, weight: int, bias: int,
+              dst: int, dst_f32: bool, dst_cs: int, dst_bs: int, in_h: int, in_w: int, out_h: int, out_w: int,
+              batch: int, accumulate: bool = False) -> None:
+        d = N.ConvDesc()
+        d.dtype, d.batch = self.dcode, batch
+        d.in_h, d.in_w, d.out_h, d.out_w = in_h, in_w, out_h, out_w
+        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.groups = cin, cout, k, k, stride, pad, 1
+        d.nsrc = len(srcs)
+        for j, s in enumerate(srcs):
+            d.src[j] = s
+        d.weight, d.bias = weight, bias
+        d.dst = dst
+        d.dst_dtype = N.F32 if dst_f32 else self.dcode
+        d.dst_cstride, d.dst_bstride = dst_cs, dst_bs
+        d.act = N.ACT_NONE
+        d.tile = 0
+        d.flags = N.CONV_ACCUMULATE if accumulate else 0
+        self._chk(self.lib.yxh_conv2d(C.byref(d), self.stream), "conv")
+
+    def _wgrad(self, srcs: list, cin: int, cin_store: int, cout: int, k: int, stride: int, pad: int, dy: N.Src,
+               dw: torch.Tensor, in_h: int, in_w: int, out_h: int, out_w: int, batch: int) -> None:
+        d = N.WgradDesc()
+        d.dtype, d.batch = self.dcode, batch
+        d.in_h, d.in_w, d.out_h, d.out_w = in_h, in_w, out_h, out_w
+        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad = cin, cout, k, k, stride, pad
+        d.nsrc, d.cin_store = len(srcs), cin_store
+        for j, s in enumerate(srcs):
+            d.src[j] = s
+        d.dy = dy
+        d.dw = dw.data_ptr()
+        d.tile = 0
+        self._chk(self.lib.yxh_conv_wgrad(C.byref(d), self.stream), "wgrad")
+
+    def _dgrad(self, conv: nn.Conv2d, dy_t: torch.Tensor, cout_pad: int, inputs: list, batch: int) -> None:
+        """Accumulate the data gradient of every input view that needs one.
+        inputs: [(Act, upsample, channel offset in the conv's cin)]."""
+        kh = conv.kernel_size[0]
+        s = conv.stride[0]
+        if s not in (1, 2):
+            raise NotImplementedError("stride > 2")
+        pad = kh - 1 - conv.padding[0]
+        dy = dense_src(dy_t, up=2 if s == 2 else 0)
+        for act, up, cb in inputs:
+            if not act.needs_grad:
+                continue
+            cs = act.ch
+            wt = torch.empty(cs * kh * kh * cout_pad, dtype=self.dtype, device=self.device)
+            self._chk(self.lib.yxh_pack_dgrad_weight(
+                conv.weight.detach().data_ptr(), conv.out_channels, conv.in_channels, kh, kh, cb, cs, cout_pad,
+                self.dcode, wt.data_ptr(), self.stream), "pack dgrad")
+            in_h, in_w = act.h << up, act.w << up  # the conv's logical input size
+            dst = (torch.zeros(batch, in_h, in_w, cs, dtype=torch.float32, device=self.device) if up
+                   else act.ensure_grad())
+            self._conv([dy], cout_pad, cs, kh, 1, pad, wt.data_ptr(), self.zero_bias.data_ptr(), dst.data_ptr(),
+                       True, cs, in_h * in_w * cs, in_h, in_w, in_h, in_w, batch, accumulate=True)
+            if up:
+                g = act.ensure_grad()
+                self._chk(self.lib.yxh_upsample_bwd(dst.data_ptr(), batch, act.h, act.w, cs, g.data_ptr(),
+                                                    self.stream), "upsample bwd")
+
+    # ------------------------------------------------------------ layers
+    def base_conv(self, m: BaseConv, inputs: list, out: Optional[Act] = None, residual: Optional[Act] = None,
+                  cin_store: Optional[int] = None) -> Act:
+        """BaseConv.forward (network_blocks.py:48-49) in train mode; inputs: [(Act,
+        upsample)] concatenated along channels (torch.cat order)."""
+        if isinstance(m, DWConv) or m.conv.groups != 1:
+            raise NotImplementedError("depthwise (yolox_nano) training is not implemented")
+        conv, bn = m.conv, m.bn
+        B = inputs[0][0].t.shape[0]
+        cin = sum(a.ch for a, _ in inputs)
+        k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        in_h, in_w = inputs[0][0].h << inputs[0][1], inputs[0][0].w << inputs[0][1]
+        oh, ow = (in_h + 2 * p - k) // s + 1, (in_w + 2 * p - k) // s + 1
+        cout = conv.out_channels
+        w, _ = self._fwd_weight(conv, cin)
+        srcs = [a.src(up) for a, up in inputs]
+        y = torch.empty(B, oh, ow, cout, dtype=self.dtype, device=self.device)
+        self._conv(srcs, cin, cout, k, s, p, w.data_ptr(), self.zero_bias.data_ptr(), y.data_ptr(), False, cout,
+                   oh * ow * cout, in_h, in_w, oh, ow, B)
+        stats = torch.empty(4, cout, dtype=torch.float32, device=self.device)
+        ys = dense_src(y)
+        self._chk(self.lib.yxh_bn_stats(
+            self.dcode, B, C.byref(ys), bn.weight.detach().data_ptr(), bn.bias.detach().data_ptr(),
+            bn.running_mean.data_ptr(), bn.running_var.data_ptr(), float(bn.eps), float(bn.momentum),
+            stats.data_ptr(), self.ws.data_ptr(), self.ws.numel(), self.stream), "bn stats")
+        bn.num_batches_tracked.add_(1)
+        if out is None:
+            out = Act(torch.empty(B, oh, ow, cout, dtype=self.dtype, device=self.device), 0, cout)
+        os_ = out.src()
+        rs = residual.src() if residual is not None else None
+        act = N.ACT_CODE[getattr(m, "act_name", "silu")]
+        self._chk(self.lib.yxh_bn_act_fwd(self.dcode, B, C.byref(ys), stats.data_ptr(), act,
+                                          C.byref(rs) if rs is not None else None, C.byref(os_), self.stream),
+                  "bn act fwd")
+        cin_store = cin_store or cin
+
+        def backward():
+            if out.grad is None:  # output unused by the loss
+                return
+            assert y.data_ptr() == ys.ptr  # the closure holds y: ys is a raw pointer into it
+            dy = torch.empty(B, oh, ow, cout, dtype=self.dtype, device=self.device)
+            go = dense_src(out.grad)
+            gb = self.grads
+            self._chk(self.lib.yxh_bn_act_bwd(
+                self.dcode, B, C.byref(ys), C.byref(go), stats.data_ptr(), bn.weight.detach().data_ptr(), act,
+                gb.of(bn.weight).data_ptr(), gb.of(bn.bias).data_ptr(), dy.data_ptr(), self.ws.data_ptr(),
+                self.ws.numel(), self.stream), "bn act bwd")
+            self._ready(bn.weight, bn.bias)
+            if residual is not None and residual.needs_grad:
+                residual.ensure_grad().add_(out.grad)
+            self._wgrad(srcs, cin, cin_store, cout, k, s, p, dense_src(dy), gb.of(conv.weight), in_h, in_w, oh, ow,
+                        B)
+            self._ready(conv.weight)
+            off, ins = 0, []
+            for a, up in inputs:
+                ins.append((a, up, off))
+                off += a.ch
+            self._dgrad(conv, dy, cout, ins, B)
+
+        self.tape.append(backward)
+        return out
+
+    def bottleneck(self, b: Bottleneck, x: Act) -> Act:
+        # network_blocks.py:95-99
+        t = self.base_conv(b.conv1, [(x, 0)])
+        return self.base_conv(b.conv2, [(t, 0)], residual=x if b.use_add else None)
+
+    def csp(self, m: CspLayer, inputs: list) -> Act:
+        # network_blocks.py:176-183
+        x1 = self.base_conv(m.conv1, inputs)
+        x2 = self.base_conv(m.conv2, inputs)
+        for b in m.m:
+            x1 = self.bottleneck(b, x1)
+        return self.base_conv(m.conv3, [(x1, 0), (x2, 0)])
+
+    def spp(self, m: SPPBottleneck, inputs: list) -> Act:
+        # network_blocks.py:137-142: x -> cat[x, mp5(x), mp9(x), mp13(x)] in one buffer
+        x0 = inputs[0][0]
+        B = x0.t.shape[0]
+        c = m.conv1.conv.out_channels
+        h, w = x0.h << inputs[0][1], x0.w << inputs[0][1]
+        cat = torch.empty(B, h, w, 4 * c, dtype=self.dtype, device=self.device)
+        x = self.base_conv(m.conv1, inputs, out=Act(cat, 0, c))
+        self._chk(self.lib.yxh_spp_maxpool(cat.data_ptr(), self.dcode, B, h, w, c, 4 * c, h * w * 4 * c,
+                                           self.stream), "spp")
+        cat_act = Act(cat, 0, 4 * c)
+
+        def backward():
+            if cat_act.grad is None:
+                return
+            xs = cat_act.src()
+            g = x.ensure_grad()
+            self._chk(self.lib.yxh_spp_bwd(self.dcode, B, C.byref(xs), c, cat_act.grad.data_ptr(), g.data_ptr(),
+                                           self.stream), "spp bwd")
+
+        self.tape.append(backward)
+        return self.base_conv(m.conv2, [(cat_act, 0)])
+
+    def focus(self, m: Focus, images: torch.Tensor) -> Act:
+        # network_blocks.py:193-208: space-to-depth into 16 NHWC channels (12 used)
+        B, _, H, W = images.shape
+        packed = torch.empty(B, H // 2, W // 2, 16, dtype=self.dtype, device=self.device)
+        self._chk(self.lib.yxh_focus_pack(images.data_ptr(), N.NCHW, N.DTYPE_CODE[images.dtype], B, H, W,
+                                          packed.data_ptr(), self.dcode, self.stream), "focus")
+        return self.base_conv(m.conv, [(Act(packed, 0, 16, needs_grad=False), 0)], cin_store=12)
+
+    def darknet(self, m: CspDarknet, images: torch.Tensor):
+        # darknet.py:165-177
+        x = self.focus(m.stem, images)
+        feats = []
+        for stage in (m.dark2, m.dark3, m.dark4, m.dark5):
+            x = self.base_conv(stage[0], [(x, 0)])
+            for blk in list(stage)[1:]:
+                x = self.spp(blk, [(x, 0)]) if isinstance(blk, SPPBottleneck) else self.csp(blk, [(x, 0)])
+            feats.append(x)
+        return feats[1], feats[2], feats[3]
+
+    def pafpn(self, m: YoloPafpn, images: torch.Tensor):
+        # yolo_pafpn.py:83-116
+        x2, x1, x0 = self.darknet(m.backbone, images)
+        fpn_out0 = self.base_conv(m.lateral_conv0, [(x0, 0)])
+        f_out0 = self.csp(m.C3_p4, [(fpn_out0, 1), (x1, 0)])
+        fpn_out1 = self.base_conv(m.reduce_conv1, [(f_out0, 0)])
+        pan_out2 = self.csp(m.C3_p3, [(fpn_out1, 1), (x2, 0)])
+        p_out1 = self.base_conv(m.bu_conv2, [(pan_out2, 0)])
+        pan_out1 = self.csp(m.C3_n3, [(p_out1, 0), (fpn_out1, 0)])
+        p_out0 = self.base_conv(m.bu_conv1, [(pan_out1, 0)])
+        pan_out0 = self.csp(m.C3_n4, [(p_out0, 0), (fpn_out0, 0)])
+        return pan_out2, pan_out1, pan_out0
+
+    def head(self, head: YoloxHead, feats, labels: torch.Tensor) -> dict:
+        # yolo_head.py:140-182 (training branch), 213-231, 253-411
+        B = feats[0].t.shape[0]
+        nc = head.num_classes
+        D = 5 + nc
+        hw = [(f.h, f.w) for f in feats]
+        A = sum(h * w for h, w in hw)
+        raw = torch.empty(B, A, D, dtype=torch.float32, device=self.device)
+        levels = []
+        a_off = 0
+        for k, x in enumerate(feats):
+            s = self.base_conv(head.stems[k], [(x, 0)])
+            c = self.base_conv(head.cls_convs[k][0], [(s, 0)])
+            c = self.base_conv(head.cls_convs[k][1], [(c, 0)])
+            r = self.base_conv(head.reg_convs[k][0], [(s, 0)])
+            r = self.base_conv(head.reg_convs[k][1], [(r, 0)])
+            h, w = x.h, x.w
+            # reg | obj preds stacked (5 rows, both read reg_feat, :155-159) and the cls
+            # preds write raw rows of [B, A, 5+C] (the cat of :164 in anchor order)
+            w_ro = torch.cat([head.reg_preds[k].weight.detach().reshape(4, -1),
+                              head.obj_preds[k].weight.detach().reshape(1, -1)]).contiguous()
+            b_ro = torch.cat([head.reg_preds[k].bias.detach(), head.obj_preds[k].bias.detach()]).contiguous()
+            pk_ro = torch.empty(5 * r.ch, dtype=self.dtype, device=self.device)
+            pk_rob = torch.empty(5, dtype=torch.float32, device=self.device)
+            self._chk(self.lib.yxh_fold_bn_pack(w_ro.data_ptr(), b_ro.data_ptr(), None, None, None, None, 0.0, 5,
+                                                r.ch, 1, 1, r.ch, self.dcode, pk_ro.data_ptr(), pk_rob.data_ptr(),
+                                                self.stream), "pack preds")
+            wc, bc = self._fwd_weight(head.cls_preds[k], c.ch)
+            base = raw.data_ptr() + a_off * D * 4
+            self._conv([r.src()], r.ch, 5, 1, 1, 0, pk_ro.data_ptr(), pk_rob.data_ptr(), base, True, D, A * D,
+                       h, w, h, w, B)
+            self._conv([c.src()], c.ch, nc, 1, 1, 0, wc.data_ptr(), bc.data_ptr(), base + 5 * 4, True, D, A * D,
+                       h, w, h, w, B)
+            levels.append((k, r, c, w_ro, a_off, h, w))
+            a_off += h * w
+        preds = torch.empty_like(raw)
+        lhw = (C.c_int32 * (2 * len(hw)))(*[v for t in hw for v in t])
+        strides = (C.c_int32 * len(hw))(*head.strides[:len(hw)])
+        self._chk(self.lib.yxh_head_decode_train(raw.data_ptr(), B, A, nc, lhw, strides, len(hw), preds.data_ptr(),
+                                                 self.stream), "decode")
+        L = labels.shape[1]
+        use_l1 = bool(head.use_l1)
+        origin = raw[..., :4].contiguous() if use_l1 else None
+        fg = torch.empty(B, A, dtype=torch.uint8, device=self.device)
+        matched = torch.empty(B, A, dtype=torch.int32, device=self.device)
+        piou = torch.empty(B, A, dtype=torch.float32, device=self.device)
+        num_fg = torch.empty(B, dtype=torch.int32, device=self.device)
+        losses = torch.empty(6, dtype=torch.float32, device=self.device)
+        ws = torch.empty(int(self.lib.yxh_yolox_loss_workspace_bytes(B, A, L)), dtype=torch.uint8,
+                         device=self.device)
+        self._chk(self.lib.yxh_yolox_loss(
+            preds.data_ptr(), origin.data_ptr() if origin is not None else None, labels.data_ptr(), B, A, nc, L,
+            lhw, strides, len(hw), fg.data_ptr(), matched.data_ptr(), piou.data_ptr(), num_fg.data_ptr(),
+            losses.data_ptr(), ws.data_ptr(), ws.numel(), self.stream), "yolox loss")
+        self.assign = {"fg_mask": fg, "matched_gt_inds": matched, "pred_ious": piou, "num_fg": num_fg}
+        self.outputs = preds
+
+        def backward():
+            g_ro = torch.empty(B, A, 8, dtype=self.dtype, device=self.device)
+            g_cls = torch.empty(B, A, nc, dtype=self.dtype, device=self.device)
+            self._chk(self.lib.yxh_yolox_loss_bwd(
+                preds.data_ptr(), raw.data_ptr(), labels.data_ptr(), B, A, nc, L, lhw, strides, len(hw),
+                fg.data_ptr(), matched.data_ptr(), piou.data_ptr(), num_fg.data_ptr(), self.grad_total.data_ptr(),
+                int(use_l1), self.dcode, g_ro.data_ptr(), g_cls.data_ptr(), self.stream), "loss bwd")
+            gb = self.grads
+            for k, r, c, w_ro, a0, h, w in reversed(levels):
+                for g_all, ch, feat, wmat, convs in (
+                        (g_ro, 8, r, w_ro, (head.reg_preds[k], head.obj_preds[k])),
+                        (g_cls, nc, c, head.cls_preds[k].weight.detach().reshape(nc, -1), (head.cls_preds[k],))):
+                    cout = sum(cv.out_channels for cv in convs)
+                    dys = N.Src()
+                    dys.ptr = g_all.data_ptr() + a0 * ch * self.esize
+                    dys.channels, dys.cstride, dys.bstride = ch, ch, A * ch
+                    dys.h, dys.w, dys.upsample = h, w, 0
+                    # weight gradient (stacked rows) and bias sums
+                    dw = torch.zeros(cout, feat.ch, dtype=torch.float32, device=self.device)
+                    self._wgrad([feat.src()], feat.ch, feat.ch, cout, 1, 1, 0, dys, dw, h, w, h, w, B)
+                    bsum = torch.empty(ch, dtype=torch.float32, device=self.device)
+                    self._chk(self.lib.yxh_channel_sum(self.dcode, B, C.byref(dys), bsum.data_ptr(),
+                                                       self.ws.data_ptr(), self.ws.numel(), self.stream), "bias sum")
+                    row = 0
+                    for cv in convs:
+                        n = cv.out_channels
+                        gb.of(cv.weight).copy_(dw[row:row + n].view_as(cv.weight))
+                        gb.of(cv.bias).copy_(bsum[row:row + n])
+                        row += n
+                        self._ready(cv.weight, cv.bias)
+                    # data gradient: 1x1 conv with the transposed pred weights (K padded to `ch`)
+                    wt = torch.empty(feat.ch * ch, dtype=self.dtype, device=self.device)
+                    wm = wmat.contiguous()
+                    self._chk(self.lib.yxh_pack_dgrad_weight(
+                        wm.data_ptr(), cout, feat.ch, 1, 1, 0, feat.ch, ch, self.dcode, wt.data_ptr(), self.stream),
+                        "pack pred dgrad")
+                    g = feat.ensure_grad()
+                    self._conv([dys], ch, feat.ch, 1, 1, 0, wt.data_ptr(), self.zero_bias.data_ptr(), g.data_ptr(),
+                               True, feat.ch, h * w * feat.ch, h, w, h, w, B, accumulate=True)
+
+        self.tape.append(backward)
+        return {k: losses[i] for i, k in enumerate(LOSS_KEYS)}
+
+    # ------------------------------------------------------------ entry points
+    def forward(self, images: torch.Tensor, labels: torch.Tensor) -> dict:
+        self.tape = []
+        if images.dim() != 4 or images.shape[1] != 3:
+            raise ValueError(f"expected [B, 3, H, W] images, got {tuple(images.shape)}")
+        if images.shape[2] % 32 or images.shape[3] % 32:
+            raise ValueError("input size must be multiples of 32")
+        images = images.to(self.device)
+        if images.dtype not in (torch.float32, torch.bfloat16, torch.float16, torch.uint8):
+            images = images.float()
+        images = images.contiguous()
+        labels = labels.to(self.device, torch.float32).contiguous()
+        self._keep = (images, labels)
+        feats = self.pafpn(self.model.backbone, images)
+        return self.head(self.model.head, feats, labels)
+
+    def backward(self, grad_total: Optional[torch.Tensor] = None) -> None:
+        if not self.tape:
+            raise RuntimeError("backward without a recorded training forward (or called twice)")
+        if grad_total is not None:
+            self.grad_total.copy_(grad_total.reshape(()).to(torch.float32))
+        prev = self.grads.begin()
+        for fn in reversed(self.tape):
+            fn()
+        self.tape = []
+        self._keep = None
+        self.grads.publish(prev)
+
+
+class _LossFn(torch.autograd.Function):
+    """Hooks the HIP reverse pass into ``loss.backward()`` (trainer.py:112)."""
+
+    @staticmethod
+    def forward(ctx, anchor, total, graph):
+        ctx.graph = graph
+        return total.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.graph.backward(g)
+        return None, None, None
+
+
+def compute_dtype_from_autocast() -> torch.dtype:
+    """The reference trains under torch.cuda.amp.autocast when --fp16 (trainer.py:103-104):
+    autocast selects the compute dtype of the HIP path; fp32 otherwise."""
+    if torch.is_autocast_enabled("cuda"):
+        return torch.get_autocast_dtype("cuda")
+    return torch.float32
+
+
+def train_forward(model, images: torch.Tensor, targets: torch.Tensor, dtype: Optional[torch.dtype] = None) -> dict:
+    """YoloxModule.forward(x, targets) in train mode: the reference's loss dict with
+    ``total_loss`` differentiable through the HIP reverse pass."""
+    dtype = dtype or compute_dtype_from_autocast()
+    g = getattr(model, "_train_graph", None)
+    if g is None or g.dtype != dtype or g.device != model.device:
+        g = TrainGraph(model, dtype)
+        model._train_graph = g
+    out = g.forward(images, targets)
+    anchor = torch.zeros((), device=model.device, requires_grad=True)
+    out["total_loss"] = _LossFn.apply(anchor, out["total_loss"], g)
+    return out

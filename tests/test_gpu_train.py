@@ -1,0 +1,392 @@
+"""Training path (yolox_amd/train.py + csrc/train.hip) on the GPU.
+
+Per kernel, against PyTorch fp32 autograd on the CPU (the plain fp32 reference of the
+same op): BN batch statistics + act (+ running stats), BN+act backward, conv weight
+gradient (1x1 / 3x3 s1 / 3x3 s2, two sources, nearest-x2 source), conv data gradient
+(transposed/flipped weights, zero-dilated source for stride 2), SPP max-pool backward,
+upsample backward, the loss gradient w.r.t. the raw head outputs.
+
+End to end: YoloxModule(train) fp32 on yolox_s 128x128 vs the oracle (reference
+restatement pinned to the reference's train fixture): the six loss values, every
+parameter gradient and the BN running statistics (north_star: 1e-3 fp32).
+"""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2, torch.float16: 4e-3}
+
+
+def lib():
+    from yolox_amd import _native as N
+    return N.lib()
+
+
+def chk(rc):
+    from yolox_amd import _native as N
+    N.check(rc)
+
+
+def src(t, coff=0, ch=None, up=0):
+    from yolox_amd.train import Act
+    return Act(t, coff, ch if ch is not None else t.shape[3] - coff).src(up)
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+def ws(C_=1024):
+    return torch.empty(int(lib().yxh_reduce_workspace_bytes(C_)), dtype=torch.uint8, device="cuda")
+
+
+# ----------------------------------------------------------------- BatchNorm + act
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H,W,Cc", [(2, 16, 16, 32), (3, 10, 7, 64), (1, 5, 5, 512)])
+def test_bn_stats_and_act_fwd(dtype, B, H, W, Cc):
+    g = torch.Generator().manual_seed(B * 100 + Cc)
+    y = (torch.randn(B, H, W, Cc, generator=g) * 3 + 5).to(dtype)
+    gamma, beta = torch.rand(Cc, generator=g) + 0.5, torch.randn(Cc, generator=g)
+    rm, rv = torch.randn(Cc, generator=g), torch.rand(Cc, generator=g) + 0.5
+    res = torch.randn(B, H, W, Cc, generator=g).to(dtype)
+    yd, rmd, rvd = y.cuda(), rm.clone().cuda(), rv.clone().cuda()
+    stats = torch.empty(4, Cc, device="cuda")
+    w = ws()
+    ys = src(yd)
+    gd, bd = gamma.cuda(), beta.cuda()  # held: the launch is asynchronous
+    chk(lib().yxh_bn_stats(DT[dtype], B, C.byref(ys), gd.data_ptr(), bd.data_ptr(),
+                           rmd.data_ptr(), rvd.data_ptr(), 1e-3, 0.03, stats.data_ptr(), w.data_ptr(), w.numel(),
+                           stream()))
+    out = torch.empty_like(yd)
+    rd = res.cuda()
+    rs, os_ = src(rd), src(out)
+    chk(lib().yxh_bn_act_fwd(DT[dtype], B, C.byref(ys), stats.data_ptr(), 1, C.byref(rs), C.byref(os_), stream()))
+    torch.cuda.synchronize()
+    # reference: torch BN (training) + SiLU + residual, fp32 on CPU
+    x = y.float().permute(0, 3, 1, 2)
+    rm_ref, rv_ref = rm.clone(), rv.clone()
+    ref = F.silu(F.batch_norm(x, rm_ref, rv_ref, gamma, beta, True, 0.03, 1e-3)).permute(0, 2, 3, 1) + res.float()
+    assert rel(out, ref) < TOL[dtype] * (1 if dtype == torch.float32 else 2)
+    assert rel(rmd, rm_ref) < 1e-5 and rel(rvd, rv_ref) < 1e-4
+    mean = x.mean((0, 2, 3))
+    assert rel(stats[0], mean) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H,W,Cc,act", [(2, 16, 16, 32, 1), (3, 9, 11, 64, 1), (2, 6, 6, 128, 3)])
+def test_bn_act_bwd(dtype, B, H, W, Cc, act):
+    g = torch.Generator().manual_seed(7 + Cc)
+    y = (torch.randn(B, H, W, Cc, generator=g) * 2 + 1).to(dtype)
+    gamma, beta = torch.rand(Cc, generator=g) + 0.5, torch.randn(Cc, generator=g)
+    dout = torch.randn(B, H, W, Cc, generator=g)
+    yd = y.cuda()
+    stats = torch.empty(4, Cc, device="cuda")
+    w = ws()
+    ys = src(yd)
+    gd, bd = gamma.cuda(), beta.cuda()  # held: the launches are asynchronous
+    chk(lib().yxh_bn_stats(DT[dtype], B, C.byref(ys), gd.data_ptr(), bd.data_ptr(), None, None,
+                           1e-3, 0.03, stats.data_ptr(), w.data_ptr(), w.numel(), stream()))
+    dgam, dbet = torch.empty(Cc, device="cuda"), torch.empty(Cc, device="cuda")
+    dx = torch.empty(B, H, W, Cc, dtype=dtype, device="cuda")
+    dd = dout.cuda()
+    gs = src(dd)
+    chk(lib().yxh_bn_act_bwd(DT[dtype], B, C.byref(ys), C.byref(gs), stats.data_ptr(), gd.data_ptr(), act,
+                             dgam.data_ptr(), dbet.data_ptr(), dx.data_ptr(), w.data_ptr(), w.numel(), stream()))
+    torch.cuda.synchronize()
+    x = y.float().permute(0, 3, 1, 2).clone().requires_grad_()
+    gm, bt = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+    z = F.batch_norm(x, None, None, gm, bt, True, 0.0, 1e-3)
+    o = F.silu(z) if act == 1 else F.leaky_relu(z, 0.1)
+    o.backward(dout.permute(0, 3, 1, 2))
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert rel(dgam, gm.grad) < tol and rel(dbet, bt.grad) < tol
+    assert rel(dx, x.grad.permute(0, 2, 3, 1)) < tol
+
+
+# ----------------------------------------------------------------- conv gradients
+def wgrad(dtype, srcs, dy, cout, cin, k, s, p, in_hw, out_hw, B, cin_store=None):
+    from yolox_amd import _native as N
+    d = N.WgradDesc()
+    d.dtype, d.batch = DT[dtype], B
+    d.in_h, d.in_w = in_hw
+    d.out_h, d.out_w = out_hw
+    d.cin, d.cout, d.kh, d.kw, d.stride, d.pad = cin, cout, k, k, s, p
+    d.nsrc, d.cin_store = len(srcs), cin_store or cin
+    for j, q in enumerate(srcs):
+        d.src[j] = q
+    d.dy = dy
+    dw = torch.zeros(cout, cin_store or cin, k, k, device="cuda")
+    d.dw = dw.data_ptr()
+    chk(lib().yxh_conv_wgrad(C.byref(d), stream()))
+    return dw
+
+
+WG_CASES = [  # cin0, cin1, up1, cout, k, s, H
+    (32, 0, 0, 64, 3, 1, 16), (64, 0, 0, 32, 3, 2, 20), (64, 0, 0, 64, 1, 1, 12), (32, 32, 0, 64, 1, 1, 10),
+    (64, 64, 1, 32, 1, 1, 8), (128, 0, 0, 128, 3, 1, 9), (16, 0, 0, 24, 3, 1, 12),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin0,cin1,up1,cout,k,s,H", WG_CASES)
+def test_conv_wgrad_and_dgrad(dtype, cin0, cin1, up1, cout, k, s, H):
+    """weight gradient (yxh_conv_wgrad) and data gradient (yxh_conv2d with
+    yxh_pack_dgrad_weight + ACCUMULATE, zero-dilated source for stride 2)."""
+    from yolox_amd import _native as N
+    from yolox_amd.train import dense_src
+    g = torch.Generator().manual_seed(cin0 + 7 * cout + H)
+    B, W = 2, H + 2
+    p = (k - 1) // 2
+    x0 = torch.randn(B, H, W, cin0, generator=g).to(dtype)
+    x1 = torch.randn(B, H >> up1, W >> up1, cin1, generator=g).to(dtype) if cin1 else None
+    oh, ow = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(B, oh, ow, cout, generator=g).to(dtype)
+    wt = torch.randn(cout, cin0 + cin1, k, k, generator=g) * 0.1
+    x0d, dyd = x0.cuda(), dy.cuda()
+    srcs = [src(x0d)]
+    if cin1:
+        x1d = x1.cuda()
+        srcs.append(src(x1d, up=up1))
+    dw = wgrad(dtype, srcs, src(dyd), cout, cin0 + cin1, k, s, p, (H, W), (oh, ow), B)
+    # data gradient of source 0 (channels [0, cin0))
+    pk = torch.empty(cin0 * k * k * cout, dtype=dtype, device="cuda")
+    wtd = wt.cuda()
+    chk(lib().yxh_pack_dgrad_weight(wtd.data_ptr(), cout, cin0 + cin1, k, k, 0, cin0, cout, DT[dtype], pk.data_ptr(),
+                                    stream()))
+    dx0 = torch.full((B, H, W, cin0), 0.5, device="cuda")  # accumulate onto 0.5
+    d = N.ConvDesc()
+    d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w = DT[dtype], B, H, W, H, W
+    d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.groups, d.nsrc = cout, cin0, k, k, 1, k - 1 - p, 1, 1
+    d.src[0] = dense_src(dyd, up=2 if s == 2 else 0)
+    zb = torch.zeros(cin0, device="cuda")
+    d.weight, d.bias, d.dst, d.dst_dtype = pk.data_ptr(), zb.data_ptr(), dx0.data_ptr(), 0
+    d.dst_cstride, d.dst_bstride, d.act, d.flags = cin0, H * W * cin0, 0, N.CONV_ACCUMULATE
+    chk(lib().yxh_conv2d(C.byref(d), stream()))
+    torch.cuda.synchronize()
+    # reference
+    xin = x0.float().permute(0, 3, 1, 2)
+    if cin1:
+        x1n = x1.float().permute(0, 3, 1, 2)
+        if up1:
+            x1n = F.interpolate(x1n, scale_factor=2, mode="nearest")
+        xin = torch.cat([xin, x1n], 1)
+    xin = xin.clone().requires_grad_()
+    wr = wt.to(dtype).float().clone().requires_grad_()
+    F.conv2d(xin, wr, stride=s, padding=p).backward(dy.float().permute(0, 3, 1, 2))
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert rel(dw, wr.grad) < tol
+    assert rel(dx0 - 0.5, xin.grad[:, :cin0].permute(0, 2, 3, 1)) < tol
+
+
+def test_wgrad_cin_store_and_strided_dy():
+    """Focus stem: 16 packed channels, gradient of the 12 real ones; dy read through a
+    strided view (the head's [B, A, 8] pred-gradient rows)."""
+    g = torch.Generator().manual_seed(3)
+    B, H, W, A0 = 2, 8, 8, 5
+    x = torch.randn(B, H, W, 16, generator=g)
+    rows = torch.randn(B, A0 + H * W + 3, 8, generator=g)
+    xd, rd = x.cuda(), rows.cuda()
+    from yolox_amd import _native as N
+    dys = N.Src()
+    dys.ptr = rd.data_ptr() + A0 * 8 * 4
+    dys.channels, dys.cstride, dys.bstride, dys.h, dys.w = 8, 8, rows.shape[1] * 8, H, W
+    dw = wgrad(torch.float32, [src(xd)], dys, 5, 16, 1, 1, 0, (H, W), (H, W), B, cin_store=12)
+    torch.cuda.synchronize()
+    dyr = rows[:, A0:A0 + H * W, :5].reshape(B, H, W, 5)
+    ref = torch.einsum("bhwn,bhwc->nc", dyr, x[..., :12])
+    assert rel(dw.view(5, 12), ref) < 1e-5
+
+
+def test_spp_and_upsample_bwd():
+    g = torch.Generator().manual_seed(11)
+    B, H, W, c = 2, 9, 10, 16
+    x = torch.randn(B, H, W, c, generator=g)
+    x[0, 1, 1, :] = x[0, 1, 2, :]  # ties: first max in scan order takes the gradient
+    cat = torch.zeros(B, H, W, 4 * c)
+    cat[..., :c] = x
+    dcat = torch.randn(B, H, W, 4 * c, generator=g)
+    catd = cat.cuda()
+    chk(lib().yxh_spp_maxpool(catd.data_ptr(), 0, B, H, W, c, 4 * c, H * W * 4 * c, stream()))
+    dx = torch.empty(B, H, W, c, device="cuda")
+    cs = src(catd)
+    dcd = dcat.cuda()
+    chk(lib().yxh_spp_bwd(0, B, C.byref(cs), c, dcd.data_ptr(), dx.data_ptr(), stream()))
+    up_g = torch.randn(B, 2 * H, 2 * W, c, generator=g)
+    acc = torch.ones(B, H, W, c)
+    accd, ugd = acc.cuda(), up_g.cuda()
+    chk(lib().yxh_upsample_bwd(ugd.data_ptr(), B, H, W, c, accd.data_ptr(), stream()))
+    torch.cuda.synchronize()
+    xr = x.permute(0, 3, 1, 2).clone().requires_grad_()
+    outs = torch.cat([xr] + [F.max_pool2d(xr, k, 1, k // 2) for k in (5, 9, 13)], 1)
+    outs.backward(dcat.permute(0, 3, 1, 2))
+    assert rel(catd[..., c:], outs.detach().permute(0, 2, 3, 1)[..., c:]) == 0.0
+    assert rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-6
+    ref = 1 + up_g.view(B, H, 2, W, 2, c).sum((2, 4))
+    assert rel(accd, ref) < 1e-6
+
+
+# ----------------------------------------------------------------- loss gradient
+@pytest.mark.parametrize("use_l1", [False, True])
+def test_loss_bwd_matches_autograd(oracle, use_l1):
+    """d total_loss / d raw head outputs vs autograd through the oracle's
+    forward_train head math (decode + SimOTA targets + losses)."""
+    from yolox_amd.models.losses import yolox_losses
+    from yolox_amd.weights import synthetic_labels
+    B, S, nc = 2, 128, 80
+    hw = [(S // 8, S // 8), (S // 16, S // 16), (S // 32, S // 32)]
+    A = sum(h * w for h, w in hw)
+    g = torch.Generator().manual_seed(5)
+    raw = torch.randn(B, A, 5 + nc, generator=g) * 0.5
+    raw[..., 4:] -= 2.0
+    labels = torch.from_numpy(synthetic_labels(B, S, S, max_gt=8, seed=9))
+    xs, ys, st = [], [], []
+    for (h, w), s in zip(hw, (8, 16, 32)):
+        yv, xv = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+        xs.append(xv.reshape(-1).float()), ys.append(yv.reshape(-1).float()), st.append(torch.full((h * w,), float(s)))
+    xs, ys, st = torch.cat(xs), torch.cat(ys), torch.cat(st)
+    rawd = raw.cuda()
+    preds = torch.empty_like(rawd)
+    lhw = (C.c_int32 * 6)(*[v for t in hw for v in t])
+    strides = (C.c_int32 * 3)(8, 16, 32)
+    chk(lib().yxh_head_decode_train(rawd.data_ptr(), B, A, nc, lhw, strides, 3, preds.data_ptr(), stream()))
+    losses, assign = yolox_losses(preds, labels.cuda(), hw, origin_reg=rawd[..., :4].contiguous() if use_l1 else None)
+    g_ro = torch.empty(B, A, 8, device="cuda")
+    g_cls = torch.empty(B, A, nc, device="cuda")
+    gt = torch.full((), 2.0, device="cuda")
+    L = labels.shape[1]
+    nfg = assign["num_fg"].int().contiguous()
+    labd = labels.cuda()
+    fgd = assign["fg_mask"].to(torch.uint8).contiguous()
+    chk(lib().yxh_yolox_loss_bwd(preds.data_ptr(), rawd.data_ptr(), labd.data_ptr(), B, A, nc, L, lhw,
+                                 strides, 3, fgd.data_ptr(),
+                                 assign["matched_gt_inds"].data_ptr(), assign["pred_ious"].data_ptr(), nfg.data_ptr(),
+                                 gt.data_ptr(), int(use_l1), 0, g_ro.data_ptr(), g_cls.data_ptr(), stream()))
+    torch.cuda.synchronize()
+    # autograd reference with the device's assignment as fixed targets
+    r = raw.clone().requires_grad_()
+    dec = torch.cat([(r[..., :2] + torch.stack([xs, ys], 1)) * st[:, None], torch.exp(r[..., 2:4]) * st[:, None],
+                     r[..., 4:]], -1)
+    fg = assign["fg_mask"].cpu().bool()
+    matched = assign["matched_gt_inds"].cpu().long()
+    piou = assign["pred_ious"].cpu()
+    num_fg = max(int(fg.sum()), 1)
+    tot = 0.0
+    for b in range(B):
+        f = fg[b]
+        gtb = labels[b][matched[b][f]]
+        tot = tot + 5.0 * oracle.iou_loss(dec[b, f, :4], gtb[:, 1:5]).sum()
+        tot = tot + F.binary_cross_entropy_with_logits(r[b, :, 4], f.float(), reduction="sum")
+        tgt = F.one_hot(gtb[:, 0].long(), nc).float() * piou[b][f][:, None]
+        tot = tot + F.binary_cross_entropy_with_logits(r[b, f, 5:], tgt, reduction="sum")
+        if use_l1:
+            s_ = st[f]
+            l1t = torch.stack([gtb[:, 1] / s_ - xs[f], gtb[:, 2] / s_ - ys[f], torch.log(gtb[:, 3] / s_ + 1e-8),
+                               torch.log(gtb[:, 4] / s_ + 1e-8)], 1)
+            tot = tot + (r[b, f, :4] - l1t).abs().sum()
+    (2.0 * tot / num_fg).backward()
+    ref = r.grad
+    assert float(losses["total_loss"]) == pytest.approx(float(tot) / num_fg, rel=1e-5)
+    assert rel(g_ro[..., :5], ref[..., :5]) < 1e-5
+    assert float(g_ro[..., 5:].abs().max()) == 0.0
+    assert rel(g_cls, ref[..., 5:]) < 1e-5
+
+
+# ----------------------------------------------------------------- end to end
+def _model_and_batch(seed=0):
+    from yolox_amd.config import named_config
+    from yolox_amd.weights import synthetic_state_dict
+    d = np.load(os.path.join(GOLDEN, "train_yolox_s_128.npz"))
+    cfg = named_config("yolox_s")
+    m = cfg.get_model()
+    sd = synthetic_state_dict(m.state_dict(), seed=seed, bn_stats="yolox_s")
+    m.load_state_dict(sd)
+    x = torch.from_numpy(d["input_u8"]).permute(0, 3, 1, 2).float()
+    return m, sd, x, torch.from_numpy(d["labels"]), d
+
+
+@pytest.mark.parametrize("use_l1", [False, True])
+def test_train_step_fp32_matches_oracle(oracle, use_l1):
+    m, sd, x, labels, d = _model_and_batch()
+    m = m.cuda().train()
+    m.head.use_l1 = use_l1
+    out = m(x.cuda(), labels.cuda())
+    out["total_loss"].backward()
+    torch.cuda.synchronize()
+    tag = "l1" if use_l1 else "nol1"
+    # losses vs the reference's own values (fixture) and vs the oracle
+    for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss", "l1_loss", "num_fg"):
+        assert float(out[k]) == pytest.approx(float(d[f"{tag}.{k}"]), rel=1e-3, abs=1e-6), k
+    # every parameter gradient vs the oracle's autograd (CPU fp32)
+    sdo = {k: v.clone().float().requires_grad_(v.is_floating_point() and "running" not in k
+                                               and "num_batches" not in k) for k, v in sd.items()}
+    ref = oracle.forward_train(sdo, oracle.ARCHS["yolox_s"], x, labels, use_l1=use_l1)
+    ref["total_loss"].backward()
+    worst = 0.0
+    for name, p in m.named_parameters():
+        gr = sdo[name].grad
+        assert p.grad is not None, name
+        e = rel(p.grad, gr)
+        worst = max(worst, e)
+        assert e < 1e-3, (name, e)
+    # reference fixture gradients (reference autograd on the same seed)
+    for key in d.files:
+        if key.startswith(f"{tag}.grad."):
+            name = key[len(f"{tag}.grad."):]
+            assert rel(dict(m.named_parameters())[name].grad, torch.from_numpy(d[key])) < 1e-3, name
+    # running statistics were updated once with momentum 0.03
+    for name, buf in m.named_buffers():
+        if name.endswith("running_mean"):
+            assert not torch.equal(buf.cpu(), sd[name]), name
+            break
+
+
+def test_train_step_bf16_autocast_close_to_fp32():
+    """bf16 compute (autocast, as --fp16 training does with fp16) gives gradients
+    aligned with the fp32 ones (cosine per tensor with > 1k elements: min > 0.95,
+    mean > 0.99)."""
+    m, sd, x, labels, _ = _model_and_batch()
+    m = m.cuda().train()
+    out32 = m(x.cuda(), labels.cuda())
+    out32["total_loss"].backward()
+    g32 = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.load_state_dict(sd)
+    m.zero_grad(set_to_none=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out16 = m(x.cuda(), labels.cuda())
+    out16["total_loss"].backward()
+    torch.cuda.synchronize()
+    assert abs(float(out16["total_loss"]) - float(out32["total_loss"])) < 0.05 * float(out32["total_loss"])
+    cos = {n: float(F.cosine_similarity(p.grad.flatten(), g32[n].flatten(), dim=0))
+           for n, p in m.named_parameters() if p.numel() > 1000}
+    # bf16 activations / conv-output gradients (8 mantissa bits) through ~80 layers
+    assert min(cos.values()) > 0.95, min(cos.items(), key=lambda kv: kv[1])
+    assert np.mean(list(cos.values())) > 0.99, np.mean(list(cos.values()))
+
+
+def test_sgd_step_changes_eval_plan():
+    """After an optimizer step the eval plan repacks the new weights."""
+    m, _, x, labels, _ = _model_and_batch()
+    m = m.cuda().train()
+    m.eval()
+    y0 = m(x.cuda()).clone()
+    m.train()
+    m(x.cuda(), labels.cuda())["total_loss"].backward()
+    torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, nesterov=True).step()
+    m.eval()
+    y1 = m(x.cuda())
+    assert not torch.equal(y0, y1)
