@@ -57,7 +57,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layers", action="store_true", help="print a per-op time/roofline table to stderr")
     ap.add_argument("--tune-file", default="", help="JSON tile choices: loaded if present (skips tuning), else written")
-    return ap.parse_args()
+    ap.add_argument("--workload", default="infer", choices=["infer", "train"],
+                    help="infer: BASELINE configs[1] (default); train: configs[2] train step (8 images / GPU)")
+    args = ap.parse_args()
+    if args.workload == "train" and args.batch == 32:
+        args.batch = 8  # -b 64 over -d 8 (config.py:249-250)
+    return args
 
 
 def dist_setup(args):
@@ -175,9 +180,134 @@ def cpu_baseline(args, budget_s):
                       f"oracle forward + C oracle NMS conf {args.conf}) in {dt:.1f}s"}
 
 
+def cpu_baseline_train(args, budget_s):
+    """Oracle training step (fp32 PyTorch-CPU forward + SimOTA + losses + autograd)."""
+    from oracle import reference_cpu as O
+    from yolox_amd.config import named_config
+    from yolox_amd.weights import synthetic_images, synthetic_labels, synthetic_state_dict
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = named_config(args.model)
+    sd = synthetic_state_dict(cfg.get_model().state_dict(), seed=0, bn_stats=cfg.name)
+    sd = {k: v.float().requires_grad_(v.is_floating_point() and "running" not in k and "num_batches" not in k)
+          for k, v in sd.items()}
+    arch = O.ARCHS[args.model]
+    bs = 2
+    x = torch.from_numpy(O.letterbox_identity(synthetic_images(bs, args.size, args.size, seed=0)))
+    lab = torch.from_numpy(synthetic_labels(bs, args.size, args.size, seed=0))
+    n_img, t0 = 0, time.perf_counter()
+    while True:
+        O.forward_train(sd, arch, x, lab)["total_loss"].backward()
+        n_img += bs
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n_img / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n_img} images ({args.model} {args.size}x{args.size}, batch {bs}, fp32 PyTorch-CPU oracle "
+                      f"train forward + SimOTA + losses + autograd backward) in {dt:.1f}s"}
+
+
+def main_train(args, world, rank):
+    """BASELINE configs[2]: yolox_s 640 train step, per-GPU batch 8, synthetic COCO-shaped
+    targets, data parallel over RCCL (bucketed all-reduce overlapped with the HIP reverse
+    pass), SGD nesterov + EMA like Trainer.train_one_iter."""
+    from yolox_amd.dp import DistributedDataParallel
+    from yolox_amd.models import YoloxModule
+    from yolox_amd.trainer import ModelEMA, get_optimizer, train_one_iter
+    from yolox_amd.weights import synthetic_images, synthetic_labels
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.dtype]
+    model = YoloxModule.synthetic(args.model, seed=0, device=dev)
+    model.train()
+    B, S = args.batch, args.size
+    net = DistributedDataParallel(model) if world > 1 else model
+    opt = get_optimizer(model, lr=0.01 / 64 * B * world)
+    scaler = torch.amp.GradScaler("cuda") if args.dtype == "fp16" else None
+    ema = ModelEMA(model, 0.9998)
+    imgs = torch.from_numpy(synthetic_images(B, S, S, seed=1000 + rank)).to(dev).permute(0, 3, 1, 2).float()
+    if amp is not None:
+        imgs = imgs.to(amp)  # trainer.py:100 (inps.to(data_type) under --fp16)
+    labels = torch.from_numpy(synthetic_labels(B, S, S, seed=2000 + rank)).to(dev)
+
+    def step():
+        return train_one_iter(net, opt, imgs, labels, amp_dtype=amp, scaler=scaler, ema=ema)
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        out = step()
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    dt_max = max_over_ranks(dt, world)
+    gpu_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    loss = float(out["total_loss"])
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    flops_fwd = _fwd_flops(model, B, S)
+    flops = 3.0 * flops_fwd  # forward + data gradient + weight gradient of every conv
+    achieved = flops / (gpu_ms * 1e-3) / 1e12
+    peak = PEAK_BF16_TFLOPS if amp is not None else 157.3
+    result = {
+        "metric": "images/sec (train step: fwd + SimOTA/loss + bwd + DP all-reduce + SGD + EMA) YOLOX-s 640x640",
+        "value": round(world * B * args.steps / dt_max, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic uniform [0,255] images + COCO-shaped random targets (G ~ U{1..50}), seeded weights",
+        "config": {"workload": f"{args.model} {S}x{S} train step, batch {B}/GPU (BASELINE configs[2]: -d 8 -b 64)",
+                   "batch_per_gpu": B, "global_batch": B * world, "image_size": S,
+                   "parallelism": f"dp{world} (bucketed RCCL all-reduce overlapped with the reverse pass)"},
+        "roofline": {"kernel": "whole step (conv fwd/dgrad/wgrad dominate; HIP events around each step)",
+                     "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "algorithmic_flops_per_launch": flops, "step_gpu_ms": round(gpu_ms, 3)},
+        "last_loss": round(loss, 4),
+    }
+    if not args.no_cpu_baseline and world == 1:
+        result["cpu_baseline"] = cpu_baseline_train(args, args.cpu_seconds)
+    else:
+        result["cpu_baseline"] = None
+    print(json.dumps(result))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def _fwd_flops(model, B, S) -> float:
+    """Algorithmic conv FLOPs of one forward (the planner's count, no device work)."""
+    from yolox_amd.engine import PlanCtx
+    ctx = PlanCtx(B, torch.float32, torch.device("cpu"))
+    feats = model.backbone.plan(ctx, ctx.image(S, S))
+    from yolox_amd.engine import OutBuffer
+    model.head.plan(ctx, feats, OutBuffer(sum(f.lh * f.lw for f in feats), 5 + model.head.num_classes))
+    return ctx.flops
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
+    if args.workload == "train":
+        return main_train(args, world, rank)
     from yolox_amd import _native as N
     from yolox_amd.models import YoloxModule
     from yolox_amd.utils.boxes import postprocess_device

@@ -187,14 +187,31 @@ struct FinArgs {
     float *out0, *out1;  // BWD: dgamma, dbeta; SUM: out0
 };
 
+// 8 channels per block, 32 lanes per channel sum the per-block partials (strided, in
+// double), then a fixed-order tree over the lanes: deterministic.
 __global__ __launch_bounds__(256) void chan_finalize(FinArgs f) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= f.C) return;
+    __shared__ double red[2][256];
+    const int j = threadIdx.x >> 5, lane = threadIdx.x & 31;
+    const int c = blockIdx.x * 8 + j;
     double t1 = 0.0, t2 = 0.0;
-    for (int b = 0; b < f.nblk; ++b) {
-        t1 += f.partial[((long long)b * 2) * f.C + c];
-        t2 += f.partial[((long long)b * 2 + 1) * f.C + c];
+    if (c < f.C)
+        for (int b = lane; b < f.nblk; b += 32) {
+            t1 += f.partial[((long long)b * 2) * f.C + c];
+            t2 += f.partial[((long long)b * 2 + 1) * f.C + c];
+        }
+    red[0][threadIdx.x] = t1;
+    red[1][threadIdx.x] = t2;
+    __syncthreads();
+    for (int s = 16; s > 0; s >>= 1) {
+        if (lane < s) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + s];
+            red[1][threadIdx.x] += red[1][threadIdx.x + s];
+        }
+        __syncthreads();
     }
+    if (lane != 0 || c >= f.C) return;
+    t1 = red[0][threadIdx.x];
+    t2 = red[1][threadIdx.x];
     if (f.mode == RED_STATS) {
         const double m1 = t1 / f.M;
         const double mean = (double)f.partial[(long long)f.nblk * 2 * f.C + c] + m1;
@@ -271,7 +288,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply(TView y, TView g, const 
 // ------------------------------------------------------------------ weight gradient
 struct WgradParams {
     int in_h, in_w, out_h, out_w, cin, cout, kh, kw, stride, pad, ohw, M;
-    int nsrc, src0_ch;
+    int nsrc, src0_ch, B;
     const void* sptr[2];
     int scs[2], sw[2], sup[2];
     long long sbs[2];
@@ -283,6 +300,8 @@ struct WgradParams {
     int sps, nst;  // stages per split, total pixel stages
     int ntc;       // channel tiles per tap
 };
+
+__device__ __attribute__((aligned(16))) uint4 g_wg_zero[4];
 
 // In-register transpose of an EPC x EPC block of T: a[e] = EPC channels of pixel e ->
 // a[j] = EPC pixels of channel j.
@@ -311,11 +330,18 @@ __device__ __forceinline__ void transpose_chunks(uint4 (&a)[4]) {  // 32-bit ele
     for (int j = 0; j < 4; ++j) a[j] = b[j];
 }
 
+// LDS row placement of the wgrad image: the chunk XOR of the forward kernel plus
+// (r >> 3) & 7 on the low bits.  A loader lane writes 8 consecutive rows of one chunk and
+// neighbouring lanes are 8 rows apart, so without the second term every lane of a
+// ds_write_b128 hits the same 32-bank group; with it 8 lanes cover all banks.  A fragment
+// read (16 consecutive rows, one chunk) stays a permutation of one 256-byte block.
+__device__ __forceinline__ int wg_row(int r, int sw) { return r ^ sw ^ ((r >> 3) & 7); }
+
 template <typename T, int TN, int TM, int WR, int WC, int KS>
 __global__ __launch_bounds__(256) void conv_wgrad(WgradParams p) {
     constexpr int EPC = Chunk<T>::N;
     constexpr int CPR = 4 * KS;           // 16-byte chunks (of EPC pixels) per row per stage
-    constexpr int KP = CPR * EPC;         // pixels per stage
+    static_assert(CPR * EPC > 0, "stage");
     constexpr int NA = (TN / EPC) * CPR;  // transpose items: A = dY rows (cout)
     constexpr int NB = (TM / EPC) * CPR;  //                  B = X rows (cin of the tap)
     constexpr int NIT = (NA + NB + 255) / 256;
@@ -334,52 +360,52 @@ __global__ __launch_bounds__(256) void conv_wgrad(WgradParams p) {
     const int st0 = blockIdx.x * p.sps, st1 = min(p.nst, st0 + p.sps);
 
     uint4 rg[NIT][EPC];
+    // K runs over "runs": EPC consecutive output pixels of one output row (rows padded to
+    // a multiple of EPC), so a run is one (b, oy, ox0) decomposition and its input pixels
+    // for the tap are one input row at stride `stride`.  Loads are branch-free: invalid
+    // lanes read a zero chunk.
+    const int rpr = (p.out_w + EPC - 1) / EPC, rpi = rpr * p.out_h;
     auto gload = [&](int stg) {
-        const int pbase = stg * KP;
 #pragma unroll
         for (int i = 0; i < NIT; ++i) {
             const int it = tid + 256 * i;
-#pragma unroll
-            for (int e = 0; e < EPC; ++e) rg[i][e] = make_uint4(0, 0, 0, 0);
-            if (it < NA) {
-                const int ci = it % (TN / EPC), pc = it / (TN / EPC);
+            if (it >= NA + NB) continue;
+            const bool isa = it < NA;
+            const int jt = isa ? it : it - NA;
+            const int rows = isa ? TN : TM;
+            const int ci = jt % (rows / EPC), pc = jt / (rows / EPC);
+            const int R = stg * CPR + pc;
+            const int b = R / rpi, rem = R - b * rpi;
+            const int oy = rem / rpr, ox0 = (rem - oy * rpr) * EPC;
+            const bool run_ok = b < p.B;
+            const T* zero = (const T*)g_wg_zero;
+            if (isa) {
                 const int n = n0 + ci * EPC;
-                if (n < p.cout) {
+                const bool ok = run_ok && n < p.cout;
+                const T* base = (const T*)p.dy + (ok ? (long long)b * p.dybs + n : 0);
+                const int o0 = (oy * p.out_w + ox0) * p.dycs;
 #pragma unroll
-                    for (int e = 0; e < EPC; ++e) {
-                        const int m = pbase + pc * EPC + e;
-                        if (m < p.M) {
-                            const int b = m / p.ohw, pix = m - b * p.ohw;
-                            rg[i][e] = *(const uint4*)((const T*)p.dy + (long long)b * p.dybs +
-                                                       (long long)pix * p.dycs + n);
-                        }
-                    }
+                for (int e = 0; e < EPC; ++e) {
+                    const bool v = ok && ox0 + e < p.out_w;
+                    rg[i][e] = *(const uint4*)(v ? base + o0 + e * p.dycs : zero);
                 }
-            } else if (it < NA + NB) {
-                const int jt = it - NA;
-                const int ci = jt % (TM / EPC), pc = jt / (TM / EPC);
+            } else {
                 int c = c0 + ci * EPC;
-                if (c < p.cin) {
-                    int s = 0;
-                    if (p.nsrc == 2 && c >= p.src0_ch) {
-                        s = 1;
-                        c -= p.src0_ch;
-                    }
-                    const T* sp = (const T*)p.sptr[s];
-                    const int up = p.sup[s];
+                int s = 0;
+                if (p.nsrc == 2 && c >= p.src0_ch) {
+                    s = 1;
+                    c -= p.src0_ch;
+                }
+                const int iy = oy * p.stride - p.pad + ky;
+                const bool ok = run_ok && c0 + ci * EPC < p.cin && iy >= 0 && iy < p.in_h;
+                const int up = p.sup[s], scs = p.scs[s];
+                const T* base = (const T*)p.sptr[s] + (ok ? (long long)b * p.sbs[s] + c : 0);
+                const int rowoff = (iy >> up) * p.sw[s];
 #pragma unroll
-                    for (int e = 0; e < EPC; ++e) {
-                        const int m = pbase + pc * EPC + e;
-                        if (m < p.M) {
-                            const int b = m / p.ohw, pix = m - b * p.ohw;
-                            const int oy = pix / p.out_w, ox = pix - oy * p.out_w;
-                            const int iy = oy * p.stride - p.pad + ky, ix = ox * p.stride - p.pad + kx;
-                            if (iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w)
-                                rg[i][e] = *(const uint4*)(sp + (long long)b * p.sbs[s] +
-                                                           ((long long)(iy >> up) * p.sw[s] + (ix >> up)) * p.scs[s] +
-                                                           c);
-                        }
-                    }
+                for (int e = 0; e < EPC; ++e) {
+                    const int ix = (ox0 + e) * p.stride - p.pad + kx;
+                    const bool v = ok && ox0 + e < p.out_w && ix >= 0 && ix < p.in_w;
+                    rg[i][e] = *(const uint4*)(v ? base + (rowoff + (ix >> up)) * scs : zero);
                 }
             }
         }
@@ -401,7 +427,7 @@ __global__ __launch_bounds__(256) void conv_wgrad(WgradParams p) {
 #pragma unroll
             for (int j = 0; j < EPC; ++j) {
                 const int r = ci * EPC + j;
-                *(uint4*)(base + (pc * rows + (r ^ sw_)) * 16) = rg[i][j];
+                *(uint4*)(base + (pc * rows + wg_row(r, sw_)) * 16) = rg[i][j];
             }
         }
     };
@@ -421,9 +447,9 @@ __global__ __launch_bounds__(256) void conv_wgrad(WgradParams p) {
             const int chunk = s * 4 + fq, sw_ = 2 * fq + s;
             uint4 af[FR], bf[FC];
 #pragma unroll
-            for (int i = 0; i < FR; ++i) af[i] = *(const uint4*)(A + (chunk * TN + ((wr * WTN + i * 16 + frow) ^ sw_)) * 16);
+            for (int i = 0; i < FR; ++i) af[i] = *(const uint4*)(A + (chunk * TN + wg_row(wr * WTN + i * 16 + frow, sw_)) * 16);
 #pragma unroll
-            for (int j = 0; j < FC; ++j) bf[j] = *(const uint4*)(B + (chunk * TM + ((wc * WTM + j * 16 + frow) ^ sw_)) * 16);
+            for (int j = 0; j < FC; ++j) bf[j] = *(const uint4*)(B + (chunk * TM + wg_row(wc * WTM + j * 16 + frow, sw_)) * 16);
 #pragma unroll
             for (int i = 0; i < FR; ++i)
 #pragma unroll
@@ -477,43 +503,78 @@ __global__ __launch_bounds__(256) void pack_dgrad(const float* w, int cout, int 
 }
 
 // ------------------------------------------------------------------ SPP / upsample backward
-// One thread per (pixel, channel) of the SPP input x (channels [0, c) of `cat`):
-// every pool output whose window holds this pixel checks whether its argmax (first
-// maximum, row-major scan, -inf padding) is this pixel.  dx = dcat[:, :c] + those.
+// Block = (kSppCpb channels, image): the plane lives in LDS.  Per pool radius r (2, 4, 6):
+// horizontal pass -> first max column of each row window; vertical pass -> first max
+// row among those = torch's argmax (first maximum in row-major scan, -inf padding);
+// then every input pixel GATHERS the gradients of the outputs whose argmax it is (fixed
+// order, no atomics: deterministic).  dx = dcat[:, :c] + gathered.
+constexpr int kSppCpb = 4;
+
 template <typename T>
 __global__ __launch_bounds__(256) void spp_bwd(TView cat, int H, int W, int c, const float* dcat, float* dx,
                                                int B) {
-    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-    const long long total = (long long)B * H * W * c;
-    if (idx >= total) return;
-    const int ch = (int)(idx % c);
-    const long long m = idx / c;
-    const int b = (int)(m / (H * W)), pix = (int)(m - (long long)b * H * W);
-    const int y = pix / W, x = pix - y * W;
+    extern __shared__ __attribute__((aligned(16))) char sm[];
+    const int HW = H * W, n = HW * kSppCpb;
+    float* pl = (float*)sm;                                   // plane
+    float* hv = pl + n;                                       // row-window max
+    unsigned short* hc = (unsigned short*)(hv + n);           // its column
+    unsigned short* am = hc + n;                              // [3][n] argmax pixel per output
+    const int c0 = blockIdx.x * kSppCpb, b = blockIdx.y;
     const T* xb = (const T*)cat.ptr + (long long)b * cat.bs;
-    const float* db = dcat + (long long)b * H * W * 4 * c;
-    float g = db[(long long)pix * 4 * c + ch];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int r = 2 + 2 * k;  // 5, 9, 13
-        for (int oy = max(0, y - r); oy <= min(H - 1, y + r); ++oy)
-            for (int ox = max(0, x - r); ox <= min(W - 1, x + r); ++ox) {
-                // argmax of output (oy, ox)'s window
-                float best = -INFINITY;
-                int by = -1, bx = -1;
-                for (int iy = max(0, oy - r); iy <= min(H - 1, oy + r); ++iy)
-                    for (int ix = max(0, ox - r); ix <= min(W - 1, ox + r); ++ix) {
-                        const float v = to_f32(xb[((long long)iy * W + ix) * cat.cs + ch]);
-                        if (v > best || by < 0) {
-                            best = v;
-                            by = iy;
-                            bx = ix;
-                        }
-                    }
-                if (by == y && bx == x) g += db[((long long)oy * W + ox) * 4 * c + (k + 1) * c + ch];
-            }
+    const float* db = dcat + (long long)b * HW * 4 * c;
+    for (int q = threadIdx.x; q < n; q += 256) {
+        const int pix = q / kSppCpb, j = q - pix * kSppCpb;
+        pl[q] = c0 + j < c ? to_f32(xb[(long long)pix * cat.cs + c0 + j]) : 0.0f;
     }
-    dx[m * c + ch] = g;
+    __syncthreads();
+    for (int k = 0; k < 3; ++k) {
+        const int r = 2 + 2 * k;
+        for (int q = threadIdx.x; q < n; q += 256) {
+            const int pix = q / kSppCpb, j = q - pix * kSppCpb;
+            const int y = pix / W, x = pix - y * W;
+            float best = 0.0f;
+            int bc = -1;
+            for (int xx = max(0, x - r); xx <= min(W - 1, x + r); ++xx) {
+                const float v = pl[(y * W + xx) * kSppCpb + j];
+                if (bc < 0 || v > best) {
+                    best = v;
+                    bc = xx;
+                }
+            }
+            hv[q] = best;
+            hc[q] = (unsigned short)bc;
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q < n; q += 256) {
+            const int pix = q / kSppCpb, j = q - pix * kSppCpb;
+            const int y = pix / W, x = pix - y * W;
+            float best = 0.0f;
+            int br = -1;
+            for (int yy = max(0, y - r); yy <= min(H - 1, y + r); ++yy) {
+                const float v = hv[(yy * W + x) * kSppCpb + j];
+                if (br < 0 || v > best) {
+                    best = v;
+                    br = yy;
+                }
+            }
+            am[k * n + q] = (unsigned short)(br * W + hc[(br * W + x) * kSppCpb + j]);
+        }
+        __syncthreads();
+    }
+    for (int q = threadIdx.x; q < n; q += 256) {
+        const int pix = q / kSppCpb, j = q - pix * kSppCpb;
+        if (c0 + j >= c) continue;
+        const int y = pix / W, x = pix - y * W;
+        float g = db[(long long)pix * 4 * c + c0 + j];
+        for (int k = 0; k < 3; ++k) {
+            const int r = 2 + 2 * k;
+            for (int oy = max(0, y - r); oy <= min(H - 1, y + r); ++oy)
+                for (int ox = max(0, x - r); ox <= min(W - 1, x + r); ++ox)
+                    if (am[k * n + (oy * W + ox) * kSppCpb + j] == pix)
+                        g += db[((long long)oy * W + ox) * 4 * c + (k + 1) * c + c0 + j];
+        }
+        dx[((long long)b * HW + pix) * c + c0 + j] = g;
+    }
 }
 
 __global__ __launch_bounds__(256) void upsample_bwd(const float* g, int B, int h, int w, int C, float* dst) {
@@ -613,7 +674,7 @@ int run_reduce(int mode, int dt, int B, const yxh_src* x, const yxh_src* g, cons
     f.C = C;
     f.M = a.M;
     f.mode = mode;
-    hipLaunchKernelGGL(chan_finalize, dim3((C + 255) / 256), dim3(256), 0, st, f);
+    hipLaunchKernelGGL(chan_finalize, dim3((C + 7) / 8), dim3(256), 0, st, f);
     YXH_CHECK_LAUNCH("chan_finalize");
     return YXH_OK;
 }
@@ -702,7 +763,8 @@ int launch_wgrad_t(WgradParams p, hipStream_t st) {
     const int ntn = (p.cout + TN - 1) / TN;
     p.ntc = (p.cin + TM - 1) / TM;
     const int ntap = p.kh * p.kw;
-    p.nst = (p.M + KP - 1) / KP;
+    p.nst = (int)(((long long)p.B * p.out_h * ((p.out_w + EPC - 1) / EPC) + 4 * KS - 1) / (4 * KS));
+    (void)KP;
     // ~2 blocks per CU over the whole grid; at least 8 stages per split
     const long long tiles = (long long)ntn * ntap * p.ntc;
     long long splits = (512 + tiles - 1) / tiles;
@@ -722,7 +784,11 @@ template <typename T>
 int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
     // default: 64 x 64 (cout x cin), 2 x 2 waves; 4 slabs (bf16: 128 pixels) per stage
     switch (tile) {
-        case 0:
+        case 0:  // by shape: the smallest tile that covers cout, wide tiles for wide layers
+            if (p.cout <= 16) return wgrad_tile<T>(4, p, st);
+            if (p.cout <= 32) return wgrad_tile<T>(3, p, st);
+            if (p.cout >= 128 && p.cin >= 128) return wgrad_tile<T>(2, p, st);
+            return wgrad_tile<T>(1, p, st);
         case 1: return sizeof(T) == 4 ? launch_wgrad_t<T, 64, 64, 2, 2, 2>(p, st) : launch_wgrad_t<T, 64, 64, 2, 2, 4>(p, st);
         case 2: return launch_wgrad_t<T, 128, 128, 2, 2, 2>(p, st);
         case 3: return launch_wgrad_t<T, 32, 64, 1, 4, 2>(p, st);
@@ -766,6 +832,10 @@ int conv_wgrad_launch(const yxh_wgrad_desc* d, hipStream_t st) {
     const long long M = (long long)d->batch * p.ohw;
     YXH_CHECK_ARG(M < (1LL << 31), "too many pixels");
     p.M = (int)M;
+    p.B = d->batch;
+    YXH_CHECK_ARG((long long)d->out_h * d->out_w * g.cstride < (1LL << 31) &&
+                      (long long)d->src[0].h * d->src[0].w * d->src[0].cstride < (1LL << 31),
+                  "wgrad: per-image offsets exceed 32 bits");
     p.nsrc = d->nsrc;
     p.src0_ch = d->src[0].channels;
     for (int s = 0; s < d->nsrc; ++s) {
@@ -806,10 +876,17 @@ int pack_dgrad_launch(const float* w, int cout, int cin, int kh, int kw, int c_b
 
 int spp_bwd_launch(int dt, int B, const yxh_src* cat, int c, const float* dcat, float* dx, hipStream_t st) {
     YXH_CHECK_ARG(cat && cat->ptr && dcat && dx && B > 0 && c > 0 && cat->cstride >= 4 * c, "spp_bwd arguments");
-    const long long total = (long long)B * cat->h * cat->w * c;
-    dim3 grid((unsigned)((total + 255) / 256));
+    const int HW = cat->h * cat->w;
+    const size_t lds = (size_t)HW * kSppCpb * (4 + 4 + 2 + 6);
+    YXH_CHECK_ARG(lds <= 160 * 1024 && HW < 65536, "spp_bwd plane %dx%d too large for LDS", cat->h, cat->w);
+    dim3 grid((c + kSppCpb - 1) / kSppCpb, B);
     TView v = tview(cat, c);
-#define YXH_SPPB(T) hipLaunchKernelGGL(spp_bwd<T>, grid, dim3(256), 0, st, v, cat->h, cat->w, c, dcat, dx, B)
+#define YXH_SPPB(T)                                                                                        \
+    do {                                                                                                   \
+        (void)hipFuncSetAttribute((const void*)spp_bwd<T>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+                                  (int)lds);                                                               \
+        hipLaunchKernelGGL(spp_bwd<T>, grid, dim3(256), lds, st, v, cat->h, cat->w, c, dcat, dx, B);       \
+    } while (0)
     if (dt == YXH_BF16) YXH_SPPB(bf16);
     else if (dt == YXH_F16) YXH_SPPB(f16);
     else YXH_SPPB(float);

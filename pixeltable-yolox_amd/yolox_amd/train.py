@@ -131,6 +131,7 @@ class TrainGraph:
         self.zero_bias = torch.zeros(MAX_CHANNELS, dtype=torch.float32, device=self.device)
         self.tape: list[Callable[[], None]] = []
         self.on_param_ready: Optional[Callable[[nn.Parameter], None]] = None
+        self.on_backward_end: Optional[Callable[[], None]] = None  # e.g. GradReducer.finish
         self._fwd_w: dict = {}
         self.grad_total = torch.ones((), dtype=torch.float32, device=self.device)
 
@@ -481,6 +482,8 @@ class TrainGraph:
             fn()
         self.tape = []
         self._keep = None
+        if self.on_backward_end is not None:
+            self.on_backward_end()
         self.grads.publish(prev)
 
 
