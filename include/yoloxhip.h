@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 3
+#define YXH_ABI_VERSION 4
 
 enum yxh_status {
     YXH_OK = 0,
@@ -337,6 +337,14 @@ typedef struct {
 
 int yxh_run_ops(const yxh_op* ops, int32_t n, void* stream);
 int yxh_graph_create(const yxh_op* ops, int32_t n, void* stream, void** graph_exec);
+/* yxh_graph_create_lanes: capture the op list with independent branches on separate
+ * streams ("lanes"): op i runs on lane lanes[i] after every op listed in
+ * deps[dep_off[i] .. dep_off[i+1]) (indices < i); cross-lane dependencies become graph
+ * edges, same-lane order is stream order.  Lane 0 forks the others at the start and
+ * joins them at the end.  Used to overlap the three head levels with each other and
+ * with the PAFPN bottom-up path (yolo_head.py:140-211 runs the levels independently). */
+int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, const int32_t* dep_off,
+                           const int32_t* deps, int32_t nlanes, void* stream, void** graph_exec);
 int yxh_graph_launch(void* graph_exec, void* stream);
 int yxh_graph_destroy(void* graph_exec);
 

@@ -473,7 +473,8 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         tile = d->tile >> 1;
         const int want_ks = (d->tile & 1) + 1;
         YXH_CHECK_ARG((tile > 0 && tile < kNumTiles) || (tile > 16 && tile < 16 + kNumTiles) ||
-                          (tile > 32 && tile <= 32 + kNumRowTiles) || (tile > 64 && tile <= 64 + kNumPwTiles),
+                          (tile > 32 && tile <= 32 + kNumRowTiles) || (tile > 64 && tile <= 64 + kNumPwTiles) ||
+                          (tile > 80 && tile <= 80 + kNumPwrTiles),
                       "tile %d", d->tile);
         YXH_CHECK_ARG(want_ks == 1 || ks == 2, "2-slab staging not possible for this conv");
         ks = want_ks;
@@ -486,6 +487,7 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         set_error("dilated (upsample == 2) sources run on the register-staged kernel only (tile ids 1-9)");
         return YXH_EUNSUPPORTED;
     }
+    if (tile > 80) return conv_pwr_dispatch(dt, tile - 80, p, st);
     if (tile > 64) return conv_pw_dispatch(dt, tile - 64, p, ks, st);
     if (tile > 32) return conv_rows_dispatch(dt, tile - 32, p, ks, st);
     if (tile > 16) return conv_glds_dispatch(dt, tile - 16, p, ks, st);

@@ -225,5 +225,8 @@ constexpr int kNumRowTiles = 19;
 // Persistent streaming 1x1 conv (conv_pw.hip): tile ids 65..64+kNumPwTiles
 int conv_pw_dispatch(int dtype, int id, const ConvParams& p, int ks, hipStream_t st);
 constexpr int kNumPwTiles = 6;
+// Register-operand 1x1 conv (conv_pwr.hip): tile ids 81..80+kNumPwrTiles
+int conv_pwr_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
+constexpr int kNumPwrTiles = 2;
 
 }  // namespace yxh

@@ -2,7 +2,10 @@
 // executor and hipGraph capture/replay of a whole forward pass.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <vector>
 
 #include "yxh_common.hpp"
 
@@ -241,6 +244,84 @@ int yxh_graph_create(const yxh_op* ops, int32_t n, void* stream, void** graph_ex
     hipGraphExec_t ge = nullptr;
     rc = check_hip(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0), "instantiate");
     (void)hipGraphDestroy(g);
+    if (rc) return rc;
+    *graph_exec = (void*)ge;
+    return YXH_OK;
+}
+
+int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, const int32_t* dep_off,
+                           const int32_t* deps, int32_t nlanes, void* stream, void** graph_exec) {
+    constexpr int kMaxLanes = 8;
+    YXH_CHECK_ARG(graph_exec && (ops || n == 0) && lanes && dep_off, "null argument");
+    YXH_CHECK_ARG(nlanes >= 1 && nlanes <= kMaxLanes, "nlanes %d", nlanes);
+    YXH_CHECK_ARG(dep_off[0] == 0, "dep_off[0] must be 0");
+    for (int i = 0; i < n; ++i) {
+        YXH_CHECK_ARG(lanes[i] >= 0 && lanes[i] < nlanes, "op %d lane %d", i, lanes[i]);
+        YXH_CHECK_ARG(dep_off[i + 1] >= dep_off[i], "dep_off not monotone at %d", i);
+        for (int k = dep_off[i]; k < dep_off[i + 1]; ++k)
+            YXH_CHECK_ARG(deps && deps[k] >= 0 && deps[k] < i, "op %d dependency %d", i, deps ? deps[k] : -1);
+    }
+    (void)stream;
+    hipStream_t st[kMaxLanes] = {};
+    hipEvent_t fork = nullptr;
+    std::vector<hipEvent_t> ev(n, nullptr), join(nlanes, nullptr);
+    int rc = YXH_OK, orc = YXH_OK;
+    bool capturing = false;
+    hipGraph_t g = nullptr;
+    for (int l = 0; l < nlanes && !rc; ++l)
+        rc = check_hip(hipStreamCreateWithFlags(&st[l], hipStreamNonBlocking), "lane stream");
+    if (!rc) rc = check_hip(hipEventCreateWithFlags(&fork, hipEventDisableTiming), "event");
+    for (int i = 0; i < n && !rc; ++i) rc = check_hip(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "event");
+    for (int l = 0; l < nlanes && !rc; ++l)
+        rc = check_hip(hipEventCreateWithFlags(&join[l], hipEventDisableTiming), "event");
+    const bool dbg = getenv("YXH_DEBUG_LANES") != nullptr;
+#define LDBG(...) do { if (dbg) { fprintf(stderr, __VA_ARGS__); fflush(stderr); } } while (0)
+    LDBG("lanes: n=%d nlanes=%d rc=%d\n", n, nlanes, rc);
+    if (!rc) {
+        rc = check_hip(hipStreamBeginCapture(st[0], hipStreamCaptureModeThreadLocal), "begin capture");
+        capturing = !rc;
+    }
+    LDBG("lanes: capture begun rc=%d\n", rc);
+    if (!rc) rc = check_hip(hipEventRecord(fork, st[0]), "fork");
+    for (int l = 1; l < nlanes && !rc; ++l) rc = check_hip(hipStreamWaitEvent(st[l], fork, 0), "fork wait");
+    for (int i = 0; i < n && !rc && !orc; ++i) {
+        hipStream_t s = st[lanes[i]];
+        for (int k = dep_off[i]; k < dep_off[i + 1] && !rc; ++k)
+            if (lanes[deps[k]] != lanes[i]) rc = check_hip(hipStreamWaitEvent(s, ev[deps[k]], 0), "dependency wait");
+        if (rc) break;
+        LDBG("lanes: op %d kind %d lane %d deps %d\n", i, ops[i].kind, lanes[i], dep_off[i + 1] - dep_off[i]);
+        orc = run_op(ops[i], s);
+        if (orc) {
+            char tmp[512];
+            snprintf(tmp, sizeof(tmp), "op %d: %s", i, g_err);
+            set_error("%s", tmp);
+        } else {
+            rc = check_hip(hipEventRecord(ev[i], s), "op event");
+        }
+    }
+    LDBG("lanes: ops done rc=%d orc=%d\n", rc, orc);
+    if (capturing) {  // join every lane (also after an error, so the capture ends cleanly)
+        for (int l = 1; l < nlanes; ++l) {
+            (void)hipEventRecord(join[l], st[l]);
+            (void)hipStreamWaitEvent(st[0], join[l], 0);
+        }
+        const int erc = check_hip(hipStreamEndCapture(st[0], &g), "end capture");
+        if (!rc) rc = erc;
+    }
+    LDBG("lanes: capture ended rc=%d\n", rc);
+    hipGraphExec_t ge = nullptr;
+    if (!rc && !orc) rc = check_hip(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0), "instantiate");
+    LDBG("lanes: instantiated rc=%d\n", rc);
+#undef LDBG
+    if (g) (void)hipGraphDestroy(g);
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : join)
+        if (e) (void)hipEventDestroy(e);
+    if (fork) (void)hipEventDestroy(fork);
+    for (int l = 0; l < nlanes; ++l)
+        if (st[l]) (void)hipStreamDestroy(st[l]);
+    if (orc) return orc;
     if (rc) return rc;
     *graph_exec = (void*)ge;
     return YXH_OK;

@@ -16,6 +16,7 @@ hipGraph (``capture()`` / ``replay()``).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import sys
 from dataclasses import dataclass, field
 from typing import Optional
@@ -99,6 +100,7 @@ class ImageRef:
 class OpRec:
     kind: int
     args: dict = field(default_factory=dict)
+    lane: int = 0  # graph branch (yxh_graph_create_lanes); 0 = backbone / neck
 
 
 class PlanCtx:
@@ -230,10 +232,10 @@ class OutBuffer:
 
 # tile codes (2 * id + slabs - 1); ids 1-9 register-staged conv_igemm, 17-25 the same
 # tiles on the LDS-DMA conv_glds kernel, 33-51 the row-tiled 3x3 conv_rows kernel,
-# 65-70 the persistent streaming 1x1 conv_pw kernel
-# (yoloxhip.h yxh_conv_desc.tile)
+# 65-70 the persistent streaming 1x1 conv_pw kernel, 81-82 the register-operand 1x1
+# conv_pwr kernel (yoloxhip.h yxh_conv_desc.tile)
 TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
-                   + list(range(65, 71)) for k in (0, 1)]
+                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82]
 _TUNE_CACHE: dict = {}
 
 
@@ -256,6 +258,41 @@ def _tune_key(d) -> tuple:
     return (d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w, d.cin, d.cout, d.kh, d.stride, d.nsrc,
             d.src[0].channels, d.src[0].upsample, d.src[1].upsample if d.nsrc > 1 else 0,
             bool(d.residual), d.dst_dtype, d.dst_cstride == d.cout, d.act >= N.ACT_DECODE)
+
+
+def op_dependencies(ops) -> list:
+    """Per op, the earlier ops it must wait for, from the buffers it reads and writes
+    (read-after-write, write-after-write, write-after-read).  Arena buffers never alias
+    (bump allocation); the input image and the [B, A, 5+C] output rows (disjoint anchor
+    ranges per level, written once) are not tracked."""
+    last_w: dict = {}
+    readers: dict = {}
+    deps = []
+    for i, r in enumerate(ops):
+        a = r.args
+        if r.kind == N.OP_SPP:
+            reads, writes = [a["buf"]], [a["buf"]]
+        elif r.kind in (N.OP_FOCUS, N.OP_STEM):
+            reads, writes = [], [a["dst"].buf]
+        else:
+            reads = [v.buf for v in a["srcs"]]
+            if a.get("residual") is not None:
+                reads.append(a["residual"].buf)
+            writes = [a["out"].buf] if a.get("out") is not None else []
+        d = set()
+        for b in reads + writes:
+            if id(b) in last_w:
+                d.add(last_w[id(b)])
+        for b in writes:
+            d.update(readers.get(id(b), ()))
+        d.discard(i)
+        for b in reads:
+            readers.setdefault(id(b), []).append(i)
+        for b in writes:
+            last_w[id(b)] = i
+            readers[id(b)] = []
+        deps.append(sorted(d))
+    return deps
 
 
 class Plan:
@@ -290,6 +327,10 @@ class Plan:
         head.plan(ctx, feats, self.out_spec, train=train)
         self.ctx = ctx
         self.anchors = anchors
+        # independent head levels run as separate graph branches (YOLOX_AMD_LANES=0: one stream)
+        self.nlanes = 1 + max((r.lane for r in ctx.ops), default=0)
+        self._deps = op_dependencies(ctx.ops)
+        self.use_lanes = os.environ.get("YOLOX_AMD_LANES", "1") != "0"
         self.flops = ctx.flops * self.nchunks
         # ------------------------------------------------ arenas
         off = 0
@@ -487,9 +528,34 @@ class Plan:
             self._graph = None
         g = C.c_void_p()
         torch.cuda.synchronize(self.device)
-        N.check(self.lib.yxh_graph_create(self._ops, len(self._ops), N.stream_ptr(self.device), C.byref(g)),
-                "graph capture")
+        if self.use_lanes and self.nlanes > 1:
+            lanes, off, deps = self._lane_arrays()
+            N.check(self.lib.yxh_graph_create_lanes(self._ops, len(self._ops), lanes, off, deps, self.nlanes,
+                                                    N.stream_ptr(self.device), C.byref(g)), "graph capture (lanes)")
+        else:
+            N.check(self.lib.yxh_graph_create(self._ops, len(self._ops), N.stream_ptr(self.device), C.byref(g)),
+                    "graph capture")
         self._graph = g
+
+    def _lane_arrays(self):
+        """(lanes, dep_off, deps) over all chunks.  Chunk c reuses chunk c-1's arena: its
+        first op (lane 0) also waits for the last op of every lane of c-1; the head lanes
+        of chunk c follow from their inputs (lane-0 ops of chunk c) and stream order."""
+        n = self._nops
+        last = {}
+        for i, r in enumerate(self.ctx.ops):
+            last[r.lane] = i
+        lanes, off, deps = [], [0], []
+        for c in range(self.nchunks):
+            for i, r in enumerate(self.ctx.ops):
+                lanes.append(r.lane)
+                d = {c * n + j for j in self._deps[i]}
+                if c and i == 0:
+                    d.update((c - 1) * n + j for j in last.values())
+                deps.extend(sorted(d))
+                off.append(len(deps))
+        arr = lambda v: (C.c_int32 * max(1, len(v)))(*v)  # noqa: E731
+        return arr(lanes), arr(off), arr(deps)
 
     def replay(self) -> torch.Tensor:
         if self._graph is None:

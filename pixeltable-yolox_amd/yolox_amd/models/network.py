@@ -248,6 +248,7 @@ class YoloxHead(_Planned):
         rows straight into ``out`` [B, A, 5+C] (yolo_head.py:140-251)."""
         a_off = 0
         for k, x in enumerate(feats):
+            n0 = len(ctx.ops)
             s = self.stems[k].plan(ctx, [x])
             c0, r0 = self.cls_convs[k][0], self.reg_convs[k][0]
             if isinstance(c0, BaseConv) and isinstance(r0, BaseConv):
@@ -260,5 +261,7 @@ class YoloxHead(_Planned):
             c = self.cls_convs[k][1].plan(ctx, [c])
             r = self.reg_convs[k][1].plan(ctx, [r])
             ctx.head_preds(k, self, c, r, out, a_off, self.strides[k], train)
+            for rec in ctx.ops[n0:]:  # levels are independent: one graph branch each
+                rec.lane = 1 + k
             a_off += x.lh * x.lw
         return out

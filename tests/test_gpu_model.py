@@ -149,3 +149,24 @@ def test_chunked_plan_matches_whole_batch():
     assert torch.equal(chunked.replay().clone(), a)
     with pytest.raises(ValueError, match="chunk"):
         Plan(m, 4, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8, chunk=3)
+
+
+def test_lane_graph_matches_single_stream_graph():
+    """The head levels run as separate hipGraph branches (lanes) beside the PAFPN
+    bottom-up path; the result equals the single-stream graph bit for bit (chunked
+    plan: chunk c+1 waits for every lane of chunk c)."""
+    from yolox_amd import _native as N
+    from yolox_amd.engine import Plan
+    from yolox_amd.weights import synthetic_images
+    m = model("yolox_s", torch.bfloat16)
+    x = torch.from_numpy(synthetic_images(4, 160, 160, seed=4)).cuda()
+    outs = []
+    for lanes in (True, False):
+        p = Plan(m, 4, 160, 160, torch.bfloat16, "cuda", N.NHWC, torch.uint8, chunk=2)
+        assert p.nlanes == 4
+        p.use_lanes = lanes
+        p.static_input().copy_(x)
+        outs.append(p.replay().clone())
+        outs.append(p.replay().clone())
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, outs[2]) for o in outs)

@@ -437,3 +437,104 @@ def test_tile_variant_rejected_when_inapplicable():
     with pytest.raises(ValueError, match="tile"):
         run_conv([(nhwc(x, torch.bfloat16), 0, 16, 0)], conv, bn, torch.bfloat16, tile=2 * 12)
     assert n is not None
+
+
+def _stem_run(src, idt, dtype, H, W, cout, conv, bn, force_tiles=False):
+    n = N()
+    f = lambda t: t.detach().float().contiguous().to(DEV)  # noqa: E731
+    args = [f(conv.weight), f(bn.weight), f(bn.bias), f(bn.running_mean), f(bn.running_var)]
+    cpad = (cout + 15) // 16 * 16
+    w = torch.empty(cpad * 6 * 32, dtype=dtype, device=DEV)
+    b = torch.empty(cpad, dtype=torch.float32, device=DEV)
+    n.check(n.lib().yxh_stem_pack(*[a.data_ptr() for a in args], float(bn.eps), cout, n.DTYPE_CODE[dtype],
+                                  w.data_ptr(), b.data_ptr(), n.stream_ptr()), "stem pack")
+    cs = cout + 16
+    dst = torch.full((2, H // 2, W // 2, cs), 7.0, dtype=dtype, device=DEV)
+    d = n.StemDesc()
+    d.img, d.layout, d.img_dtype = src.data_ptr(), n.NHWC, n.DTYPE_CODE[idt]
+    d.batch, d.h, d.w, d.dtype, d.cout, d.act = 2, H, W, n.DTYPE_CODE[dtype], cout, n.ACT_CODE["silu"]
+    d.weight, d.bias, d.dst = w.data_ptr(), b.data_ptr(), dst.data_ptr()
+    d.dst_cstride, d.dst_bstride = cs, (H // 2) * (W // 2) * cs
+    d.reserved = 1 if force_tiles else 0
+    n.check(n.lib().yxh_stem_conv(ctypes.byref(d), n.stream_ptr()), "stem")
+    torch.cuda.synchronize()
+    return dst
+
+
+@pytest.mark.parametrize("idt", [torch.uint8, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("hw,cout", [((64, 640), 32), ((42, 96), 48), ((20, 16), 80), ((30, 48), 16)])
+def test_stem_full_row_strips_match_tiles(idt, dtype, hw, cout):
+    """NHWC images whose rows are whole 16-byte chunks take the full-row strip kernel;
+    it is bit-identical to the 4x64-tile kernel (forced by yxh_stem_desc.reserved = 1)
+    and matches the reference order (space-to-depth, conv, BN, SiLU in fp32)."""
+    H, W = hw
+    img = torch.randint(0, 256, (2, 3, H, W)).float()
+    src = img.permute(0, 2, 3, 1).to(DEV, idt).contiguous()
+    conv, bn = make_conv(12, cout, 3, 1, seed=cout + W)
+    strip = _stem_run(src, idt, dtype, H, W, cout, conv, bn)
+    tiles = _stem_run(src, idt, dtype, H, W, cout, conv, bn, force_tiles=True)
+    assert torch.equal(strip, tiles)
+    x = torch.cat([img[..., ::2, ::2], img[..., 1::2, ::2], img[..., ::2, 1::2], img[..., 1::2, 1::2]], 1)
+    want = ref_conv(x.to(dtype).float(), conv, bn, "silu")
+    got = strip.float().cpu().permute(0, 3, 1, 2)
+    assert (got[:, cout:] == 7.0).all()
+    err = (got[:, :cout] - want).abs().max().item() / want.abs().max().item()
+    assert err < TOL[dtype], err
+
+
+PWR_GEOMS = [  # cin, cout, H, W (cin <= 256: the whole K in registers)
+    (32, 16, 16, 16), (64, 64, 20, 20), (96, 192, 7, 9), (256, 5, 6, 6), (128, 80, 33, 17), (256, 256, 4, 4),
+    (16, 32, 9, 11), (64, 255, 5, 7)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("geom", PWR_GEOMS)
+def test_register_pointwise_conv(dtype, geom):
+    """conv_pwr (ids 81-82): 1x1 conv with the pixel operand loaded straight into MFMA
+    fragments, both channel tilings, into a compute-dtype and an fp32 destination, vs
+    the fp32 reference (ragged pixel / channel tails included)."""
+    cin, cout, H, W = geom
+    conv, bn = make_conv(cin, cout, 1, 1, seed=cin + 5 * cout)
+    x = torch.randn(3, cin, H, W, generator=torch.Generator().manual_seed(11))
+    want = ref_conv(x, conv, bn, "silu")
+    X = nhwc(x, dtype)
+    for tid in (81, 82):
+        y = run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid)
+        close(y.permute(0, 3, 1, 2), want, dtype)
+        out = torch.zeros(3, H, W, cout, dtype=torch.float32, device=DEV)
+        run_conv([(X, 0, cin, 0)], conv, bn, dtype, out=out, tile=2 * tid)
+        close(out.permute(0, 3, 1, 2), want, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_register_pointwise_two_sources_upsample(dtype):
+    """conv_pwr on the PAFPN pattern: cat([upsample(slice of a), b]) into an output slice."""
+    a_full = torch.randn(2, 192, 5, 6)
+    b = torch.randn(2, 64, 10, 12)
+    conv, bn = make_conv(128 + 64, 96, 1, 1, seed=9)
+    A, Bt = nhwc(a_full, dtype), nhwc(b, dtype)
+    ref = ref_conv(torch.cat([F.interpolate(a_full[:, 64:], scale_factor=2, mode="nearest"), b], 1), conv, bn,
+                   "silu")
+    for tid in (81, 82):
+        out = torch.zeros(2, 10, 12, 160, dtype=dtype, device=DEV)
+        run_conv([(A, 64, 128, 1), (Bt, 0, 64, 0)], conv, bn, dtype, out=out, out_coff=32, tile=2 * tid)
+        close(out[..., 32:128].permute(0, 3, 1, 2), ref, dtype)
+        assert out[..., :32].abs().max().item() == 0 and out[..., 128:].abs().max().item() == 0
+
+
+def test_register_pointwise_rejects():
+    x = nhwc(torch.randn(1, 32, 8, 8), torch.bfloat16)
+    conv3, bn3 = make_conv(32, 32, 3, 1, seed=1)
+    with pytest.raises(NotImplementedError, match="conv_pwr"):
+        run_conv([(x, 0, 32, 0)], conv3, bn3, torch.bfloat16, tile=2 * 81)
+    conv1, bn1 = make_conv(32, 32, 1, 1, seed=2)
+    with pytest.raises(NotImplementedError, match="conv_pwr"):
+        run_conv([(nhwc(torch.randn(1, 32, 8, 8), torch.float32), 0, 32, 0)], conv1, bn1, torch.float32,
+                 tile=2 * 81)
+    with pytest.raises(NotImplementedError, match="conv_pwr"):
+        run_conv([(x, 0, 32, 0)], conv1, bn1, torch.bfloat16, residual=(x.clone(), 0), tile=2 * 81)
+    big, bnb = make_conv(512, 32, 1, 1, seed=3)
+    with pytest.raises(NotImplementedError, match="conv_pwr"):
+        run_conv([(nhwc(torch.randn(1, 512, 4, 4), torch.bfloat16), 0, 512, 0)], big, bnb, torch.bfloat16,
+                 tile=2 * 81)
