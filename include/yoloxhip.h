@@ -261,7 +261,10 @@ typedef struct {
     yxh_src src[2];
     yxh_src dy;
     float* dw;
-    int32_t tile, reserved;  /* tile 0: default */
+    int32_t tile, reserved;  /* tile 0: by shape; 1-4: 64x64, 128x128, 32x64, 16x64 (cout x cin,
+                                register-transposed loader); 5-10 (bf16/f16): LDS-DMA +
+                                ds_read_b64_tr_b16, 128x128 (3 / 2 buffers), 64x64 (3 / 2),
+                                128x64, 64x128 */
 } yxh_wgrad_desc;
 int yxh_conv_wgrad(const yxh_wgrad_desc* d, void* stream);
 

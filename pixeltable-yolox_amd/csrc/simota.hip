@@ -3,12 +3,13 @@
 // get_geometry_constraint, simota_matching), losses.py:13-51 (IouLoss).
 //
 // The reference runs a Python loop over images and, inside it, over ground truths
-// with several host syncs per image.  Here the whole batch is four launches with no
+// with several host syncs per image.  Here the whole batch is six launches with no
 // host sync:
-//   sim_candidates : block per image.  Centre-radius geometry (strict > 0 against
-//                    +-1.5 strides), ordered compaction of the anchors inside any GT's
-//                    radius (the reference's anchor_filter order), and per candidate
+//   sim_flags      : thread per anchor.  Centre-radius geometry (strict > 0 against
+//                    +-1.5 strides) and, for anchors inside any GT's radius,
 //                    S1 = sum_c -max(log(1 - p_c), -100) with p = sqrt(sig(cls)*sig(obj)).
+//   sim_candidates : block per image: ordered compaction of the flagged anchors (the
+//                    reference's anchor_filter order) with their S1.
 //   sim_match      : block per (image, GT).  IoU + cost for every candidate
 //                    (cls cost = S1 - term(1-p_k) + term(p_k): torch's clamped BCE of the
 //                    one-hot target), dynamic_k = max(1, int(sum of the top-10 IoUs)),
@@ -35,6 +36,8 @@ struct SimWork {
     int* nmatch;      // [B][A] matches per candidate
     int* lastg;       // [B][A] a GT that matched it
     float* partial;   // [B][nblk][4]
+    float* s1a;       // [B][A] class-cost base sum per anchor (flagged anchors only)
+    uint8_t* flag;    // [B][A] anchor inside some GT's centre radius
 };
 
 struct SimGeom {
@@ -87,24 +90,46 @@ __device__ __forceinline__ float iou_cxcywh(const float* a, const float* b) {
     return area_i / ((area_a + area_b) - area_i);
 }
 
-__global__ __launch_bounds__(1024) void sim_candidates(const float* preds, const float* labels, int A, int C,
-                                                       int L, SimGeom geo, SimWork w) {
+// One thread per anchor: the 80 class-logit reads of different anchors are independent,
+// so thousands are in flight instead of one image's block walking them chunk by chunk.
+__global__ __launch_bounds__(256) void sim_flags(const float* preds, const float* labels, int A, int C, int L,
+                                                 SimGeom geo, SimWork w) {
+    const int b = blockIdx.y, a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= A) return;
+    const float* lab = labels + (long long)b * L * 5;
+    const int G = num_labels(lab, L);
+    bool in = false;
+    if (G > 0) {
+        float xs, ys, st;
+        anchor_geom(geo, a, xs, ys, st);
+        for (int g = 0; g < G && !in; ++g) in = in_center(lab + 5 * g + 1, xs, ys, st);
+    }
+    w.flag[(long long)b * A + a] = in ? 1 : 0;
+    if (!in) return;
+    const float* p = preds + ((long long)b * A + a) * (5 + C);
+    const float so = sig(p[4]);
+    float s1 = 0.0f;
+    int c = 0;
+    for (; c + 8 <= C; c += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[5 + c + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s1 += -clamped_log(1.0f - sqrtf(sig(v[u]) * so));
+    }
+    for (; c < C; ++c) s1 += -clamped_log(1.0f - sqrtf(sig(p[5 + c]) * so));
+    w.s1a[(long long)b * A + a] = s1;
+}
+
+__global__ __launch_bounds__(1024) void sim_candidates(int A, SimWork w) {
     __shared__ int wsum[16];
     __shared__ int base;
     const int b = blockIdx.x, tid = threadIdx.x;
-    const float* lab = labels + (long long)b * L * 5;
-    const int G = num_labels(lab, L);
     if (tid == 0) base = 0;
     __syncthreads();
-    const int D = 5 + C;
     for (int a0 = 0; a0 < A; a0 += 1024) {
         const int a = a0 + tid;
-        bool in = false;
-        if (a < A && G > 0) {
-            float xs, ys, st;
-            anchor_geom(geo, a, xs, ys, st);
-            for (int g = 0; g < G && !in; ++g) in = in_center(lab + 5 * g + 1, xs, ys, st);
-        }
+        const bool in = a < A && w.flag[(long long)b * A + a];
         // ordered compaction: wave ballot + per-wave prefix
         const unsigned long long m = __ballot(in);
         const int lane = tid & 63, wv = tid >> 6;
@@ -115,14 +140,7 @@ __global__ __launch_bounds__(1024) void sim_candidates(const float* preds, const
         const int pos = off + __popcll(m & ((1ull << lane) - 1ull));
         if (in) {
             w.cand[(long long)b * A + pos] = a;
-            const float* p = preds + ((long long)b * A + a) * D;
-            const float so = sig(p[4]);
-            float s1 = 0.0f;
-            for (int c = 0; c < C; ++c) {
-                const float pc = sqrtf(sig(p[5 + c]) * so);
-                s1 += -clamped_log(1.0f - pc);
-            }
-            w.s1[(long long)b * A + pos] = s1;
+            w.s1[(long long)b * A + pos] = w.s1a[(long long)b * A + a];
         }
         __syncthreads();
         if (tid == 0) {
@@ -449,7 +467,7 @@ size_t sim_workspace(int B, int A, int L) {
     const int nblk = (A + 255) / 256;
     return al(sizeof(int) * B) + al(sizeof(int) * (size_t)B * A) + al(sizeof(float) * (size_t)B * A) +
            2 * al(sizeof(float) * (size_t)B * L * A) + 2 * al(sizeof(int) * (size_t)B * A) +
-           al(sizeof(float) * 4 * (size_t)B * nblk);
+           al(sizeof(float) * 4 * (size_t)B * nblk) + al(sizeof(float) * (size_t)B * A) + al((size_t)B * A);
 }
 
 int yolox_loss(const float* preds, const float* origin, const float* labels, int B, int A, int C, int L,
@@ -476,6 +494,8 @@ int yolox_loss(const float* preds, const float* origin, const float* labels, int
     w.nmatch = (int*)take(sizeof(int) * (size_t)B * A);
     w.lastg = (int*)take(sizeof(int) * (size_t)B * A);
     w.partial = (float*)take(sizeof(float) * 4 * (size_t)B * nblk);
+    w.s1a = (float*)take(sizeof(float) * (size_t)B * A);
+    w.flag = (uint8_t*)take((size_t)B * A);
     int rc = 0;
     rc |= check_hip(hipMemsetAsync(w.nmatch, 0, sizeof(int) * (size_t)B * A, st), "memset");
     rc |= check_hip(hipMemsetAsync(fg, 0, (size_t)B * A, st), "memset");
@@ -483,7 +503,9 @@ int yolox_loss(const float* preds, const float* origin, const float* labels, int
     rc |= check_hip(hipMemsetAsync(piou, 0, sizeof(float) * (size_t)B * A, st), "memset");
     rc |= check_hip(hipMemsetAsync(num_fg, 0, sizeof(int) * B, st), "memset");
     if (rc) return YXH_EHIP;
-    hipLaunchKernelGGL(sim_candidates, dim3(B), dim3(1024), 0, st, preds, labels, A, C, L, geo, w);
+    hipLaunchKernelGGL(sim_flags, dim3((A + 255) / 256, B), dim3(256), 0, st, preds, labels, A, C, L, geo, w);
+    YXH_CHECK_LAUNCH("sim_flags");
+    hipLaunchKernelGGL(sim_candidates, dim3(B), dim3(1024), 0, st, A, w);
     YXH_CHECK_LAUNCH("sim_candidates");
     hipLaunchKernelGGL(sim_match, dim3(L, B), dim3(kSimThreads), 0, st, preds, labels, A, C, L, geo, w);
     YXH_CHECK_LAUNCH("sim_match");

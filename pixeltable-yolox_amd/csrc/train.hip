@@ -32,6 +32,7 @@ struct TView {
 };
 
 __device__ __forceinline__ long long vofs(const TView& v, int m) {
+    if (v.bs == (long long)v.HW * v.cs) return (long long)m * v.cs;  // images back to back: no (b, pix) split
     const int b = m / v.HW, pix = m - b * v.HW;
     return (long long)b * v.bs + (long long)pix * v.cs;
 }
@@ -80,7 +81,7 @@ template <bool PRECISE>
 __device__ __forceinline__ float act_grad(float z, int act) {
     switch (act) {
         case YXH_ACT_SILU: {
-            const float s = 1.0f / (1.0f + (PRECISE ? expf(-z) : __expf(-z)));
+            const float s = PRECISE ? 1.0f / (1.0f + expf(-z)) : __builtin_amdgcn_rcpf(1.0f + __expf(-z));
             return s * (1.0f + z * (1.0f - s));
         }
         case YXH_ACT_RELU: return z > 0.0f ? 1.0f : 0.0f;
@@ -131,31 +132,47 @@ __global__ __launch_bounds__(256) void chan_reduce(RedArgs a) {
         }
     }
     const int r0 = blockIdx.x * a.rpb, r1 = min(a.M, r0 + a.rpb);
-    if (rl < rpi) {
-        for (int r = r0 + rl; r < r1; r += rpi) {
-            float v[EPC];
-            load_f<T, EPC>(xp + vofs(a.x, r) + c0, v);
-            if (MODE == RED_STATS) {
+    auto accum = [&](const float (&v)[EPC], const float (&gv)[EPC]) {
+        if (MODE == RED_STATS) {
 #pragma unroll
-                for (int e = 0; e < EPC; ++e) {
-                    const float d = v[e] - sh[e];
-                    s1[e] += d;
-                    s2[e] += d * d;
-                }
-            } else if (MODE == RED_SUM) {
-#pragma unroll
-                for (int e = 0; e < EPC; ++e) s1[e] += v[e];
-            } else {
-                float gv[EPC];
-                load_f<float, EPC>((const float*)a.g.ptr + vofs(a.g, r) + c0, gv);
-#pragma unroll
-                for (int e = 0; e < EPC; ++e) {
-                    const float z = v[e] * sc[e] + sf[e];
-                    const float dz = gv[e] * act_grad<sizeof(T) == 4>(z, a.act);
-                    s1[e] += dz;
-                    s2[e] += dz * ((v[e] - mu[e]) * is[e]);
-                }
+            for (int e = 0; e < EPC; ++e) {
+                const float d = v[e] - sh[e];
+                s1[e] += d;
+                s2[e] += d * d;
             }
+        } else if (MODE == RED_SUM) {
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) s1[e] += v[e];
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+                const float z = v[e] * sc[e] + sf[e];
+                const float dz = gv[e] * act_grad<sizeof(T) == 4>(z, a.act);
+                s1[e] += dz;
+                s2[e] += dz * ((v[e] - mu[e]) * is[e]);
+            }
+        }
+    };
+    // U rows in flight per thread: all loads first, then the rows in order (the same
+    // fixed summation order as one row at a time)
+    constexpr int U = 4;
+    if (rl < rpi) {
+        int r = r0 + rl;
+        for (; r + (U - 1) * rpi < r1; r += U * rpi) {
+            float v[U][EPC], gv[U][EPC] = {};
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                load_f<T, EPC>(xp + vofs(a.x, r + u * rpi) + c0, v[u]);
+                if (MODE == RED_BWD) load_f<float, EPC>((const float*)a.g.ptr + vofs(a.g, r + u * rpi) + c0, gv[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) accum(v[u], gv[u]);
+        }
+        for (; r < r1; r += rpi) {
+            float v[EPC], gv[EPC] = {};
+            load_f<T, EPC>(xp + vofs(a.x, r) + c0, v);
+            if (MODE == RED_BWD) load_f<float, EPC>((const float*)a.g.ptr + vofs(a.g, r) + c0, gv);
+            accum(v, gv);
         }
     }
 #pragma unroll
@@ -185,6 +202,8 @@ struct FinArgs {
     float eps, momentum;
     float* stats;        // STATS out [4][C] = mean, invstd, scale, shift
     float *out0, *out1;  // BWD: dgamma, dbeta; SUM: out0
+    const float* st_in;  // BWD: the forward's stats [4][C]
+    float* coef;         // BWD out [3][C]: dx = k1*dz + k2*(y - mean) + k3
 };
 
 // 8 channels per block, 32 lanes per channel sum the per-block partials (strided, in
@@ -233,6 +252,11 @@ __global__ __launch_bounds__(256) void chan_finalize(FinArgs f) {
     } else if (f.mode == RED_BWD) {
         f.out0[c] = (float)t2;  // dgamma = sum dz * xhat
         f.out1[c] = (float)t1;  // dbeta = sum dz
+        const float is = f.st_in[f.C + c], inv_m = 1.0f / (float)f.M;
+        const float k1 = (f.gamma ? f.gamma[c] : 1.0f) * is;
+        f.coef[c] = k1;
+        f.coef[f.C + c] = -k1 * is * ((float)t2 * inv_m);
+        f.coef[2 * f.C + c] = -k1 * ((float)t1 * inv_m);
     } else {
         f.out0[c] = (float)t1;
     }
@@ -246,10 +270,12 @@ __global__ __launch_bounds__(256) void bn_act_fwd(TView y, const float* st, int 
     const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
     if (idx >= (long long)M * nch) return;
     const int m = (int)(idx / nch), c0 = (int)(idx - (long long)m * nch) * EPC;
-    float v[EPC];
+    float v[EPC], sc[EPC], sf[EPC];
     load_f<T, EPC>((const T*)y.ptr + vofs(y, m) + c0, v);
+    load_f<float, EPC>(st + 2 * C + c0, sc);
+    load_f<float, EPC>(st + 3 * C + c0, sf);
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) v[e] = apply_act<sizeof(T) == 4>(v[e] * st[2 * C + c0 + e] + st[3 * C + c0 + e], act);
+    for (int e = 0; e < EPC; ++e) v[e] = apply_act<sizeof(T) == 4>(v[e] * sc[e] + sf[e], act);
     if (res.ptr) {
         float r[EPC];
         load_f<T, EPC>((const T*)res.ptr + vofs(res, m) + c0, r);
@@ -259,28 +285,30 @@ __global__ __launch_bounds__(256) void bn_act_fwd(TView y, const float* st, int 
     store_f<T, EPC>((T*)out.ptr + vofs(out, m) + c0, v);
 }
 
+// dx = k1*dz + k2*(y - mean) + k3 with the per-channel coefficients chan_finalize derived
+// from dgamma / dbeta (BatchNorm's backward with batch statistics).
 template <typename T>
-__global__ __launch_bounds__(256) void bn_act_bwd_apply(TView y, TView g, const float* st, const float* gamma,
-                                                       const float* dgamma, const float* dbeta, int act, int M,
-                                                       T* dx) {
+__global__ __launch_bounds__(256) void bn_act_bwd_apply(TView y, TView g, const float* st, const float* coef,
+                                                       int act, int M, T* dx) {
     constexpr int EPC = Chunk<T>::N;
     const int C = y.C, nch = C / EPC;
     const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
     if (idx >= (long long)M * nch) return;
     const int m = (int)(idx / nch), c0 = (int)(idx - (long long)m * nch) * EPC;
-    float v[EPC], gv[EPC], o[EPC];
+    float v[EPC], gv[EPC], o[EPC], mu[EPC], sc[EPC], sf[EPC], k1[EPC], k2[EPC], k3[EPC];
     load_f<T, EPC>((const T*)y.ptr + vofs(y, m) + c0, v);
     load_f<float, EPC>((const float*)g.ptr + vofs(g, m) + c0, gv);
-    const float inv_m = 1.0f / (float)M;
+    load_f<float, EPC>(st + c0, mu);
+    load_f<float, EPC>(st + 2 * C + c0, sc);
+    load_f<float, EPC>(st + 3 * C + c0, sf);
+    load_f<float, EPC>(coef + c0, k1);
+    load_f<float, EPC>(coef + C + c0, k2);
+    load_f<float, EPC>(coef + 2 * C + c0, k3);
 #pragma unroll
     for (int e = 0; e < EPC; ++e) {
-        const int c = c0 + e;
-        const float mu = st[c], is = st[C + c];
-        const float z = v[e] * st[2 * C + c] + st[3 * C + c];
+        const float z = v[e] * sc[e] + sf[e];
         const float dz = gv[e] * act_grad<sizeof(T) == 4>(z, act);
-        const float xh = (v[e] - mu) * is;
-        const float gm = gamma ? gamma[c] : 1.0f;
-        o[e] = (gm * is) * ((dz - dbeta[c] * inv_m) - xh * (dgamma[c] * inv_m));
+        o[e] = k1[e] * dz + k2[e] * (v[e] - mu[e]) + k3[e];
     }
     store_f<T, EPC>(dx + (long long)m * C + c0, o);
 }
@@ -299,6 +327,7 @@ struct WgradParams {
     int cin_store;
     int sps, nst;  // stages per split, total pixel stages
     int ntc;       // channel tiles per tap
+    int dych;      // channels of the dy view (loads past them read the zero chunk)
 };
 
 __device__ __attribute__((aligned(16))) uint4 g_wg_zero[4];
@@ -485,6 +514,224 @@ __global__ __launch_bounds__(256) void conv_wgrad(WgradParams p) {
         }
 }
 
+// ------------------------------------------------------------------ weight gradient, LDS-DMA + transposed reads
+// bf16/f16 variant (tile ids 5-10, TN and TM in {64, 128}): both operands land in LDS in
+// their natural pixel-major layout by LDS-DMA (global_load_lds_dwordx4: one 16-byte
+// channel chunk per lane, the zero chunk for padding taps and the pixel tail), and the
+// MFMA fragments come out pixel(K)-major through gfx950's ds_read_b64_tr_b16 -- no
+// register staging and no in-register transpose, so the K loop is DMA issue + LDS reads
+// + MFMA over an NBUF-deep ring with counted vmcnt waits and raw barriers.  K = linear
+// output pixels, 64 per stage; each lane's DMA rows advance incrementally (no division
+// in the loop).  Row images are [pixel][chunk ^ f(pixel)]: the transposed reads of a
+// 32-lane half (4 consecutive rows, two blocks 8 rows apart) cover all 64 banks once.
+typedef short wg_i16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint2 lds_read_tr16(const char* ptr) {
+    const auto q = (__attribute__((address_space(3))) wg_i16x4*)(const_cast<char*>(ptr));
+    return __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(q));
+}
+
+template <int NCH>
+__device__ __forceinline__ int wg2_swz(int row) {
+    if constexpr (NCH == 16) return ((row & 3) << 2) | ((row >> 2) & 3);
+    else return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2);
+}
+
+__device__ __forceinline__ void wg2_glds16(const void* g, void* l) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wg2_wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void wg2_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+struct Wg2Pix {
+    int b, oy, ox;
+};
+
+template <typename T, int TN, int TM, int NBUF>
+__global__ __launch_bounds__(256) void conv_wgrad2(WgradParams p) {
+    constexpr int KP = 64;                     // output pixels per stage (two 32-deep K slabs)
+    constexpr int NCA = TN / 8, NCB = TM / 8;  // 16-byte chunks per pixel row
+    constexpr int RBA = NCA * 16, RBB = NCB * 16;
+    constexpr int A_BYTES = KP * RBA, B_BYTES = KP * RBB, BUF = A_BYTES + B_BYTES;
+    constexpr int PWA = A_BYTES / 4096, PWB = B_BYTES / 4096;  // 1 KiB DMA pieces per wave per stage
+    constexpr int PW = PWA + PWB;
+    constexpr int WTN = TN / 2, WTM = TM / 2, FR = WTN / 16, FC = WTM / 16;
+    static_assert(PWA >= 1 && PWB >= 1 && sizeof(T) == 2 && (NBUF == 2 || NBUF == 3), "tile");
+    __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 1, wc = wave & 1;
+    const int n0 = blockIdx.y * TN;
+    const int tap = blockIdx.z / p.ntc, c0 = (blockIdx.z - tap * p.ntc) * TM;
+    const int ky = tap / p.kw, kx = tap - ky * p.kw;
+    const int st0 = blockIdx.x * p.sps;
+    const int nst = min(p.nst, st0 + p.sps) - st0;
+    if (nst <= 0) return;
+
+    // this lane's DMA slots: piece k of an image holds bytes [1024k, 1024k + 1024)
+    int rowA[PWA], chA[PWA], rowB[PWB], chB[PWB];
+#pragma unroll
+    for (int a = 0; a < PWA; ++a) {
+        const int byte = (wave * PWA + a) * 1024 + lane * 16;
+        rowA[a] = byte / RBA;
+        chA[a] = ((byte % RBA) >> 4) ^ wg2_swz<NCA>(rowA[a]);
+    }
+#pragma unroll
+    for (int q = 0; q < PWB; ++q) {
+        const int byte = (wave * PWB + q) * 1024 + lane * 16;
+        rowB[q] = byte / RBB;
+        chB[q] = ((byte % RBB) >> 4) ^ wg2_swz<NCB>(rowB[q]);
+    }
+    Wg2Pix sa[PWA], sb[PWB];
+    auto init = [&](Wg2Pix& s, int row) {
+        const long long m = (long long)st0 * KP + row;
+        s.b = (int)(m / p.ohw);
+        const int pix = (int)(m - (long long)s.b * p.ohw);
+        s.oy = pix / p.out_w;
+        s.ox = pix - s.oy * p.out_w;
+    };
+    auto adv = [&](Wg2Pix& s) {
+        s.ox += KP;
+        while (s.ox >= p.out_w) {
+            s.ox -= p.out_w;
+            if (++s.oy == p.out_h) {
+                s.oy = 0;
+                ++s.b;
+            }
+        }
+    };
+#pragma unroll
+    for (int a = 0; a < PWA; ++a) init(sa[a], rowA[a]);
+#pragma unroll
+    for (int q = 0; q < PWB; ++q) init(sb[q], rowB[q]);
+
+    const T* dyp = (const T*)p.dy;
+    const void* zero = (const void*)g_wg_zero;
+    auto issue = [&](int buf) {
+        char* A = smem + buf * BUF;
+        char* Bm = A + A_BYTES;
+#pragma unroll
+        for (int a = 0; a < PWA; ++a) {
+            const int n = n0 + chA[a] * 8;
+            const void* g = zero;
+            if (sa[a].b < p.B && n < p.dych)
+                g = dyp + (long long)sa[a].b * p.dybs + (long long)(sa[a].oy * p.out_w + sa[a].ox) * p.dycs + n;
+            wg2_glds16(g, A + (wave * PWA + a) * 1024);
+        }
+#pragma unroll
+        for (int q = 0; q < PWB; ++q) {
+            int c = c0 + chB[q] * 8;
+            const int iy = sb[q].oy * p.stride - p.pad + ky, ix = sb[q].ox * p.stride - p.pad + kx;
+            const void* g = zero;
+            if (sb[q].b < p.B && c < p.cin && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w) {
+                int si = 0;
+                if (p.nsrc == 2 && c >= p.src0_ch) {
+                    si = 1;
+                    c -= p.src0_ch;
+                }
+                const int up = p.sup[si];
+                g = (const T*)p.sptr[si] + (long long)sb[q].b * p.sbs[si] +
+                    ((long long)(iy >> up) * p.sw[si] + (ix >> up)) * p.scs[si] + c;
+            }
+            wg2_glds16(g, Bm + (wave * PWB + q) * 1024);
+        }
+#pragma unroll
+        for (int a = 0; a < PWA; ++a) adv(sa[a]);
+#pragma unroll
+        for (int q = 0; q < PWB; ++q) adv(sb[q]);
+    };
+
+    // transposed-read addresses (image-relative, K slab 0): lane 4q+p of a 16-lane group
+    // supplies row q of the 4-row block, columns 4p..4p+3; it receives its own column
+    const int g4 = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    int offA[2][FR], offB[2][FC];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int row = 8 * g4 + 4 * h + q4;
+#pragma unroll
+        for (int i = 0; i < FR; ++i) {
+            const int ch = ((wr * WTN + i * 16) >> 3) + (p4 >> 1);
+            offA[h][i] = row * RBA + 16 * (ch ^ wg2_swz<NCA>(row)) + 8 * (p4 & 1);
+        }
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+            const int ch = ((wc * WTM + j * 16) >> 3) + (p4 >> 1);
+            offB[h][j] = row * RBB + 16 * (ch ^ wg2_swz<NCB>(row)) + 8 * (p4 & 1);
+        }
+    }
+
+    f32x4 acc[FR][FC];
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](int buf) {
+        const char* A = smem + buf * BUF;
+        const char* Bm = A + A_BYTES;
+#pragma unroll
+        for (int s = 0; s < KP / 32; ++s) {
+            uint4 af[FR], bf[FC];
+#pragma unroll
+            for (int i = 0; i < FR; ++i) {
+                const uint2 lo = lds_read_tr16(A + s * 32 * RBA + offA[0][i]);
+                const uint2 hi = lds_read_tr16(A + s * 32 * RBA + offA[1][i]);
+                af[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            }
+#pragma unroll
+            for (int j = 0; j < FC; ++j) {
+                const uint2 lo = lds_read_tr16(Bm + s * 32 * RBB + offB[0][j]);
+                const uint2 hi = lds_read_tr16(Bm + s * 32 * RBB + offB[1][j]);
+                bf[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            }
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], af[i], bf[j]);
+        }
+    };
+
+    constexpr int D = NBUF - 1;  // stages in flight ahead of the one being computed
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        if (d < nst) issue(d);
+    for (int k = 0; k < nst; ++k) {
+        if constexpr (D == 2) {
+            if (k + 1 < nst) wg2_wait_vm<PW>();  // stage k landed; stage k+1 may still fly
+            else wg2_wait_vm<0>();
+        } else {
+            wg2_wait_vm<0>();
+        }
+        wg2_barrier();  // every wave's pieces landed; compute(k-1) done -> its buffer is free
+        if (k + D < nst) issue((k + D) % NBUF);
+        compute(k % NBUF);
+    }
+    // dW (torch layout [cout][cin_store][kh][kw]) += acc
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+            const int c = c0 + wc * WTM + j * 16 + (lane & 15);
+            if (c >= p.cin_store) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n0 + wr * WTN + i * 16 + (lane >> 4) * 4 + r;
+                if (n < p.cout)
+                    atomicAdd(p.dw + (((long long)n * p.cin_store + c) * p.kh + ky) * p.kw + kx, acc[i][j][r]);
+            }
+        }
+}
+
 // dgrad weights: w [cout][cin][kh][kw] fp32 -> [c_count][kh][kw][cout_pad] of T, taps
 // flipped (ky -> kh-1-ky), input channels [c_begin, c_begin + c_count).
 template <typename T>
@@ -515,10 +762,11 @@ __global__ __launch_bounds__(256) void spp_bwd(TView cat, int H, int W, int c, c
                                                int B) {
     extern __shared__ __attribute__((aligned(16))) char sm[];
     const int HW = H * W, n = HW * kSppCpb;
-    float* pl = (float*)sm;                                   // plane
+    unsigned short* am = (unsigned short*)sm;                 // [3][n] argmax pixel per output
+    float* pl = (float*)(sm + 6 * (size_t)n);                 // plane
     float* hv = pl + n;                                       // row-window max
     unsigned short* hc = (unsigned short*)(hv + n);           // its column
-    unsigned short* am = hc + n;                              // [3][n] argmax pixel per output
+    float* dg = pl;  // [3][n] pooled-output gradients, once the argmax passes are done
     const int c0 = blockIdx.x * kSppCpb, b = blockIdx.y;
     const T* xb = (const T*)cat.ptr + (long long)b * cat.bs;
     const float* db = dcat + (long long)b * HW * 4 * c;
@@ -561,6 +809,12 @@ __global__ __launch_bounds__(256) void spp_bwd(TView cat, int H, int W, int c, c
         }
         __syncthreads();
     }
+    for (int q = threadIdx.x; q < 3 * n; q += 256) {  // the plane is dead: stage the gradients
+        const int k = q / n, r = q - k * n;
+        const int pix = r / kSppCpb, j = r - pix * kSppCpb;
+        dg[q] = c0 + j < c ? db[(long long)pix * 4 * c + (k + 1) * c + c0 + j] : 0.0f;
+    }
+    __syncthreads();
     for (int q = threadIdx.x; q < n; q += 256) {
         const int pix = q / kSppCpb, j = q - pix * kSppCpb;
         if (c0 + j >= c) continue;
@@ -569,9 +823,10 @@ __global__ __launch_bounds__(256) void spp_bwd(TView cat, int H, int W, int c, c
         for (int k = 0; k < 3; ++k) {
             const int r = 2 + 2 * k;
             for (int oy = max(0, y - r); oy <= min(H - 1, y + r); ++oy)
-                for (int ox = max(0, x - r); ox <= min(W - 1, x + r); ++ox)
-                    if (am[k * n + (oy * W + ox) * kSppCpb + j] == pix)
-                        g += db[((long long)oy * W + ox) * 4 * c + (k + 1) * c + c0 + j];
+                for (int ox = max(0, x - r); ox <= min(W - 1, x + r); ++ox) {
+                    const int o = k * n + (oy * W + ox) * kSppCpb + j;
+                    if (am[o] == pix) g += dg[o];
+                }
         }
         dx[((long long)b * HW + pix) * c + c0 + j] = g;
     }
@@ -628,7 +883,7 @@ constexpr int kRedMaxBlocks = 1024;
 int red_blocks(int M, int C, int dt, int* rpb) {
     const int nch = C / (16 / esz(dt));
     const int rpi = nch >= 256 ? 1 : 256 / nch;
-    int nblk = (int)(((long long)M + rpi * 16 - 1) / (rpi * 16));  // ~16 rows per thread
+    int nblk = (int)(((long long)M + rpi * 8 - 1) / (rpi * 8));  // ~8 rows per thread (4 in flight)
     nblk = nblk < 1 ? 1 : (nblk > kRedMaxBlocks ? kRedMaxBlocks : nblk);
     *rpb = (M + nblk - 1) / nblk;
     return (M + *rpb - 1) / *rpb;
@@ -645,7 +900,8 @@ int launch_reduce(int dt, const RedArgs& a, int nblk, hipStream_t st) {
 
 }  // namespace
 
-size_t reduce_workspace(int C) { return (size_t)(kRedMaxBlocks * 2 + 1) * C * sizeof(float); }
+// partials [nblk][2][C] + the stats shift row [C] + the backward coefficients [3][C]
+size_t reduce_workspace(int C) { return (size_t)(kRedMaxBlocks * 2 + 4) * C * sizeof(float); }
 
 namespace {
 
@@ -707,7 +963,7 @@ int bn_act_fwd_launch(int dt, int B, const yxh_src* y, const float* stats, int a
     YXH_CHECK_ARG(out->channels == C && out->h == y->h && out->w == y->w, "bn_act_fwd: out view shape");
     YXH_CHECK_ARG(!res || !res->ptr || (res->channels == C && res->h == y->h && res->w == y->w),
                   "bn_act_fwd: residual view shape");
-    YXH_CHECK_ARG(stats && B > 0, "bn_act_fwd: stats / batch");
+    YXH_CHECK_ARG(stats && a16(stats) && B > 0, "bn_act_fwd: stats (16-byte aligned) / batch");
     const long long M = (long long)B * y->h * y->w;
     const long long total = M * (C / (16 / esz(dt)));
     TView r = tview(res && res->ptr ? res : nullptr, C);
@@ -728,16 +984,21 @@ int bn_act_bwd_launch(int dt, int B, const yxh_src* y, const yxh_src* dout, cons
     const int C = y->channels;
     YXH_CHECK_ARG(dout->channels == C && dout->h == y->h && dout->w == y->w, "bn_act_bwd: dout view shape");
     YXH_CHECK_ARG(stats && dgamma && dbeta && dx && a16(dx), "bn_act_bwd: null / unaligned outputs");
+    YXH_CHECK_ARG(a16(stats), "bn_act_bwd: stats not 16-byte aligned");
     FinArgs f{};
     f.out0 = dgamma;
     f.out1 = dbeta;
+    f.gamma = gamma;
+    f.st_in = stats;
+    float* coef = (float*)ws + (size_t)(kRedMaxBlocks * 2 + 1) * C;
+    f.coef = coef;
     if (int rc = run_reduce(RED_BWD, dt, B, y, dout, stats, act, ws, ws_bytes, f, st)) return rc;
     const long long M = (long long)B * y->h * y->w;
     const long long total = M * (C / (16 / esz(dt)));
     dim3 grid((unsigned)((total + 255) / 256));
 #define YXH_BNB(T)                                                                                                 \
-    hipLaunchKernelGGL(bn_act_bwd_apply<T>, grid, dim3(256), 0, st, tview(y, C), tview(dout, C), stats, gamma,   \
-                       dgamma, dbeta, act, (int)M, (T*)dx)
+    hipLaunchKernelGGL(bn_act_bwd_apply<T>, grid, dim3(256), 0, st, tview(y, C), tview(dout, C), stats, coef, act, \
+                       (int)M, (T*)dx)
     if (dt == YXH_BF16) YXH_BNB(bf16);
     else if (dt == YXH_F16) YXH_BNB(f16);
     else YXH_BNB(float);
@@ -780,6 +1041,34 @@ int launch_wgrad_t(WgradParams p, hipStream_t st) {
     return YXH_OK;
 }
 
+template <typename T, int TN, int TM, int NBUF>
+int launch_wgrad2_t(WgradParams p, hipStream_t st) {
+    if constexpr (sizeof(T) != 2) {
+        set_error("wgrad tiles 5-10 (LDS-DMA + transposed LDS reads) are built for bf16/f16 only");
+        return YXH_EUNSUPPORTED;
+    } else {
+        constexpr int KP = 64;
+        constexpr int LDS = NBUF * KP * (TN + TM) * 2;
+        const int ntn = (p.cout + TN - 1) / TN;
+        p.ntc = (p.cin + TM - 1) / TM;
+        const int ntap = p.kh * p.kw;
+        p.nst = (int)(((long long)p.M + KP - 1) / KP);
+        const long long tiles = (long long)ntn * ntap * p.ntc;
+        const int occ = (160 * 1024) / LDS;
+        long long splits = (256LL * (occ < 1 ? 1 : occ) + tiles - 1) / tiles;  // about one wave of blocks
+        const long long max_splits = (p.nst + 3) / 4;                           // >= 4 stages per split
+        if (splits > max_splits) splits = max_splits;
+        if (splits < 1) splits = 1;
+        p.sps = (int)((p.nst + splits - 1) / splits);
+        splits = (p.nst + p.sps - 1) / p.sps;
+        YXH_CHECK_ARG(ntap * p.ntc < 65536 && ntn < 65536, "wgrad grid");
+        hipLaunchKernelGGL((conv_wgrad2<T, TN, TM, NBUF>), dim3((unsigned)splits, ntn, ntap * p.ntc), dim3(256), 0,
+                           st, p);
+        YXH_CHECK_LAUNCH("conv_wgrad2");
+        return YXH_OK;
+    }
+}
+
 template <typename T>
 int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
     // default: 64 x 64 (cout x cin), 2 x 2 waves; 4 slabs (bf16: 128 pixels) per stage
@@ -793,6 +1082,12 @@ int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
         case 2: return launch_wgrad_t<T, 128, 128, 2, 2, 2>(p, st);
         case 3: return launch_wgrad_t<T, 32, 64, 1, 4, 2>(p, st);
         case 4: return launch_wgrad_t<T, 16, 64, 1, 4, 2>(p, st);
+        case 5: return launch_wgrad2_t<T, 128, 128, 3>(p, st);
+        case 6: return launch_wgrad2_t<T, 128, 128, 2>(p, st);
+        case 7: return launch_wgrad2_t<T, 64, 64, 3>(p, st);
+        case 8: return launch_wgrad2_t<T, 64, 64, 2>(p, st);
+        case 9: return launch_wgrad2_t<T, 128, 64, 3>(p, st);
+        case 10: return launch_wgrad2_t<T, 64, 128, 3>(p, st);
         default: set_error("wgrad tile %d", tile); return YXH_EINVAL;
     }
 }
@@ -850,6 +1145,7 @@ int conv_wgrad_launch(const yxh_wgrad_desc* d, hipStream_t st) {
     p.dybs = g.bstride;
     p.dw = d->dw;
     p.cin_store = d->cin_store;
+    p.dych = g.channels;
     if (dt == YXH_BF16) return wgrad_tile<bf16>(d->tile, p, st);
     if (dt == YXH_F16) return wgrad_tile<f16>(d->tile, p, st);
     return wgrad_tile<float>(d->tile, p, st);
@@ -877,7 +1173,7 @@ int pack_dgrad_launch(const float* w, int cout, int cin, int kh, int kw, int c_b
 int spp_bwd_launch(int dt, int B, const yxh_src* cat, int c, const float* dcat, float* dx, hipStream_t st) {
     YXH_CHECK_ARG(cat && cat->ptr && dcat && dx && B > 0 && c > 0 && cat->cstride >= 4 * c, "spp_bwd arguments");
     const int HW = cat->h * cat->w;
-    const size_t lds = (size_t)HW * kSppCpb * (4 + 4 + 2 + 6);
+    const size_t lds = (size_t)HW * kSppCpb * (6 + 12);  // argmax u16 [3], then plane/row max/column or f32 [3]
     YXH_CHECK_ARG(lds <= 160 * 1024 && HW < 65536, "spp_bwd plane %dx%d too large for LDS", cat->h, cat->w);
     dim3 grid((c + kSppCpb - 1) / kSppCpb, B);
     TView v = tview(cat, c);

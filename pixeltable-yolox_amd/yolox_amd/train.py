@@ -26,6 +26,7 @@ the reverse pass completes them (``on_param_ready``).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -113,6 +114,21 @@ class GradBuffer:
                 p.grad.add_(g)
 
 
+# Tiles of the training convolutions, picked on the device the first time a shape runs
+# (HIP events around each candidate, outputs redirected to scratch) and cached for the
+# process.  Forward/data-gradient convs: the conv_igemm, conv_glds and conv_rows
+# families (tile codes as engine.TILE_CANDIDATES); weight gradients: yxh_wgrad_desc
+# tiles 1-10.  YOLOX_AMD_TRAIN_TUNE=0 keeps the by-shape defaults.
+CONV_TUNE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
+                   for k in (0, 1)]
+WGRAD_TUNE_TILES = list(range(1, 11))
+_TRAIN_TILES: dict = {}
+
+
+def _src_key(s: N.Src) -> tuple:
+    return (s.channels, s.cstride, s.h, s.w, s.upsample)
+
+
 class TrainGraph:
     """Executes one training forward (recording the tape) and its backward."""
 
@@ -134,6 +150,8 @@ class TrainGraph:
         self.on_backward_end: Optional[Callable[[], None]] = None  # e.g. GradReducer.finish
         self._fwd_w: dict = {}
         self.grad_total = torch.ones((), dtype=torch.float32, device=self.device)
+        self.tune = os.environ.get("YOLOX_AMD_TRAIN_TUNE", "1") != "0"
+        self._scratch = torch.empty(0, dtype=torch.uint8, device=self.device)
 
     # ------------------------------------------------------------ helpers
     @property
@@ -181,8 +199,11 @@ class TrainGraph:
         d.dst_dtype = N.F32 if dst_f32 else self.dcode
         d.dst_cstride, d.dst_bstride = dst_cs, dst_bs
         d.act = N.ACT_NONE
-        d.tile = 0
         d.flags = N.CONV_ACCUMULATE if accumulate else 0
+        key = ("conv", self.dcode, batch, in_h, in_w, out_h, out_w, cin, cout, k, stride, pad, int(dst_f32),
+               dst_cs, d.flags) + tuple(_src_key(q) for q in srcs)
+        d.tile = self._tile(key, d, self.lib.yxh_conv2d, "dst", batch * dst_bs * (4 if dst_f32 else self.esize),
+                            CONV_TUNE_TILES)
         self._chk(self.lib.yxh_conv2d(C.byref(d), self.stream), "conv")
 
     def _wgrad(self, srcs: list, cin: int, cin_store: int, cout: int, k: int, stride: int, pad: int, dy: N.Src,
@@ -196,8 +217,44 @@ class TrainGraph:
             d.src[j] = s
         d.dy = dy
         d.dw = dw.data_ptr()
-        d.tile = 0
+        key = ("wgrad", self.dcode, batch, in_h, in_w, out_h, out_w, cin, cin_store, cout, k, stride, pad,
+               _src_key(dy)) + tuple(_src_key(q) for q in srcs)
+        d.tile = self._tile(key, d, self.lib.yxh_conv_wgrad, "dw", cout * cin_store * k * k * 4, WGRAD_TUNE_TILES)
         self._chk(self.lib.yxh_conv_wgrad(C.byref(d), self.stream), "wgrad")
+
+    def _tile(self, key: tuple, d, fn, out_field: str, out_bytes: int, candidates: list, reps: int = 3) -> int:
+        """The cached tile for this shape, or the fastest candidate timed now (writing to
+        scratch instead of ``out_field``); 0 (by shape) when tuning is off."""
+        t = _TRAIN_TILES.get(key)
+        if t is not None:
+            return t
+        if not self.tune:
+            return 0
+        if self._scratch.numel() < out_bytes:
+            self._scratch = torch.empty(out_bytes, dtype=torch.uint8, device=self.device)
+        real = getattr(d, out_field)
+        setattr(d, out_field, self._scratch.data_ptr())
+        stream = torch.cuda.current_stream(self.device)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st, ref = self.stream, C.byref(d)
+        best = (float("inf"), 0)
+        try:
+            for tile in candidates:
+                d.tile = tile
+                if fn(ref, st) != N.OK:  # variant not applicable to this shape
+                    continue
+                ev0.record(stream)
+                for _ in range(reps):
+                    fn(ref, st)
+                ev1.record(stream)
+                ev1.synchronize()
+                ms = ev0.elapsed_time(ev1) / reps
+                if ms < best[0]:
+                    best = (ms, tile)
+        finally:
+            setattr(d, out_field, real)
+        _TRAIN_TILES[key] = best[1]
+        return best[1]
 
     def _dgrad(self, conv: nn.Conv2d, dy_t: torch.Tensor, cout_pad: int, inputs: list, batch: int) -> None:
         """Accumulate the data gradient of every input view that needs one.

@@ -119,7 +119,7 @@ def test_bn_act_bwd(dtype, B, H, W, Cc, act):
 
 
 # ----------------------------------------------------------------- conv gradients
-def wgrad(dtype, srcs, dy, cout, cin, k, s, p, in_hw, out_hw, B, cin_store=None):
+def wgrad(dtype, srcs, dy, cout, cin, k, s, p, in_hw, out_hw, B, cin_store=None, tile=0):
     from yolox_amd import _native as N
     d = N.WgradDesc()
     d.dtype, d.batch = DT[dtype], B
@@ -132,6 +132,7 @@ def wgrad(dtype, srcs, dy, cout, cin, k, s, p, in_hw, out_hw, B, cin_store=None)
     d.dy = dy
     dw = torch.zeros(cout, cin_store or cin, k, k, device="cuda")
     d.dw = dw.data_ptr()
+    d.tile = tile
     chk(lib().yxh_conv_wgrad(C.byref(d), stream()))
     return dw
 
@@ -191,6 +192,46 @@ def test_conv_wgrad_and_dgrad(dtype, cin0, cin1, up1, cout, k, s, H):
     tol = 1e-4 if dtype == torch.float32 else 2e-2
     assert rel(dw, wr.grad) < tol
     assert rel(dx0 - 0.5, xin.grad[:, :cin0].permute(0, 2, 3, 1)) < tol
+
+
+WG_TILE_CASES = [  # cin0, cin1, up1, cout, k, s, H, B
+    (32, 0, 0, 64, 3, 1, 16, 2), (64, 0, 0, 32, 3, 2, 20, 3), (64, 64, 1, 128, 1, 1, 8, 2),
+    (128, 0, 0, 128, 3, 1, 9, 2), (16, 0, 0, 24, 3, 1, 12, 1), (256, 0, 0, 192, 1, 1, 23, 2),
+    (96, 32, 0, 136, 3, 2, 17, 2),
+]
+
+
+@pytest.mark.parametrize("tile", [1, 2, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("cin0,cin1,up1,cout,k,s,H,B", WG_TILE_CASES)
+def test_conv_wgrad_tiles(tile, dtype, cin0, cin1, up1, cout, k, s, H, B):
+    """every weight-gradient tile (register-transposed 1-4, LDS-DMA + ds_read_b64_tr_b16
+    5-10) against torch autograd: ragged pixel counts (stage tails), cout / cin not
+    multiples of the tile, two sources with an upsampled second one, stride 2."""
+    g = torch.Generator().manual_seed(cin0 * 3 + cout + H + tile)
+    W = H + 4
+    p = (k - 1) // 2
+    x0 = torch.randn(B, H, W, cin0, generator=g).to(dtype)
+    x1 = torch.randn(B, H >> up1, W >> up1, cin1, generator=g).to(dtype) if cin1 else None
+    oh, ow = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dyc = (cout + 7) // 8 * 8
+    dy = torch.randn(B, oh, ow, dyc, generator=g).to(dtype)
+    x0d, dyd = x0.cuda(), dy.cuda()
+    srcs = [src(x0d)]
+    if cin1:
+        x1d = x1.cuda()
+        srcs.append(src(x1d, up=up1))
+    dw = wgrad(dtype, srcs, src(dyd), cout, cin0 + cin1, k, s, p, (H, W), (oh, ow), B, tile=tile)
+    torch.cuda.synchronize()
+    xin = x0.float().permute(0, 3, 1, 2)
+    if cin1:
+        x1n = x1.float().permute(0, 3, 1, 2)
+        if up1:
+            x1n = F.interpolate(x1n, scale_factor=2, mode="nearest")
+        xin = torch.cat([xin, x1n], 1)
+    wr = torch.zeros(cout, cin0 + cin1, k, k, requires_grad=True)
+    F.conv2d(xin, wr, stride=s, padding=p).backward(dy[..., :cout].float().permute(0, 3, 1, 2))
+    assert rel(dw, wr.grad) < 1e-4  # fp32 accumulation of exact products: order-only differences
 
 
 def test_wgrad_cin_store_and_strided_dy():
