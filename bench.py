@@ -262,7 +262,7 @@ def main_train(args, world, rank):
     achieved = flops / (gpu_ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if amp is not None else 157.3
     result = {
-        "metric": "images/sec (train step: fwd + SimOTA/loss + bwd + DP all-reduce + SGD + EMA) YOLOX-s 640x640",
+        "metric": f"images/sec (train step: fwd + SimOTA/loss + bwd + DP all-reduce + SGD + EMA) {args.model} {S}x{S}",
         "value": round(world * B * args.steps / dt_max, 2),
         "unit": "images/s",
         "n_gpus": world,

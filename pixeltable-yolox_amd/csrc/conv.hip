@@ -467,7 +467,10 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
 
     // K staging: two 64-byte slabs per stage when the channel structure allows it
     const int k2 = 8 * epc;
-    int ks = (d->cin >= k2 && (d->nsrc == 1 || p.src0_ch % k2 == 0)) ? 2 : 1;
+    // (every loader picks the source per 16-byte chunk, so a concat split only has to
+    // fall on a chunk boundary -- checked above -- not on a stage boundary: yolox_x's
+    // 80/160/320-channel CSP halves)
+    int ks = d->cin >= k2 ? 2 : 1;
     int tile = heuristic_tile(p);
     if (d->tile > 0) {
         tile = d->tile >> 1;
@@ -480,8 +483,6 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         ks = want_ks;
     }
     const int kstage = 4 * ks * epc;
-    YXH_CHECK_ARG(d->nsrc == 1 || p.src0_ch % kstage == 0, "src0 channels %d not a multiple of %d", p.src0_ch,
-                  kstage);
     p.ncb = (d->cin + kstage - 1) / kstage;
     if (dilated && tile > 16) {
         set_error("dilated (upsample == 2) sources run on the register-staged kernel only (tile ids 1-9)");

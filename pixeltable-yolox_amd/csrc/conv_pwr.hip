@@ -55,17 +55,6 @@ __global__ __launch_bounds__(256) void conv_pwr(ConvParams p, PwrArgs a) {
     const int n0 = blockIdx.y * TN;
     char* wst = smem + WB + wave * STG;
 
-    for (int s = tid; s < TN * NCH; s += 256) {
-        const int c = s / TN, rp = s - c * TN;
-        const int n = n0 + (rp ^ (2 * (c & 3) + (c >> 2)));
-        const int ch = c * EPC;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (n < p.cout && ch < p.cin) v = *(const uint4*)((const T*)p.w + (long long)n * p.cin + ch);
-        *(uint4*)(wl + s * 16) = v;
-    }
-    if (tid < TN) lbias[tid] = n0 + tid < p.cout ? p.bias[n0 + tid] : 0.0f;
-    __syncthreads();
-
     const int nwav = gridDim.x * 4;
     const int first = pwr_xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
     const T* sp0 = (const T*)p.sptr[0];
@@ -108,7 +97,19 @@ __global__ __launch_bounds__(256) void conv_pwr(ConvParams p, PwrArgs a) {
 
     const bool staged = p.vec16 && !p.dst_f32;
     uint4 bf[FC][KSL], nb[FC][KSL];
+    // first pixel tile in flight before the weight image is staged: the two global
+    // round trips overlap instead of chaining through the barrier
     load(first, bf);
+    for (int s = tid; s < TN * NCH; s += 256) {
+        const int c = s / TN, rp = s - c * TN;
+        const int n = n0 + (rp ^ (2 * (c & 3) + (c >> 2)));
+        const int ch = c * EPC;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (n < p.cout && ch < p.cin) v = *(const uint4*)((const T*)p.w + (long long)n * p.cin + ch);
+        *(uint4*)(wl + s * 16) = v;
+    }
+    if (tid < TN) lbias[tid] = n0 + tid < p.cout ? p.bias[n0 + tid] : 0.0f;
+    __syncthreads();
     for (int t = first; t < a.ntiles; t += nwav) {
         load(t + nwav, nb);
         f32x4 acc[FR][FC];

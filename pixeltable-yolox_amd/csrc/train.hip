@@ -107,13 +107,14 @@ template <typename T, int MODE>
 __global__ __launch_bounds__(256) void chan_reduce(RedArgs a) {
     constexpr int EPC = Chunk<T>::N;
     __shared__ float red[2][256 * EPC];
-    const int C = a.x.C, nch = C / EPC;
+    // blockIdx.y = channel group of up to 256 16-byte chunks (yolox_x fp32: 1280 channels)
+    const int C = a.x.C, cg = blockIdx.y * 256 * EPC, CL = min(C - cg, 256 * EPC), nch = CL / EPC;
     const int tid = threadIdx.x;
     const int q = tid % nch, rl = tid / nch, rpi = 256 / nch;
     float s1[EPC], s2[EPC], sh[EPC];
 #pragma unroll
     for (int e = 0; e < EPC; ++e) s1[e] = s2[e] = sh[e] = 0.0f;
-    const int c0 = q * EPC;
+    const int c0 = cg + q * EPC;
     const T* xp = (const T*)a.x.ptr;
     if (MODE == RED_STATS && rl < rpi) {
         load_f<T, EPC>(xp + c0, sh);  // shift = pixel 0 (cancellation guard)
@@ -182,15 +183,15 @@ __global__ __launch_bounds__(256) void chan_reduce(RedArgs a) {
     }
     __syncthreads();
     // thread t < C sums channel t over the row lanes (fixed order: deterministic)
-    for (int c = tid; c < C; c += 256) {
+    for (int c = tid; c < CL; c += 256) {
         const int qq = c / EPC, e = c - qq * EPC;
         float t1 = 0.0f, t2 = 0.0f;
         for (int l = 0; l < rpi; ++l) {
             t1 += red[0][(l * nch + qq) * EPC + e];
             t2 += red[1][(l * nch + qq) * EPC + e];
         }
-        a.partial[((long long)blockIdx.x * 2) * C + c] = t1;
-        a.partial[((long long)blockIdx.x * 2 + 1) * C + c] = t2;
+        a.partial[((long long)blockIdx.x * 2) * C + cg + c] = t1;
+        a.partial[((long long)blockIdx.x * 2 + 1) * C + cg + c] = t2;
     }
 }
 
@@ -275,7 +276,12 @@ __global__ __launch_bounds__(256) void bn_act_fwd(TView y, const float* st, int 
     load_f<float, EPC>(st + 2 * C + c0, sc);
     load_f<float, EPC>(st + 3 * C + c0, sf);
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) v[e] = apply_act<sizeof(T) == 4>(v[e] * sc[e] + sf[e], act);
+    for (int e = 0; e < EPC; ++e) {
+        const float z = v[e] * sc[e] + sf[e];
+        // training keeps the IEEE-divide SiLU on every dtype: the SimOTA assignment
+        // downstream is discrete, so the bf16/f16 step stays bit-stable across builds
+        v[e] = (act == YXH_ACT_SILU && sizeof(T) != 4) ? z / (1.0f + __expf(-z)) : apply_act<sizeof(T) == 4>(z, act);
+    }
     if (res.ptr) {
         float r[EPC];
         load_f<T, EPC>((const T*)res.ptr + vofs(res, m) + c0, r);
@@ -891,9 +897,11 @@ int red_blocks(int M, int C, int dt, int* rpb) {
 
 template <int MODE>
 int launch_reduce(int dt, const RedArgs& a, int nblk, hipStream_t st) {
-    if (dt == YXH_BF16) hipLaunchKernelGGL((chan_reduce<bf16, MODE>), dim3(nblk), dim3(256), 0, st, a);
-    else if (dt == YXH_F16) hipLaunchKernelGGL((chan_reduce<f16, MODE>), dim3(nblk), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((chan_reduce<float, MODE>), dim3(nblk), dim3(256), 0, st, a);
+    const int per = 256 * (16 / esz(dt));  // channels per group (256 chunks)
+    const dim3 grid(nblk, (a.x.C + per - 1) / per);
+    if (dt == YXH_BF16) hipLaunchKernelGGL((chan_reduce<bf16, MODE>), grid, dim3(256), 0, st, a);
+    else if (dt == YXH_F16) hipLaunchKernelGGL((chan_reduce<f16, MODE>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((chan_reduce<float, MODE>), grid, dim3(256), 0, st, a);
     YXH_CHECK_LAUNCH("chan_reduce");
     return YXH_OK;
 }
@@ -909,7 +917,7 @@ int run_reduce(int mode, int dt, int B, const yxh_src* x, const yxh_src* g, cons
                void* ws, size_t ws_bytes, FinArgs f, hipStream_t st) {
     const int C = x->channels;
     YXH_CHECK_ARG(B > 0, "batch %d", B);
-    YXH_CHECK_ARG(C / (16 / esz(dt)) <= 256, "reduction: %d channels exceed one block's chunks", C);
+    YXH_CHECK_ARG(C > 0 && C % (16 / esz(dt)) == 0, "reduction: %d channels not in 16-byte chunks", C);
     YXH_CHECK_ARG(ws && ws_bytes >= reduce_workspace(C), "reduction workspace too small");
     RedArgs a{};
     a.x = tview(x, C);

@@ -23,11 +23,14 @@ template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T
 // 16-byte chunk of T (8 bf16/f16, 4 f32): the unit of every global/LDS move.
 template <typename T> struct Chunk { static constexpr int N = 16 / sizeof(T); };
 
-// PRECISE: the fp32 parity path uses the correctly-rounded-ish expf; the bf16/f16
-// paths use the hardware exp2 (their outputs are rounded to 8/11 bits anyway).
+// PRECISE: the fp32 parity path uses the correctly-rounded-ish expf and an IEEE
+// divide; the bf16/f16 paths (outputs rounded to 8/11 bits) use the hardware exp and
+// one v_rcp_f32 (~1 ulp) -- the IEEE divide sequence alone was ~10 VALU ops per output
+// and the SiLU epilogue up to ~25% of a wide 1x1 conv's time (tools/pw_probe.py).
 template <bool PRECISE>
 __device__ __forceinline__ float silu(float v) {
-    return v / (1.0f + (PRECISE ? expf(-v) : __expf(-v)));
+    if (PRECISE) return v / (1.0f + expf(-v));
+    return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
 }
 
 template <bool PRECISE = false>

@@ -237,6 +237,7 @@ class OutBuffer:
 TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
                    + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82]
 _TUNE_CACHE: dict = {}
+_TUNE_ALL = os.environ.get("YOLOX_AMD_TUNE_ALL", "0") == "1"  # print every variant's time
 
 
 def save_tune_cache(path: str) -> None:
@@ -606,6 +607,8 @@ class Plan:
                 ev1.record(stream)
                 ev1.synchronize()
                 t = ev0.elapsed_time(ev1) / reps
+                if _TUNE_ALL:
+                    print(f"  op {i} tile {tile >> 1} slabs {(tile & 1) + 1}: {t * 1e3:.1f} us", file=sys.stderr)
                 if t < best[0]:
                     best = (t, tile)
             op.u.conv.tile = best[1]

@@ -57,7 +57,7 @@ def ws(C_=1024):
 
 # ----------------------------------------------------------------- BatchNorm + act
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B,H,W,Cc", [(2, 16, 16, 32), (3, 10, 7, 64), (1, 5, 5, 512)])
+@pytest.mark.parametrize("B,H,W,Cc", [(2, 16, 16, 32), (3, 10, 7, 64), (1, 5, 5, 512), (1, 4, 6, 1280), (2, 3, 3, 2560)])
 def test_bn_stats_and_act_fwd(dtype, B, H, W, Cc):
     g = torch.Generator().manual_seed(B * 100 + Cc)
     y = (torch.randn(B, H, W, Cc, generator=g) * 3 + 5).to(dtype)
@@ -66,7 +66,7 @@ def test_bn_stats_and_act_fwd(dtype, B, H, W, Cc):
     res = torch.randn(B, H, W, Cc, generator=g).to(dtype)
     yd, rmd, rvd = y.cuda(), rm.clone().cuda(), rv.clone().cuda()
     stats = torch.empty(4, Cc, device="cuda")
-    w = ws()
+    w = ws(max(Cc, 1024))
     ys = src(yd)
     gd, bd = gamma.cuda(), beta.cuda()  # held: the launch is asynchronous
     chk(lib().yxh_bn_stats(DT[dtype], B, C.byref(ys), gd.data_ptr(), bd.data_ptr(),
@@ -88,7 +88,8 @@ def test_bn_stats_and_act_fwd(dtype, B, H, W, Cc):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B,H,W,Cc,act", [(2, 16, 16, 32, 1), (3, 9, 11, 64, 1), (2, 6, 6, 128, 3)])
+@pytest.mark.parametrize("B,H,W,Cc,act", [(2, 16, 16, 32, 1), (3, 9, 11, 64, 1), (2, 6, 6, 128, 3),
+                                             (1, 4, 5, 1280, 1)])
 def test_bn_act_bwd(dtype, B, H, W, Cc, act):
     g = torch.Generator().manual_seed(7 + Cc)
     y = (torch.randn(B, H, W, Cc, generator=g) * 2 + 1).to(dtype)
@@ -96,7 +97,7 @@ def test_bn_act_bwd(dtype, B, H, W, Cc, act):
     dout = torch.randn(B, H, W, Cc, generator=g)
     yd = y.cuda()
     stats = torch.empty(4, Cc, device="cuda")
-    w = ws()
+    w = ws(max(Cc, 1024))
     ys = src(yd)
     gd, bd = gamma.cuda(), beta.cuda()  # held: the launches are asynchronous
     chk(lib().yxh_bn_stats(DT[dtype], B, C.byref(ys), gd.data_ptr(), bd.data_ptr(), None, None,
@@ -140,6 +141,8 @@ def wgrad(dtype, srcs, dy, cout, cin, k, s, p, in_hw, out_hw, B, cin_store=None,
 WG_CASES = [  # cin0, cin1, up1, cout, k, s, H
     (32, 0, 0, 64, 3, 1, 16), (64, 0, 0, 32, 3, 2, 20), (64, 0, 0, 64, 1, 1, 12), (32, 32, 0, 64, 1, 1, 10),
     (64, 64, 1, 32, 1, 1, 8), (128, 0, 0, 128, 3, 1, 9), (16, 0, 0, 24, 3, 1, 12),
+    # concat split on a 16-byte chunk but not on a K-stage boundary (yolox_m 48, yolox_x 80)
+    (48, 48, 0, 64, 1, 1, 10), (80, 80, 0, 96, 1, 1, 7),
 ]
 
 
@@ -198,6 +201,8 @@ WG_TILE_CASES = [  # cin0, cin1, up1, cout, k, s, H, B
     (32, 0, 0, 64, 3, 1, 16, 2), (64, 0, 0, 32, 3, 2, 20, 3), (64, 64, 1, 128, 1, 1, 8, 2),
     (128, 0, 0, 128, 3, 1, 9, 2), (16, 0, 0, 24, 3, 1, 12, 1), (256, 0, 0, 192, 1, 1, 23, 2),
     (96, 32, 0, 136, 3, 2, 17, 2),
+    # tiny head levels (rows narrower than one 8-pixel chunk): 128 px / 32 px / 8 px per batch
+    (128, 0, 0, 128, 3, 1, 8, 2), (128, 0, 0, 128, 3, 1, 4, 2), (128, 0, 0, 128, 1, 1, 2, 2),
 ]
 
 
@@ -394,6 +399,42 @@ def test_train_step_fp32_matches_oracle(oracle, use_l1):
         if name.endswith("running_mean"):
             assert not torch.equal(buf.cpu(), sd[name]), name
             break
+
+
+@pytest.mark.parametrize("name", ["yolox_m", "yolox_x"])
+def test_train_step_other_widths_match_oracle(oracle, name):
+    """yolox_m / yolox_x widths (48/80-channel CSP halves: concat splits that are not
+    K-stage aligned) train through the HIP path: fp32 losses and every parameter
+    gradient vs the oracle's autograd (1e-3), and an fp16 autocast step (the --fp16 of
+    BASELINE configs[4]) gives a finite loss close to the fp32 one."""
+    from yolox_amd.config import named_config
+    from yolox_amd.weights import synthetic_images, synthetic_labels, synthetic_state_dict
+    m = named_config(name).get_model()
+    sd = synthetic_state_dict(m.state_dict(), seed=3, bn_stats=name)
+    m.load_state_dict(sd)
+    x = torch.from_numpy(synthetic_images(2, 64, 64, seed=5)).permute(0, 3, 1, 2).float()
+    labels = torch.from_numpy(synthetic_labels(2, 64, 64, max_gt=6, seed=7))
+    m = m.cuda().train()
+    out = m(x.cuda(), labels.cuda())
+    out["total_loss"].backward()
+    torch.cuda.synchronize()
+    sdo = {k: v.clone().float().requires_grad_(v.is_floating_point() and "running" not in k
+                                               and "num_batches" not in k) for k, v in sd.items()}
+    ref = oracle.forward_train(sdo, oracle.ARCHS[name], x, labels, use_l1=False)
+    ref["total_loss"].backward()
+    for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss", "num_fg"):
+        assert float(out[k]) == pytest.approx(float(ref[k]), rel=1e-3, abs=1e-6), k
+    for pname, prm in m.named_parameters():
+        assert rel(prm.grad, sdo[pname].grad) < 1e-3, pname
+    m.load_state_dict(sd)
+    m.zero_grad(set_to_none=True)
+    with torch.autocast("cuda", dtype=torch.float16):
+        out16 = m(x.cuda().half(), labels.cuda())
+    out16["total_loss"].backward()
+    torch.cuda.synchronize()
+    l16 = float(out16["total_loss"])
+    assert np.isfinite(l16) and abs(l16 - float(out["total_loss"])) < 0.05 * float(out["total_loss"])
+    assert all(torch.isfinite(prm.grad).all() for prm in m.parameters())
 
 
 def test_train_step_bf16_autocast_close_to_fp32():
