@@ -65,14 +65,24 @@ def parse():
     return args
 
 
+# "nccl" (RCCL over xGMI, one rank per GPU) for real runs; "gloo" only to rehearse the
+# multi-rank code path with several ranks sharing one GPU (numbers then meaningless)
+_BACKEND = os.environ.get("YOLOX_AMD_BENCH_BACKEND", "nccl")
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if _BACKEND == "gloo":  # rehearsal of the N>1 path on a box with fewer GPUs than ranks
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -88,7 +98,7 @@ def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if _BACKEND == "gloo" else "cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

@@ -139,6 +139,8 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvParams p) {
         }
     };
 
+    float lbias[FR][4];
+    load_lane_bias<TN, WR, WC>(p, n0, lbias);
     const int nk = p.taps * p.ncb;
     gload(0);
     lstore(0);
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvParams p) {
         __syncthreads();
     }
 
-    conv_epilogue<T, TN, TM, WR, WC, 2 * BUF>(p, acc, smem, m0, n0);
+    conv_epilogue<T, TN, TM, WR, WC, 2 * BUF>(p, acc, smem, m0, n0, lbias);
 }
 
 // ---------------------------------------------------------------- depthwise

@@ -137,9 +137,24 @@ __device__ __forceinline__ void store4(const ConvParams& p, float v[4], int n, i
 // the output dtype goes through LDS, then whole pixel rows leave as 16-byte chunks
 // (coalesced) instead of 8-byte lane-scattered stores.  Caller guarantees all LDS
 // reads of the K loop are done.
+// The bias of this lane's output channels, loaded before the K loop so the epilogue
+// does not start with a dependent global round trip (caller: load_lane_bias at entry).
+template <int TN, int WR, int WC>
+__device__ __forceinline__ void load_lane_bias(const ConvParams& p, int n0, float (&bias)[TN / WR / 16][4]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, fq = lane >> 4;
+    const int wr = wave / WC;
+#pragma unroll
+    for (int i = 0; i < TN / WR / 16; ++i) {
+        const int n = n0 + wr * (TN / WR) + i * 16 + fq * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[i][r] = n + r < p.cout ? p.bias[n + r] : 0.0f;
+    }
+}
+
 template <typename T, int TN, int TM, int WR, int WC, int SMEM_BYTES, typename Map>
 __device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&acc)[TN / WR / 16][TM / WC / 16],
-                                                  char* smem, const Map& map, int n0) {
+                                                  char* smem, const Map& map, int n0,
+                                                  const float (&bias)[TN / WR / 16][4]) {
     constexpr int WTN = TN / WR, WTM = TM / WC;
     constexpr int FR = WTN / 16, FC = WTM / 16;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -162,7 +177,7 @@ __device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&a
                 const int n = n0 + nl;
                 float v[4];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + (n + r < p.cout ? p.bias[n + r] : 0.0f);
+                for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[i][r];
                 if (m >= 0 && n < p.cout) finish4<T>(p, v, n, b, pix, ox, oy);
                 T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
                 char* dstl = smem + pl * OROW + nl * OES;
@@ -202,7 +217,7 @@ __device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&a
             if (n >= p.cout) continue;
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + (n + r < p.cout ? p.bias[n + r] : 0.0f);
+            for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[i][r];
             store4<T>(p, v, n, b, pix, ox, oy);
         }
     }
@@ -211,10 +226,10 @@ __device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&a
 // Linear pixel tiles: tile-local pixel pl is output pixel m0 + pl.
 template <typename T, int TN, int TM, int WR, int WC, int SMEM_BYTES>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TN / WR / 16][TM / WC / 16],
-                                              char* smem, int m0, int n0) {
+                                              char* smem, int m0, int n0, const float (&bias)[TN / WR / 16][4]) {
     const int M = p.M;
     conv_epilogue_map<T, TN, TM, WR, WC, SMEM_BYTES>(
-        p, acc, smem, [m0, M](int pl) { return m0 + pl < M ? m0 + pl : -1; }, n0);
+        p, acc, smem, [m0, M](int pl) { return m0 + pl < M ? m0 + pl : -1; }, n0, bias);
 }
 
 // LDS-DMA variant (conv_glds.hip); id as in conv.hip's tile table

@@ -144,6 +144,8 @@ __global__ __launch_bounds__(256) void conv_glds(ConvParams p) {
         }
     };
 
+    float lbias[FR][4];
+    load_lane_bias<TN, WR, WC>(p, n0, lbias);
     const int nk = p.taps * p.ncb;
     issue(0, 0);
     if (nk > 1) issue(1, 1);
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(256) void conv_glds(ConvParams p) {
         compute(k % NBUF);
     }
     block_barrier();
-    conv_epilogue<T, TN, TM, WR, WC, NBUF * BUF>(p, acc, smem, m0, n0);
+    conv_epilogue<T, TN, TM, WR, WC, NBUF * BUF>(p, acc, smem, m0, n0, lbias);
 }
 
 template <typename T, int TN, int TM, int WR, int WC>

@@ -117,6 +117,8 @@ __global__ __launch_bounds__(256) void conv_rows(ConvParams p, int tiles_x, int 
     for (int i = 0; i < FR; ++i)
 #pragma unroll
         for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float lbias[FR][4];
+    load_lane_bias<TN, WN, WM>(p, n0, lbias);
 
     const int frow = lane & 15, fq = lane >> 4;
     int hp0[FC];  // B-image pixel of this lane's fragment column at kx = 0
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(256) void conv_rows(ConvParams p, int tiles_x, int 
             const int oy = oy0 + ty, ox = ox0 + tx;
             return (oy < OH && ox < OW) ? mb + oy * OW + ox : -1;
         },
-        n0);
+        n0, lbias);
 }
 
 template <typename T, int S, int TX, int TY, int CH, int TN, int NBUF>
