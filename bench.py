@@ -241,8 +241,11 @@ def main_train(args, world, rank):
         imgs = imgs.to(amp)  # trainer.py:100 (inps.to(data_type) under --fp16)
     labels = torch.from_numpy(synthetic_labels(B, S, S, seed=2000 + rank)).to(dev)
 
+    from yolox_amd.optim import FusedStep
+    fused = FusedStep(model, opt, ema) if scaler is None else None
+
     def step():
-        return train_one_iter(net, opt, imgs, labels, amp_dtype=amp, scaler=scaler, ema=ema)
+        return train_one_iter(net, opt, imgs, labels, amp_dtype=amp, scaler=scaler, ema=ema, fused=fused)
 
     for _ in range(args.warmup):
         out = step()

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 4
+#define YXH_ABI_VERSION 5
 
 enum yxh_status {
     YXH_OK = 0,
@@ -350,6 +350,41 @@ int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, c
                            const int32_t* deps, int32_t nlanes, void* stream, void** graph_exec);
 int yxh_graph_launch(void* graph_exec, void* stream);
 int yxh_graph_destroy(void* graph_exec);
+
+/* ---------------------------------------------------------------- optimizer step
+ * yxh_sgd_ema_step: one fused pass = torch.optim.SGD.step (momentum, nesterov, per-group
+ * weight decay, dampening 0) + ModelEMA.update, replacing the reference's
+ * `scaler.step(optimizer)` + `ema_model.update(model)` (core/trainer.py:124-127,
+ * config.py:307-333, utils/ema.py:46-58).  segs: device array of segments (one per
+ * parameter, plus EMA-only segments with param == NULL for floating buffers); chunks:
+ * device int32 pairs {segment, chunk index} covering every segment in chunks of
+ * yxh_opt_chunk_elems() elements.  All arrays fp32.  first_step: momentum buffers are
+ * initialised to the (decayed) gradient, as torch does when a parameter has no
+ * momentum_buffer yet. */
+typedef struct yxh_opt_seg {
+    float* param;       /* updated in place; NULL: EMA-only segment */
+    const float* grad;  /* param's gradient */
+    float* buf;         /* momentum buffer */
+    float* ema;         /* EMA copy (NULL: none) */
+    const float* src;   /* EMA source of an EMA-only segment */
+    int64_t n;          /* elements */
+    float weight_decay;
+    int32_t group;      /* index into yxh_opt_hparams.lr */
+} yxh_opt_seg;
+
+typedef struct yxh_opt_hparams {
+    float lr[4];        /* per parameter group */
+    float momentum;
+    float ema_d;        /* ModelEMA decay d for this update */
+    float ema_omd;      /* 1 - d (rounded from double like torch's alpha) */
+    int32_t nesterov;
+    int32_t first_step;
+    int32_t do_ema;
+} yxh_opt_hparams;
+
+int yxh_opt_chunk_elems(void);
+int yxh_sgd_ema_step(const yxh_opt_seg* segs, const int32_t* chunks, int32_t nchunks,
+                     const yxh_opt_hparams* hp, void* stream);
 
 int yxh_abi_version(void);
 const char* yxh_last_error(void);

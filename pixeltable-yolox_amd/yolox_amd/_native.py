@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -50,6 +50,16 @@ class ConvDesc(C.Structure):
 
 
 CONV_ACCUMULATE = 1
+
+
+class OptSeg(C.Structure):
+    _fields_ = [("param", C.c_void_p), ("grad", C.c_void_p), ("buf", C.c_void_p), ("ema", C.c_void_p),
+                ("src", C.c_void_p), ("n", C.c_int64), ("weight_decay", C.c_float), ("group", C.c_int32)]
+
+
+class OptHparams(C.Structure):
+    _fields_ = [("lr", C.c_float * 4), ("momentum", C.c_float), ("ema_d", C.c_float), ("ema_omd", C.c_float),
+                ("nesterov", C.c_int32), ("first_step", C.c_int32), ("do_ema", C.c_int32)]
 
 
 class WgradDesc(C.Structure):
@@ -139,6 +149,8 @@ def lib():
             "yxh_head_decode_train": ([vp, i32, i32, i32, vp, vp, i32, vp, vp], C.c_int),
             "yxh_yolox_loss_bwd": ([vp, vp, vp, i32, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, i32, i32, vp,
                                     vp, vp], C.c_int),
+            "yxh_opt_chunk_elems": ([], C.c_int),
+            "yxh_sgd_ema_step": ([vp, vp, i32, C.POINTER(OptHparams), vp], C.c_int),
             "yxh_run_ops": ([C.POINTER(Op), i32, vp], C.c_int),
             "yxh_graph_create": ([C.POINTER(Op), i32, vp, C.POINTER(vp)], C.c_int),
             "yxh_graph_create_lanes": ([C.POINTER(Op), i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32,
@@ -163,7 +175,8 @@ EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_co
             "yxh_postprocess", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
             "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_spp_bwd",
-            "yxh_upsample_bwd", "yxh_head_decode_train", "yxh_yolox_loss_bwd"]
+            "yxh_upsample_bwd", "yxh_head_decode_train", "yxh_yolox_loss_bwd", "yxh_opt_chunk_elems",
+            "yxh_sgd_ema_step"]
 
 
 def check(rc: int, what: str = "") -> None:

@@ -308,7 +308,7 @@ class TrainGraph:
             self.dcode, B, C.byref(ys), bn.weight.detach().data_ptr(), bn.bias.detach().data_ptr(),
             bn.running_mean.data_ptr(), bn.running_var.data_ptr(), float(bn.eps), float(bn.momentum),
             stats.data_ptr(), self.ws.data_ptr(), self.ws.numel(), self.stream), "bn stats")
-        bn.num_batches_tracked.add_(1)
+        self._bn_counters.append(bn.num_batches_tracked)  # += 1 for all BNs in one launch (forward end)
         if out is None:
             out = Act(torch.empty(B, oh, ow, cout, dtype=self.dtype, device=self.device), 0, cout)
         os_ = out.src()
@@ -526,8 +526,12 @@ class TrainGraph:
         images = images.contiguous()
         labels = labels.to(self.device, torch.float32).contiguous()
         self._keep = (images, labels)
+        self._bn_counters = []
         feats = self.pafpn(self.model.backbone, images)
-        return self.head(self.model.head, feats, labels)
+        out = self.head(self.model.head, feats, labels)
+        if self._bn_counters:
+            torch._foreach_add_(self._bn_counters, 1)
+        return out
 
     def backward(self, grad_total: Optional[torch.Tensor] = None) -> None:
         if not self.tape:

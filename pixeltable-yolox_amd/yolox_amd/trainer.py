@@ -65,8 +65,13 @@ class ModelEMA:
 
 
 def train_one_iter(model: nn.Module, optimizer, images: torch.Tensor, targets: torch.Tensor,
-                   amp_dtype: Optional[torch.dtype] = None, scaler=None, ema: Optional[ModelEMA] = None) -> dict:
-    """trainer.py:96-129 (minus data loading / logging / LR schedule)."""
+                   amp_dtype: Optional[torch.dtype] = None, scaler=None, ema: Optional[ModelEMA] = None,
+                   fused=None) -> dict:
+    """trainer.py:96-129 (minus data loading / logging / LR schedule).
+
+    ``fused`` (yolox_amd.optim.FusedStep over the same optimizer and EMA) replaces
+    ``optimizer.step()`` + ``ema.update(model)`` with one HIP pass; with a GradScaler
+    (fp16) the scaler's unscale / inf-check step runs on torch as in the reference."""
     with torch.autocast("cuda", dtype=amp_dtype or torch.float16, enabled=amp_dtype is not None):
         outputs = model(images, targets)
     loss = outputs["total_loss"]
@@ -77,6 +82,9 @@ def train_one_iter(model: nn.Module, optimizer, images: torch.Tensor, targets: t
         scaler.update()
     else:
         loss.backward()
+        if fused is not None:
+            fused.step()  # SGD + EMA in one pass
+            return outputs
         optimizer.step()
     if ema is not None:
         ema.update(model)
