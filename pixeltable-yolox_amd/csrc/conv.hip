@@ -62,9 +62,19 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvParams p) {
     }
 
     uint4 ra[NA], rb[NB];
-    auto gload = [&](int kit) {
-        const int t = kit / p.ncb, cb = kit - t * p.ncb;
-        const int ky = t / p.kw, kx = t - ky * p.kw;
+    // K iterations (tap t = (ky, kx), channel block cb) are loaded strictly in order:
+    // the indices advance incrementally instead of two divides per stage
+    int g_t = 0, g_cb = 0, g_ky = 0, g_kx = 0;
+    auto gload = [&](int) {
+        const int t = g_t, cb = g_cb, ky = g_ky, kx = g_kx;
+        if (++g_cb == p.ncb) {
+            g_cb = 0;
+            ++g_t;
+            if (++g_kx == p.kw) {
+                g_kx = 0;
+                ++g_ky;
+            }
+        }
         const int c = cb * KSTAGE + coff;
         const bool cok = c < p.cin;
 #pragma unroll
@@ -453,6 +463,8 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
                       : 0;
     p.vec_res = d->residual && ((uintptr_t)d->residual % 8) == 0 && (d->res_cstride * es) % 8 == 0 &&
                 (d->res_bstride * es) % 8 == 0;
+    p.dst_dense = d->dst_bstride == (long long)p.ohw * d->dst_cstride;
+    p.res_dense = d->residual && d->res_bstride == (long long)p.ohw * d->res_cstride;
     p.vec16 = d->dst_dtype == dt && ((uintptr_t)d->dst % 16) == 0 && (d->dst_cstride * des) % 16 == 0 &&
               (d->dst_bstride * des) % 16 == 0 && (d->cout * des) % 16 == 0;
 

@@ -22,6 +22,9 @@ struct ConvParams {
     int dst_f32, act, dcoff, vec_store, vec_res;
     int vec16;  // dst rows 16-byte aligned and cout a chunk multiple: LDS-staged epilogue
     int accum;  // f32 dst += result (YXH_CONV_ACCUMULATE: data-gradient accumulation)
+    // image stride == pixels x pixel stride: pixel m lives at m * cs, no (b, pix) split
+    // (the integer divides were most of a 1x1 conv's VALU work: tools/gpu_pmc.sh)
+    int dst_dense, res_dense;
     float dstride;
 };
 
@@ -169,8 +172,13 @@ __device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&a
             const int pl = wc * WTM + j * 16 + frow;
             const int m = map(pl);
             const int mm = m >= 0 ? m : 0;
-            const int b = mm / p.ohw, pix = mm - b * p.ohw;
-            const int oy = pix / p.out_w, ox = pix - oy * p.out_w;
+            // residual offset b*res_bs + pix*res_cs; no decode on this path (bf16/f16 dst)
+            int b = 0, pix = mm;
+            if (p.res && !p.res_dense) {
+                b = mm / p.ohw;
+                pix = mm - b * p.ohw;
+            }
+            const int oy = 0, ox = 0;
 #pragma unroll
             for (int i = 0; i < FR; ++i) {
                 const int nl = wr * WTN + i * 16 + fq * 4;
@@ -199,9 +207,15 @@ __device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&a
             const int r = q / CPO, c = q - r * CPO;
             const int m = map(r);
             if (m < 0 || c >= ncols) continue;
-            const int b = m / p.ohw, pix = m - b * p.ohw;
+            long long off;
+            if (p.dst_dense) {
+                off = (long long)m * p.dst_cs;
+            } else {
+                const int b = m / p.ohw, pix = m - b * p.ohw;
+                off = (long long)b * p.dst_bs + (long long)pix * p.dst_cs;
+            }
             const uint4 u = *(const uint4*)(smem + r * OROW + c * 16);
-            *(uint4*)((char*)p.dst + ((long long)b * p.dst_bs + (long long)pix * p.dst_cs + n0) * OES + c * 16) = u;
+            *(uint4*)((char*)p.dst + (off + n0) * OES + c * 16) = u;
         }
         return;
     }

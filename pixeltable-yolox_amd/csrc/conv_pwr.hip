@@ -153,9 +153,15 @@ __global__ __launch_bounds__(256) void conv_pwr(ConvParams p, PwrArgs a) {
                 const int r = q / CPO, c = q - r * CPO;
                 const int m = m0 + r;
                 if (m >= p.M || c >= ncols) continue;
-                const int b = m / p.ohw, pix = m - b * p.ohw;
+                long long off;
+                if (p.dst_dense) {
+                    off = (long long)m * p.dst_cs;
+                } else {
+                    const int b = m / p.ohw, pix = m - b * p.ohw;
+                    off = (long long)b * p.dst_bs + (long long)pix * p.dst_cs;
+                }
                 const uint4 u = *(const uint4*)(wst + r * OROW + c * 16);
-                *(uint4*)((char*)p.dst + ((long long)b * p.dst_bs + (long long)pix * p.dst_cs + n0) * OES + c * 16) = u;
+                *(uint4*)((char*)p.dst + (off + n0) * OES + c * 16) = u;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
