@@ -53,6 +53,12 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvParams p) {
         int r = rq + i * RPP;
         int m = m0 + r;
         bool ok = r < TM && m < p.M;
+        if (p.src_dense) {  // 1x1 s1 over dense sources: pixel m is at m * scs, no split
+            bb[i] = ok ? 0 : -1;
+            by[i] = m;
+            bx[i] = 0;
+            continue;
+        }
         int b = ok ? m / p.ohw : 0;
         int rem = m - b * p.ohw;
         int oy = rem / p.out_w, ox = rem - oy * p.out_w;
@@ -93,6 +99,14 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvParams p) {
         const int scs = p.scs[s], sw = p.sw[s], up = p.sup[s] ? 1 : 0;
         const int odd = p.sup[s] == 2 ? 1 : 0;  // zero-inserting dilation: odd positions read 0
         const long long sbs = p.sbs[s];
+        if (p.src_dense) {
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                rb[i] = make_uint4(0, 0, 0, 0);
+                if (bb[i] >= 0 && cok) rb[i] = *(const uint4*)(sp + (long long)by[i] * scs + cc);
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
             int iy = by[i] + ky, ix = bx[i] + kx;
@@ -463,6 +477,9 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
                       : 0;
     p.vec_res = d->residual && ((uintptr_t)d->residual % 8) == 0 && (d->res_cstride * es) % 8 == 0 &&
                 (d->res_bstride * es) % 8 == 0;
+    p.src_dense = p.taps == 1 && p.stride == 1 && p.pad == 0;
+    for (int s = 0; s < d->nsrc; ++s)
+        p.src_dense &= !p.sup[s] && p.sw[s] == p.out_w && p.sbs[s] == (long long)p.ohw * p.scs[s];
     p.dst_dense = d->dst_bstride == (long long)p.ohw * d->dst_cstride;
     p.res_dense = d->residual && d->res_bstride == (long long)p.ohw * d->res_cstride;
     p.vec16 = d->dst_dtype == dt && ((uintptr_t)d->dst % 16) == 0 && (d->dst_cstride * des) % 16 == 0 &&

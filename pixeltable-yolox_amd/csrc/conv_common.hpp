@@ -25,6 +25,7 @@ struct ConvParams {
     // image stride == pixels x pixel stride: pixel m lives at m * cs, no (b, pix) split
     // (the integer divides were most of a 1x1 conv's VALU work: tools/gpu_pmc.sh)
     int dst_dense, res_dense;
+    int src_dense;  // 1x1 s1 p0 over sources without upsample whose pixel m is at m * scs
     float dstride;
 };
 
