@@ -83,9 +83,18 @@ __global__ __launch_bounds__(256) void conv_glds(ConvParams p) {
         }
     }
 
-    auto issue = [&](int kit, int buf) {
-        const int t = kit / p.ncb, cb = kit - t * p.ncb;
-        const int ky = t / p.kw, kx = t - ky * p.kw;
+    // stages are issued strictly in order: (tap, channel block) advance incrementally
+    int g_t = 0, g_cb = 0, g_ky = 0, g_kx = 0;
+    auto issue = [&](int, int buf) {
+        const int t = g_t, cb = g_cb, ky = g_ky, kx = g_kx;
+        if (++g_cb == p.ncb) {
+            g_cb = 0;
+            ++g_t;
+            if (++g_kx == p.kw) {
+                g_kx = 0;
+                ++g_ky;
+            }
+        }
         char* base = smem + buf * BUF;
 #pragma unroll
         for (int i = 0; i < G; ++i) {
