@@ -30,7 +30,8 @@ template <typename T> struct Chunk { static constexpr int N = 16 / sizeof(T); };
 template <bool PRECISE>
 __device__ __forceinline__ float silu(float v) {
     if (PRECISE) return v / (1.0f + expf(-v));
-    return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+    // one v_mul + v_exp_f32 (2^x) + v_add + v_rcp_f32 + v_mul; exp2 overflow -> rcp(inf) = 0
+    return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.4426950408889634f));
 }
 
 template <bool PRECISE = false>
