@@ -36,9 +36,34 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-METRIC = "images/sec (fwd+NMS) YOLOX-s 640×640 bf16 @1/2/4/8 MI355X; box mAP parity"
-PEAK_BF16_TFLOPS = 2500.0  # dense MFMA, MI355X_MICROARCH.md
+METRIC = "images/sec (fwd+NMS) YOLOX-s 640×640 bf16 @1/2/4/8 MI355X; box mAP parity"  # BASELINE.json
+PEAK_BF16_TFLOPS = 2500.0  # dense MFMA bf16/fp16, MI355X_MICROARCH.md
+PEAK_F32_TFLOPS = 157.3    # dense MFMA fp32 (v_mfma_f32_16x16x4_f32)
 PEAK_HBM_GBS = 8000.0
+
+# BASELINE.json configs this bench reproduces: index -> (workload, model, size, dtype, batch per GPU)
+CONFIGS = {
+    1: ("infer", "yolox_s", 640, "bf16", 32),
+    2: ("train", "yolox_s", 640, "fp32", 8),   # -d 8 -b 64, no --fp16 (cli/train.py:56-58)
+    3: ("infer", "yolox_l", 640, "fp16", 16),
+    4: ("train", "yolox_x", 1280, "fp16", 8),  # -d 8 --fp16, default batch 64 -> 8 per GPU
+}
+
+
+def config_index(args):
+    for i, c in CONFIGS.items():
+        if c == (args.workload, args.model, args.size, args.dtype, args.batch):
+            return i
+    return None
+
+
+def metric_name(args) -> str:
+    idx = config_index(args)
+    if idx == 1:
+        return METRIC
+    what = "fwd+NMS" if args.workload == "infer" else "train step"
+    tag = f" (BASELINE configs[{idx}])" if idx is not None else " (not a BASELINE config)"
+    return f"images/sec ({what}) {args.model} {args.size}x{args.size} {args.dtype} batch {args.batch}/GPU MI355X{tag}"
 
 
 def parse():
@@ -50,11 +75,16 @@ def parse():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--chunk", type=int, default=0, help="images per pass of the op list (0 = whole batch)")
     ap.add_argument("--size", type=int, default=640)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32"],
+                    help="compute dtype (default: bf16 for infer = configs[1]; fp32 for train = configs[2], "
+                         "the reference's precision without --fp16)")
     ap.add_argument("--conf", type=float, default=0.5)
     ap.add_argument("--nms", type=float, default=0.65)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="exercise only the process topology (spawn, rendezvous, barrier, max over ranks) "
+                         "with gloo on the CPU; prints one JSON line from rank 0")
     ap.add_argument("--layers", action="store_true", help="print a per-op time/roofline table to stderr")
     ap.add_argument("--tune-file", default="", help="JSON tile choices: loaded if present (skips tuning), else written")
     ap.add_argument("--workload", default="infer", choices=["infer", "train"],
@@ -62,7 +92,29 @@ def parse():
     args = ap.parse_args()
     if args.workload == "train" and args.batch == 32:
         args.batch = 8  # -b 64 over -d 8 (config.py:249-250)
+    if args.dtype is None:
+        args.dtype = "fp32" if args.workload == "train" else "bf16"
     return args
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N fresh processes, one per GPU, under
+    torch.distributed.run (the reference's launch.py:57-94 creates its own process
+    topology the same way: mp.start_processes, one worker per GPU).  Nothing here has
+    touched the GPU (device_count does not initialise it on this image), and the ranks
+    are children -- this process only waits and forwards their exit status."""
+    import socket
+    import subprocess
+    if _BACKEND != "gloo" and torch.cuda.device_count() < args.gpus:
+        sys.exit(f"--gpus {args.gpus}: only {torch.cuda.device_count()} GPU(s) visible")
+    with socket.socket() as sk:  # launch.py:22-34 _find_free_port
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 # "nccl" (RCCL over xGMI, one rank per GPU) for real runs; "gloo" only to rehearse the
@@ -74,6 +126,11 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+        return world, rank, local
     if world > 1:
         import torch.distributed as dist
         if _BACKEND == "gloo":  # rehearsal of the N>1 path on a box with fewer GPUs than ranks
@@ -242,7 +299,7 @@ def main_train(args, world, rank):
     labels = torch.from_numpy(synthetic_labels(B, S, S, seed=2000 + rank)).to(dev)
 
     from yolox_amd.optim import FusedStep
-    fused = FusedStep(model, opt, ema) if scaler is None else None
+    fused = FusedStep(model, opt, ema)  # SGD + EMA (+ GradScaler under fp16) on the device
 
     def step():
         return train_one_iter(net, opt, imgs, labels, amp_dtype=amp, scaler=scaler, ema=ema, fused=fused)
@@ -273,9 +330,10 @@ def main_train(args, world, rank):
     flops_fwd = _fwd_flops(model, B, S)
     flops = 3.0 * flops_fwd  # forward + data gradient + weight gradient of every conv
     achieved = flops / (gpu_ms * 1e-3) / 1e12
-    peak = PEAK_BF16_TFLOPS if amp is not None else 157.3
+    peak = PEAK_BF16_TFLOPS if amp is not None else PEAK_F32_TFLOPS
+    idx = config_index(args)
     result = {
-        "metric": f"images/sec (train step: fwd + SimOTA/loss + bwd + DP all-reduce + SGD + EMA) {args.model} {S}x{S}",
+        "metric": metric_name(args),
         "value": round(world * B * args.steps / dt_max, 2),
         "unit": "images/s",
         "n_gpus": world,
@@ -287,7 +345,10 @@ def main_train(args, world, rank):
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic uniform [0,255] images + COCO-shaped random targets (G ~ U{1..50}), seeded weights",
-        "config": {"workload": f"{args.model} {S}x{S} train step, batch {B}/GPU (BASELINE configs[2]: -d 8 -b 64)",
+        "config": {"workload": f"{args.model} {S}x{S} {args.dtype} train step (fwd + SimOTA/losses + bwd + "
+                               f"DP all-reduce + SGD + EMA), batch {B}/GPU"
+                               + (f" (BASELINE configs[{idx}])" if idx is not None else " (not a BASELINE config)"),
+                   "baseline_config_index": idx,
                    "batch_per_gpu": B, "global_batch": B * world, "image_size": S,
                    "parallelism": f"dp{world} (bucketed RCCL all-reduce overlapped with the reverse pass)"},
         "roofline": {"kernel": "whole step (conv fwd/dgrad/wgrad dominate; HIP events around each step)",
@@ -316,9 +377,33 @@ def _fwd_flops(model, B, S) -> float:
     return ctx.flops
 
 
+def main_dry_run(args, world, rank, local):
+    """The launch/timing skeleton of main() without device work (CPU test of --gpus N)."""
+    ranks = [(rank, local, os.getpid())]
+    if world > 1:
+        import torch.distributed as dist
+        ranks = [None] * world
+        dist.all_gather_object(ranks, (rank, local, os.getpid()))
+    t0 = time.perf_counter()
+    barrier(world)
+    dt_max = max_over_ranks(time.perf_counter() - t0 + 0.001 * rank, world)
+    if rank == 0:
+        print(json.dumps({"metric": metric_name(args), "n_gpus": world, "dry_run": True, "ranks": ranks,
+                          "max_rank_seconds": dt_max}))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     world, rank, local = dist_setup(args)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting n_gpus={world}", file=sys.stderr)
+    if args.dry_run:
+        return main_dry_run(args, world, rank, local)
     if args.workload == "train":
         return main_train(args, world, rank)
     from yolox_amd import _native as N
@@ -383,8 +468,9 @@ def main():
     flops = plan.flops  # algorithmic conv FLOPs of one forward (all images of the batch)
     achieved = flops / (fwd_ms * 1e-3) / 1e12
     traffic = load_traffic(args.model, B, S, args.dtype)
+    idx = config_index(args)
     result = {
-        "metric": METRIC,
+        "metric": metric_name(args),
         "value": round(value, 2),
         "unit": "images/s",
         "n_gpus": world,
@@ -398,7 +484,9 @@ def main():
         "data": "synthetic uniform [0,255] images, seeded weights with calibrated BN (no checkpoints offline)",
         "config": {
             "workload": f"{args.model} {S}x{S} {args.dtype} batch={B}/GPU inference: forward (hipGraph) + "
-                        f"device NMS conf={args.conf} nms={args.nms} (BASELINE configs[1])",
+                        f"device NMS conf={args.conf} nms={args.nms}"
+                        + (f" (BASELINE configs[{idx}])" if idx is not None else " (not a BASELINE config)"),
+            "baseline_config_index": idx,
             "batch_per_gpu": B, "global_batch": B * world, "image_size": S,
             "parallelism": f"replicas x{world} (no data-path collective)",
             "input": f"{args.dtype} NHWC resident in HBM",
@@ -408,9 +496,9 @@ def main():
             "kernel": "conv_igemm (all conv launches of one forward; HIP events around each graph replay)",
             "bound": "mfma",
             "achieved": round(achieved, 2),
-            "peak": PEAK_BF16_TFLOPS if args.dtype != "fp32" else 157.3,
+            "peak": PEAK_BF16_TFLOPS if args.dtype != "fp32" else PEAK_F32_TFLOPS,
             "unit": "TFLOP/s",
-            "frac": round(achieved / (PEAK_BF16_TFLOPS if args.dtype != "fp32" else 157.3), 4),
+            "frac": round(achieved / (PEAK_BF16_TFLOPS if args.dtype != "fp32" else PEAK_F32_TFLOPS), 4),
             "traffic": None if traffic is None else traffic["hbm_bytes_per_forward"],
             "algorithmic_flops_per_launch": flops,
             "forward_ms": round(fwd_ms, 4),

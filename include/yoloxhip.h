@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 5
+#define YXH_ABI_VERSION 7
 
 enum yxh_status {
     YXH_OK = 0,
@@ -167,13 +167,25 @@ int yxh_fold_bn_pack(const float* conv_w, const float* conv_bias, const float* b
                      int32_t dtype, void* w_out, float* b_out, void* stream);
 
 /*
- * yxh_letterbox: preproc / ValTransform (data_augment.py:140-156, processor.py:30-37)
- * of one uint8 HWC RGB image (device memory) into a dst_h x dst_w canvas (pad 114):
- * out_nchw != 0 -> float32 [3][dst_h][dst_w] (the reference's tensor), else uint8
- * [dst_h][dst_w][3] (consumed directly by yxh_focus_pack).
+ * yxh_letterbox_batch: preproc / ValTransform (data_augment.py:140-156) for a whole
+ * batch, replacing YoloxProcessor.__images_to_tensor's per-image loop + torch.stack
+ * (processor.py:30-37).  `pool`: device bytes holding every source image (uint8 HWC
+ * RGB, as np.array(PIL image) gives it); `images` (device): per image the byte offset
+ * of its pixels in `pool` and its size.  Each image is resized by r = min(dst_h/h,
+ * dst_w/w) (cv2 INTER_LINEAR restated; r == 1 is an exact copy) into the top-left of a
+ * dst_h x dst_w canvas filled with 114.  out_format: YXH_LB_F32_NCHW -> float32
+ * [B][3][dst_h][dst_w] (the reference's tensor), YXH_LB_U8_NHWC / YXH_LB_BF16_NHWC ->
+ * [B][dst_h][dst_w][3] (read directly by yxh_stem_conv / yxh_focus_pack).  dst_w must be
+ * a multiple of 4 and dst 16-byte aligned.  Images whose resized size is empty come
+ * out as a plain 114 canvas (the Python layer rejects them first).
  */
-int yxh_letterbox(const uint8_t* src, int32_t src_h, int32_t src_w, int32_t dst_h, int32_t dst_w,
-                  int32_t out_nchw, void* dst, void* stream);
+typedef struct {
+    int64_t src_offset;  /* bytes into pool */
+    int32_t src_h, src_w;
+} yxh_lb_image;
+enum yxh_lb_format { YXH_LB_F32_NCHW = 0, YXH_LB_U8_NHWC = 1, YXH_LB_BF16_NHWC = 2 };
+int yxh_letterbox_batch(const uint8_t* pool, const yxh_lb_image* images, int32_t batch, int32_t dst_h,
+                        int32_t dst_w, int32_t out_format, void* dst, void* stream);
 
 /*
  * yxh_postprocess: utils.postprocess (utils/boxes.py:31-75) with torchvision
@@ -183,7 +195,8 @@ int yxh_letterbox(const uint8_t* src, int32_t src_h, int32_t src_w, int32_t dst_
  *   det       [B, A, 7] fp32 out: rows [x1,y1,x2,y2,obj,cls_conf,cls_idx] in keep order
  *   counts    [B] int32 out: detections per image (0 == the reference's None)
  *   workspace >= yxh_postprocess_workspace_bytes(B, A)
- * Candidate sets larger than 16384 per image set counts[b] = -1 (unsupported).
+ * Any candidate count (anchors <= 2^19 per image); the workspace holds a
+ * [B][A][ceil(A/64)] u64 suppression matrix.
  */
 size_t yxh_postprocess_workspace_bytes(int32_t batch, int32_t anchors);
 int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_classes,
@@ -363,7 +376,7 @@ int yxh_graph_destroy(void* graph_exec);
  * momentum_buffer yet. */
 typedef struct yxh_opt_seg {
     float* param;       /* updated in place; NULL: EMA-only segment */
-    const float* grad;  /* param's gradient */
+    const float* grad;  /* param's gradient (unscaled in place when amp_scale is set) */
     float* buf;         /* momentum buffer */
     float* ema;         /* EMA copy (NULL: none) */
     const float* src;   /* EMA source of an EMA-only segment */
@@ -380,11 +393,25 @@ typedef struct yxh_opt_hparams {
     int32_t nesterov;
     int32_t first_step;
     int32_t do_ema;
+    int32_t reserved;
+    const float* amp_scale;      /* GradScaler scale (device fp32) or NULL: gradients are
+                                    unscaled in place by float(1/double(scale)) first */
+    const float* amp_found_inf;  /* device flag from yxh_amp_found_inf: != 0 skips the SGD
+                                    update (the EMA update still runs, as trainer.py:126-127) */
 } yxh_opt_hparams;
 
 int yxh_opt_chunk_elems(void);
 int yxh_sgd_ema_step(const yxh_opt_seg* segs, const int32_t* chunks, int32_t nchunks,
                      const yxh_opt_hparams* hp, void* stream);
+
+/* GradScaler on the device (torch.amp.GradScaler step/update, core/trainer.py:111-114),
+ * no host sync: yxh_amp_found_inf sets *found_inf = 1 if any parameter segment's gradient
+ * is non-finite (else 0); yxh_amp_update_scale is torch._amp_update_scale_ (scale *=
+ * backoff on inf, else *= growth every growth_interval clean steps). */
+int yxh_amp_found_inf(const yxh_opt_seg* segs, const int32_t* chunks, int32_t nchunks, float* found_inf,
+                      void* stream);
+int yxh_amp_update_scale(float* scale, int32_t* growth_tracker, const float* found_inf, double growth_factor,
+                         double backoff_factor, int32_t growth_interval, void* stream);
 
 int yxh_abi_version(void);
 const char* yxh_last_error(void);

@@ -337,6 +337,26 @@ def forward_train(sd: SD, arch: Arch, x: Tensor, labels: Tensor, use_l1: bool = 
             origin.append(reg.permute(0, 2, 3, 1).reshape(B, h * w, 4))
     out = torch.cat(outs, 1)
     x_shifts, y_shifts, strides = torch.cat(xs_), torch.cat(ys_), torch.cat(ss_)
+    return losses(out, torch.cat(origin, 1) if use_l1 else None, labels, x_shifts, y_shifts, strides, C)
+
+
+def level_grid(hw, strides=(8, 16, 32)):
+    """(x_shifts, y_shifts, strides) [A] for the levels' (h, w) (yolo_head.py:213-231)."""
+    xs_, ys_, ss_ = [], [], []
+    for (h, w), s in zip(hw, strides):
+        gx, gy, _ = anchors_for([(h, w)], (s,))
+        xs_.append(gx)
+        ys_.append(gy)
+        ss_.append(torch.full((h * w,), float(s)))
+    return torch.cat(xs_), torch.cat(ys_), torch.cat(ss_)
+
+
+def losses(out: Tensor, origin, labels: Tensor, x_shifts: Tensor, y_shifts: Tensor, strides: Tensor,
+           C: int = 80):
+    """YoloxHead.get_losses (yolo_head.py:253-411) from train-mode head outputs ``out``
+    [B, A, 5+C] (decoded boxes, raw logits) and, for the L1 term, the raw reg outputs
+    ``origin`` [B, A, 4] (None: use_l1 False)."""
+    use_l1 = origin is not None
     bbox, obj, cls = out[..., :4], out[..., 4:5], out[..., 5:]
     B, A = out.shape[:2]
     nlabel = (labels.sum(dim=2) > 0).sum(dim=1)
@@ -381,7 +401,7 @@ def forward_train(sd: SD, arch: Arch, x: Tensor, labels: Tensor, use_l1: bool = 
                                                   reduction="none").sum() / num_fg
     if use_l1:
         l1_t = torch.cat(l1_t)
-        loss_l1 = F.l1_loss(torch.cat(origin, 1).reshape(-1, 4)[fg_all], l1_t, reduction="none").sum() / num_fg
+        loss_l1 = F.l1_loss(origin.reshape(-1, 4)[fg_all], l1_t, reduction="none").sum() / num_fg
     else:
         loss_l1 = 0.0
     loss = 5.0 * loss_iou + loss_obj + loss_cls + loss_l1
@@ -486,3 +506,63 @@ def fuse_conv_bn(w: Tensor, gamma: Tensor, beta: Tensor, mean: Tensor, var: Tens
     """BN folding (utils/model_utils.py:33-75): W' = W*g/sqrt(v+eps), b' = beta - g*mu/sqrt(v+eps)."""
     s = gamma / torch.sqrt(var + eps)
     return w * s.view(-1, 1, 1, 1), beta - mean * s
+
+
+# ----------------------------------------------------------------- processor
+def _lb_coeffs(dst: int, scale: float, ssize: int):
+    """cv2 INTER_LINEAR source index + 11-bit weights per destination index (restated,
+    see csrc/preprocess.hip): fx = float((d+0.5)*scale - 0.5), clamped at the borders."""
+    f = ((np.arange(dst, dtype=np.float64) + 0.5) * scale - 0.5).astype(np.float32)
+    s = np.floor(f).astype(np.int64)
+    f = (f - s.astype(np.float32)).astype(np.float32)
+    lo = s < 0
+    f[lo], s[lo] = 0.0, 0
+    hi = s >= ssize - 1
+    f[hi], s[hi] = 0.0, ssize - 1
+    a0 = np.rint((np.float32(1.0) - f) * np.float32(2048.0)).astype(np.int64)
+    a1 = np.rint(f * np.float32(2048.0)).astype(np.int64)
+    return s, np.minimum(s + 1, ssize - 1), a0, a1
+
+
+def letterbox(image: np.ndarray, size) -> np.ndarray:
+    """preproc (data_augment.py:140-156) of one H x W x 3 uint8 image -> float32 CHW:
+    r = min(th/h, tw/w), resize to (int(w*r), int(h*r)), top-left paste on a 114 canvas.
+    r == 1 is the reference exactly; the resize restates cv2's fixed-point INTER_LINEAR
+    (vector-path rounding; exact 2x takes INTER_AREA) -- parity unpinned (no cv2)."""
+    th, tw = size
+    h, w = image.shape[:2]
+    r = min(th / h, tw / w)
+    rw, rh = int(w * r), int(h * r)
+    out = np.full((th, tw, 3), 114, np.uint8)
+    if rw == w and rh == h:
+        res = image
+    else:
+        sx, sy = 1.0 / (rw / w), 1.0 / (rh / h)
+        if abs(sx - 2.0) < 2.220446049250313e-16 and abs(sy - 2.0) < 2.220446049250313e-16:
+            a = image.astype(np.int64)
+            res = ((a[0:2 * rh:2, 0:2 * rw:2] + a[0:2 * rh:2, 1:2 * rw:2] + a[1:2 * rh:2, 0:2 * rw:2]
+                    + a[1:2 * rh:2, 1:2 * rw:2] + 2) >> 2).astype(np.uint8)
+        else:
+            x0, x1, ax0, ax1 = _lb_coeffs(rw, sx, w)
+            y0, y1, by0, by1 = _lb_coeffs(rh, sy, h)
+            a = image.astype(np.int64)
+            h0 = a[y0][:, x0] * ax0[None, :, None] + a[y0][:, x1] * ax1[None, :, None]
+            h1 = a[y1][:, x0] * ax0[None, :, None] + a[y1][:, x1] * ax1[None, :, None]
+            t = (((h0 >> 4) * by0[:, None, None]) >> 16) + (((h1 >> 4) * by1[:, None, None]) >> 16) + 2
+            res = np.clip(t >> 2, 0, 255).astype(np.uint8)
+    out[:rh, :rw] = res
+    return np.ascontiguousarray(out.transpose(2, 0, 1), dtype=np.float32)
+
+
+def detections(rows, image_hw, test_size):
+    """YoloxProcessor.postprocess formatting (processor.py:39-54) of one image's [N, 7]
+    float32 rows (or None): boxes / ratio as a CPU fp32 tensor op, scores as the Python
+    double product of the two fp32 confidences, integer labels."""
+    if rows is None:
+        return {"bboxes": [], "scores": [], "labels": []}
+    h, w = image_hw
+    ratio = min(test_size[0] / h, test_size[1] / w)
+    t = torch.from_numpy(np.asarray(rows, np.float32))
+    return {"bboxes": [tuple((r[:4] / ratio).tolist()) for r in t],
+            "scores": [r[4].item() * r[5].item() for r in t],
+            "labels": [int(r[6]) for r in t]}

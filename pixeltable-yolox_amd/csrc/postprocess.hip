@@ -8,9 +8,12 @@
 //               per-image atomic counter.  Slot order is arbitrary; everything
 //               downstream is keyed by (score desc, anchor asc) so results are
 //               deterministic.
-//   pp_sort   : one 1024-thread block per image, bitonic sort of 64-bit keys in LDS
-//               (<= 16384 candidates), sorted rows gathered, max coordinate for the
-//               coordinate-offset branch.
+//   pp_sort_chunk / pp_merge / pp_gather : score sort of each image's candidates by
+//               64-bit keys: chunks of 16384 bitonic-sorted in LDS (one chunk covers a
+//               640 input's 8400 anchors), then, only for larger candidate sets (1280
+//               inputs: 33600 anchors), log2(n/16384) pairwise merge passes (rank in own
+//               run + lower_bound in the partner run); sorted rows gathered, max
+//               coordinate for the coordinate-offset branch.  No candidate cap.
 //   pp_mask   : 64x64 tiles of the upper-triangular suppression matrix; lane t of a
 //               wave owns sorted box i = 64*rb + t and emits one 64-bit word per column
 //               block (the wave64 <-> 64-bit mask correspondence).
@@ -27,7 +30,8 @@
 
 namespace yxh {
 
-constexpr int kSortCap = 16384;
+constexpr int kSortCap = 16384;      // keys sorted per block in LDS (128 KiB)
+constexpr int kMaxAnchors = 1 << 19;  // pp_reduce keeps one removed-bit per candidate in LDS
 constexpr int kRow = 8;  // x1 y1 x2 y2 obj conf cls score
 
 struct PPWork {
@@ -82,32 +86,21 @@ __global__ __launch_bounds__(64) void pp_filter(float* pred, int A, int C, float
     }
 }
 
-__global__ __launch_bounds__(1024) void pp_sort(int A, PPWork w, int* counts) {
+// Stage 1 of the score sort: chunk c of image b (keys [c*kSortCap, ...) of its n
+// candidates) is bitonic-sorted in LDS and written back in place.  With A <= kSortCap
+// there is one chunk and the sort is complete.
+__global__ __launch_bounds__(1024) void pp_sort_chunk(int A, PPWork w) {
     __shared__ unsigned long long keys[kSortCap];
-    __shared__ float red[1024 / 64];
-    const int b = blockIdx.x, tid = threadIdx.x;
+    const int b = blockIdx.y, tid = threadIdx.x;
     const int n = w.cnt[b];
-    if (n > kSortCap || n > w.cap) {
-        if (tid == 0) counts[b] = -1;
-        return;
-    }
+    const int lo = blockIdx.x * kSortCap;
+    if (lo >= n) return;
+    const int m = min(kSortCap, n - lo);
+    unsigned long long* g = w.key + (long long)b * A + lo;
     int np2 = 1;
-    while (np2 < n) np2 <<= 1;
-    for (int q = tid; q < np2; q += 1024) keys[q] = q < n ? w.key[(long long)b * A + q] : ~0ull;
-    // max coordinate over the candidates' 4 box values (batched_nms coordinate trick)
-    float m = -INFINITY;
-    for (int q = tid; q < n; q += 1024) {
-        const float4 r = *(const float4*)(w.cand + ((long long)b * A + q) * kRow);
-        m = fmaxf(m, fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w)));
-    }
-    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    if ((tid & 63) == 0) red[tid >> 6] = m;
+    while (np2 < m) np2 <<= 1;
+    for (int q = tid; q < np2; q += 1024) keys[q] = q < m ? g[q] : ~0ull;
     __syncthreads();
-    if (tid == 0) {
-        float mm = red[0];
-        for (int i = 1; i < 16; ++i) mm = fmaxf(mm, red[i]);
-        w.maxc[b] = mm;
-    }
     for (int k = 2; k <= np2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int q = tid; q < np2; q += 1024) {
@@ -124,8 +117,59 @@ __global__ __launch_bounds__(1024) void pp_sort(int A, PPWork w, int* counts) {
             __syncthreads();
         }
     }
+    for (int q = tid; q < m; q += 1024) g[q] = keys[q];
+}
+
+// Stage 2 (only when A > kSortCap): merge sorted runs of length L pairwise.  Keys are
+// unique (the anchor index is in the low word), so an element's output position is
+// its rank in its own run plus the number of smaller keys in the partner run.
+__global__ __launch_bounds__(256) void pp_merge(int A, PPWork w, int L, const unsigned long long* src,
+                                                unsigned long long* dst) {
+    const int b = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    const int n = w.cnt[b];
+    if (i >= n) return;
+    const unsigned long long* s = src + (long long)b * A;
+    unsigned long long* d = dst + (long long)b * A;
+    const int run = i / L, start = run * L;
+    const int ps = (run ^ 1) * L;
+    const unsigned long long key = s[i];
+    if (ps >= n) {
+        d[i] = key;
+        return;
+    }
+    int lo = ps, hi = min(ps + L, n);  // lower_bound of key in [ps, pe)
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s[mid] < key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    d[min(start, ps) + (i - start) + (lo - ps)] = key;
+}
+
+// Stage 3: sorted candidate rows (by the final key order) and the max box coordinate
+// for the coordinate-offset branch of batched_nms.
+__global__ __launch_bounds__(1024) void pp_gather(int A, PPWork w, const unsigned long long* keys) {
+    __shared__ float red[1024 / 64];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int n = w.cnt[b];
+    float m = -INFINITY;
     for (int q = tid; q < n; q += 1024) {
-        const int a = (int)(keys[q] & 0xffffffffu);
+        const float4 r = *(const float4*)(w.cand + ((long long)b * A + q) * kRow);
+        m = fmaxf(m, fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w)));
+    }
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) {
+        float mm = red[0];
+        for (int i = 1; i < 16; ++i) mm = fmaxf(mm, red[i]);
+        w.maxc[b] = mm;
+    }
+    const unsigned long long* kb = keys + (long long)b * A;
+    for (int q = tid; q < n; q += 1024) {
+        const int a = (int)(kb[q] & 0xffffffffu);
         const int slot = w.slot_of[(long long)b * A + a];
         const float* s = w.cand + ((long long)b * A + slot) * kRow;
         float* d = w.srt + ((long long)b * A + q) * kRow;
@@ -177,7 +221,7 @@ __global__ __launch_bounds__(64) void pp_mask(int A, double thr, int agnostic, l
     __shared__ Box cols[64];
     const int b = blockIdx.y, lane = threadIdx.x;
     const int n = w.cnt[b];
-    if (n > w.cap || n <= 0) return;
+    if (n <= 0) return;
     const int mode = image_mode(n, agnostic, vanilla_numel);
     const float step = w.maxc[b] + 1.0f;
     const int nb = (n + 63) / 64;
@@ -185,13 +229,14 @@ __global__ __launch_bounds__(64) void pp_mask(int A, double thr, int agnostic, l
     const float* srt = w.srt + (long long)b * A * kRow;
     for (long long pi = blockIdx.x; pi < pairs; pi += gridDim.x) {
         // triangular index -> (rb, cb), cb >= rb
-        int rb = 0;
-        long long rem = pi;
-        while (rem >= nb - rb) {
-            rem -= nb - rb;
-            ++rb;
-        }
-        const int cb = rb + (int)rem;
+        // rows r < rb hold S(rb) = rb*nb - rb*(rb-1)/2 pairs; largest rb with S(rb) <= pi
+        const double q = 2.0 * nb + 1.0;
+        int rb = (int)((q - sqrt(q * q - 8.0 * (double)pi)) * 0.5);
+        rb = max(0, min(rb, nb - 1));
+        auto S = [nb](long long r) { return r * nb - r * (r - 1) / 2; };
+        while (rb > 0 && S(rb) > pi) --rb;
+        while (rb + 1 < nb && S(rb + 1) <= pi) ++rb;
+        const int cb = rb + (int)(pi - S(rb));
         const int j = cb * 64 + lane;
         __syncthreads();
         if (j < n) cols[lane] = load_box(srt + (long long)j * kRow, mode, step);
@@ -218,10 +263,9 @@ __global__ __launch_bounds__(64) void pp_mask(int A, double thr, int agnostic, l
 // then every kept lane ORs its own mask row into the later words (independent
 // loads across lanes) -- no dependent global load per kept box.
 __global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int* counts) {
-    __shared__ unsigned long long removed[kSortCap / 64];
+    extern __shared__ unsigned long long removed[];  // [capw]
     const int b = blockIdx.x, lane = threadIdx.x;
     const int n = w.cnt[b];
-    if (n > w.cap) return;  // counts[b] = -1 already
     const int nw = (n + 63) / 64;
     for (int q = lane; q < nw; q += 64) removed[q] = 0;
     __syncthreads();
@@ -263,7 +307,7 @@ __global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int
 }
 
 size_t pp_workspace(int B, int A) {
-    const size_t cap = (size_t)(A < kSortCap ? A : kSortCap);
+    const size_t cap = (size_t)A;
     const size_t capw = (cap + 63) / 64;
     size_t s = 0;
     auto add = [&](size_t bytes) { s += (bytes + 255) & ~(size_t)255; };
@@ -274,6 +318,7 @@ size_t pp_workspace(int B, int A) {
     add(sizeof(float) * kRow * (size_t)B * A);
     add(sizeof(float) * kRow * (size_t)B * A);
     add(sizeof(unsigned long long) * (size_t)B * cap * capw);
+    add(sizeof(unsigned long long) * (size_t)B * A);  // merge ping-pong keys
     return s;
 }
 
@@ -292,7 +337,8 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
         p += (bytes + 255) & ~(size_t)255;
         return r;
     };
-    w.cap = A < kSortCap ? A : kSortCap;
+    YXH_CHECK_ARG(A <= kMaxAnchors, "postprocess supports at most %d anchors per image (got %d)", kMaxAnchors, A);
+    w.cap = A;
     w.capw = (w.cap + 63) / 64;
     w.cnt = (int*)take(sizeof(int) * B);
     w.maxc = (float*)take(sizeof(float) * B);
@@ -301,6 +347,7 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     w.cand = (float*)take(sizeof(float) * kRow * (size_t)B * A);
     w.srt = (float*)take(sizeof(float) * kRow * (size_t)B * A);
     w.mask = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * w.cap * w.capw);
+    unsigned long long* key2 = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * A);
     int rc = check_hip(hipMemsetAsync(w.cnt, 0, sizeof(int) * B, st), "memset counters");
     if (rc) return rc;
     rc = check_hip(hipMemsetAsync(counts, 0, sizeof(int) * B, st), "memset counts");
@@ -308,11 +355,23 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     if (A == 0) return YXH_OK;
     hipLaunchKernelGGL(pp_filter, dim3((A + 63) / 64, B), dim3(64), lds, st, pred, A, C, conf, w);
     YXH_CHECK_LAUNCH("pp_filter");
-    hipLaunchKernelGGL(pp_sort, dim3(B), dim3(1024), 0, st, A, w, counts);
-    YXH_CHECK_LAUNCH("pp_sort");
+    const int nch = (A + kSortCap - 1) / kSortCap;
+    hipLaunchKernelGGL(pp_sort_chunk, dim3(nch, B), dim3(1024), 0, st, A, w);
+    YXH_CHECK_LAUNCH("pp_sort_chunk");
+    unsigned long long* cur = w.key;
+    unsigned long long* nxt = key2;
+    for (int L = kSortCap; L < A; L *= 2) {
+        hipLaunchKernelGGL(pp_merge, dim3((A + 255) / 256, B), dim3(256), 0, st, A, w, L, cur, nxt);
+        YXH_CHECK_LAUNCH("pp_merge");
+        unsigned long long* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+    hipLaunchKernelGGL(pp_gather, dim3(B), dim3(1024), 0, st, A, w, (const unsigned long long*)cur);
+    YXH_CHECK_LAUNCH("pp_gather");
     hipLaunchKernelGGL(pp_mask, dim3(128, B), dim3(64), 0, st, A, nms, agnostic, vanilla_numel, w);
     YXH_CHECK_LAUNCH("pp_mask");
-    hipLaunchKernelGGL(pp_reduce, dim3(B), dim3(64), 0, st, A, w, det, counts);
+    hipLaunchKernelGGL(pp_reduce, dim3(B), dim3(64), (size_t)w.capw * 8, st, A, w, det, counts);
     YXH_CHECK_LAUNCH("pp_reduce");
     return YXH_OK;
 }

@@ -41,7 +41,8 @@ size_t sim_workspace(int B, int A, int L);
 int yolox_loss(const float* preds, const float* origin, const float* labels, int B, int A, int C, int L,
                const int* lhw, const int* strides, int nlev, uint8_t* fg, int* matched, float* piou, int* num_fg,
                float* losses, void* ws, size_t ws_bytes, hipStream_t st);
-int letterbox_launch(const uint8_t* src, int sh, int sw, int th, int tw, int out_nchw, void* dst, hipStream_t st);
+int letterbox_batch_launch(const uint8_t* pool, const yxh_lb_image* images, int B, int th, int tw, int fmt,
+                           void* dst, hipStream_t st);
 size_t reduce_workspace(int C);
 int bn_stats(int dt, int B, const yxh_src* y, const float* gamma, const float* beta, float* rmean, float* rvar,
              float eps, float momentum, float* stats, void* ws, size_t ws_bytes, hipStream_t st);
@@ -123,9 +124,9 @@ int yxh_fold_bn_pack(const float* conv_w, const float* conv_bias, const float* b
                        dtype, w_out, b_out, (hipStream_t)stream);
 }
 
-int yxh_letterbox(const uint8_t* src, int32_t src_h, int32_t src_w, int32_t dst_h, int32_t dst_w,
-                  int32_t out_nchw, void* dst, void* stream) {
-    return letterbox_launch(src, src_h, src_w, dst_h, dst_w, out_nchw, dst, (hipStream_t)stream);
+int yxh_letterbox_batch(const uint8_t* pool, const yxh_lb_image* images, int32_t batch, int32_t dst_h,
+                        int32_t dst_w, int32_t out_format, void* dst, void* stream) {
+    return letterbox_batch_launch(pool, images, batch, dst_h, dst_w, out_format, dst, (hipStream_t)stream);
 }
 
 size_t yxh_postprocess_workspace_bytes(int32_t batch, int32_t anchors) { return pp_workspace(batch, anchors); }

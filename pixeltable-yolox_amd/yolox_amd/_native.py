@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 5
+ABI_VERSION = 7
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -25,6 +25,7 @@ F32, BF16, F16, U8 = 0, 1, 2, 3
 ACT_NONE, ACT_SILU, ACT_RELU, ACT_LRELU, ACT_DECODE, ACT_DECODE_TRAIN = range(6)
 NCHW, NHWC = 0, 1
 OP_CONV, OP_FOCUS, OP_SPP, OP_STEM = 0, 1, 2, 3
+LB_F32_NCHW, LB_U8_NHWC, LB_BF16_NHWC = 0, 1, 2
 
 TORCH_DTYPE = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16, U8: torch.uint8}
 DTYPE_CODE = {v: k for k, v in TORCH_DTYPE.items()}
@@ -59,7 +60,8 @@ class OptSeg(C.Structure):
 
 class OptHparams(C.Structure):
     _fields_ = [("lr", C.c_float * 4), ("momentum", C.c_float), ("ema_d", C.c_float), ("ema_omd", C.c_float),
-                ("nesterov", C.c_int32), ("first_step", C.c_int32), ("do_ema", C.c_int32)]
+                ("nesterov", C.c_int32), ("first_step", C.c_int32), ("do_ema", C.c_int32), ("reserved", C.c_int32),
+                ("amp_scale", C.c_void_p), ("amp_found_inf", C.c_void_p)]
 
 
 class WgradDesc(C.Structure):
@@ -130,7 +132,7 @@ def lib():
             "yxh_stem_pack": ([vp, vp, vp, vp, vp, f32, i32, i32, vp, vp, vp], C.c_int),
             "yxh_fold_bn_pack": ([vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, i32, vp, vp, vp],
                                  C.c_int),
-            "yxh_letterbox": ([vp, i32, i32, i32, i32, i32, vp, vp], C.c_int),
+            "yxh_letterbox_batch": ([vp, vp, i32, i32, i32, i32, vp, vp], C.c_int),
             "yxh_postprocess_workspace_bytes": ([i32, i32], sz),
             "yxh_postprocess": ([vp, i32, i32, i32, f32, f64, i32, i64, vp, vp, vp, sz, vp], C.c_int),
             "yxh_yolox_loss_workspace_bytes": ([i32, i32, i32], sz),
@@ -151,6 +153,8 @@ def lib():
                                     vp, vp], C.c_int),
             "yxh_opt_chunk_elems": ([], C.c_int),
             "yxh_sgd_ema_step": ([vp, vp, i32, C.POINTER(OptHparams), vp], C.c_int),
+            "yxh_amp_found_inf": ([vp, vp, i32, vp, vp], C.c_int),
+            "yxh_amp_update_scale": ([vp, vp, vp, f64, f64, i32, vp], C.c_int),
             "yxh_run_ops": ([C.POINTER(Op), i32, vp], C.c_int),
             "yxh_graph_create": ([C.POINTER(Op), i32, vp, C.POINTER(vp)], C.c_int),
             "yxh_graph_create_lanes": ([C.POINTER(Op), i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32,
@@ -171,12 +175,12 @@ def lib():
 
 
 EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d",
-            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox", "yxh_postprocess_workspace_bytes",
+            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_postprocess_workspace_bytes",
             "yxh_postprocess", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
             "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_spp_bwd",
             "yxh_upsample_bwd", "yxh_head_decode_train", "yxh_yolox_loss_bwd", "yxh_opt_chunk_elems",
-            "yxh_sgd_ema_step"]
+            "yxh_sgd_ema_step", "yxh_amp_found_inf", "yxh_amp_update_scale"]
 
 
 def check(rc: int, what: str = "") -> None:

@@ -372,13 +372,16 @@ class Plan:
         for c in range(self.nchunks):
             self._encode_chunk(c)
 
-    def _encode_chunk(self, c: int) -> None:
+    def _encode_chunk(self, c: int, out_ptr: Optional[int] = None, heads_only: bool = False) -> None:
         ctx, B = self.ctx, self.chunk
-        out_base = self.output.data_ptr() + c * B * self.anchors * self.out_spec.row * 4
+        out_ptr = self.output.data_ptr() if out_ptr is None else out_ptr
+        out_base = out_ptr + c * B * self.anchors * self.out_spec.row * 4
         for i, rec in enumerate(ctx.ops):
+            a = rec.args
+            if heads_only and not (rec.kind == N.OP_CONV and a["dst_f32"]):
+                continue
             op = self._ops[c * self._nops + i]
             op.kind = rec.kind
-            a = rec.args
             if rec.kind == N.OP_FOCUS:
                 f = op.u.focus
                 f.layout = self.input_layout
@@ -442,7 +445,9 @@ class Plan:
 
     # -------------------------------------------------------------- weights
     def _signature(self):
-        return tuple((p.data_ptr(), p._version) for p in self._model.state_dict().values())
+        # parameters and buffers (BN running statistics), by storage and version counter
+        m = self._model
+        return tuple((t.data_ptr(), t._version) for t in list(m.parameters()) + list(m.buffers()))
 
     def pack_weights(self, force: bool = False) -> None:
         sig = self._signature()
@@ -504,13 +509,33 @@ class Plan:
                 op.u.focus.img = x.data_ptr() + c * step
         return x
 
-    def run(self, x: torch.Tensor) -> torch.Tensor:
-        """Eager execution of the op list on the current stream; returns the plan's
-        output buffer [B, A, 5+C] (overwritten by the next run)."""
+    def _bind_output(self, out: Optional[torch.Tensor]) -> None:
+        """Point the head-pred ops' decoded rows at ``out`` (None: the plan's own buffer)."""
+        ptr = None
+        if out is not None:
+            if (tuple(out.shape) != tuple(self.output.shape) or out.dtype != torch.float32 or out.device != self.device
+                    or not out.is_contiguous()):
+                raise ValueError(f"output must be a contiguous float32 {tuple(self.output.shape)} tensor on "
+                                 f"{self.device}")
+            ptr = out.data_ptr()
+        for c in range(self.nchunks):
+            self._encode_chunk(c, ptr, heads_only=True)
+
+    def run(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Eager execution of the op list on the current stream.  Writes ``out`` if given
+        (a fresh tensor the caller owns), else returns the plan's output buffer
+        [B, A, 5+C] (overwritten by the next run)."""
         self.pack_weights()
         x = self._bind_input(x)
-        N.check(self.lib.yxh_run_ops(self._ops, len(self._ops), N.stream_ptr(self.device)), "forward")
-        return self.output
+        if out is None:
+            N.check(self.lib.yxh_run_ops(self._ops, len(self._ops), N.stream_ptr(self.device)), "forward")
+            return self.output
+        self._bind_output(out)
+        try:
+            N.check(self.lib.yxh_run_ops(self._ops, len(self._ops), N.stream_ptr(self.device)), "forward")
+        finally:
+            self._bind_output(None)
+        return out
 
     def static_input(self) -> torch.Tensor:
         """The fixed input buffer a captured graph reads."""
@@ -559,6 +584,10 @@ class Plan:
         return arr(lanes), arr(off), arr(deps)
 
     def replay(self) -> torch.Tensor:
+        """Launch the captured forward; parameters changed since the capture (optimizer or
+        EMA step, load_state_dict) are re-folded into the same weight arena first, which
+        the graph reads in place."""
+        self.pack_weights()
         if self._graph is None:
             self.capture()
         N.check(self.lib.yxh_graph_launch(self._graph, N.stream_ptr(self.device)), "graph replay")

@@ -79,8 +79,20 @@ class YoloxModule(nn.Module):
         if x.dtype not in (torch.float32, torch.bfloat16, torch.float16, torch.uint8):
             x = x.float()
         plan = self.plan_for(B, H, W, N.NCHW, x.dtype)
-        out = plan.run(x)
-        return out.clone()
+        return plan.run(x, out=torch.empty_like(plan.output))
+
+    def forward_nhwc(self, x: torch.Tensor) -> torch.Tensor:
+        """Eval forward from letterboxed NHWC images ([B, H, W, 3] uint8 / bfloat16 on
+        the device, as YoloxProcessor.images_to_device writes them): the fused
+        Focus+stem conv reads them directly, so no float32 NCHW tensor is built.  Same
+        output as ``forward`` on the equivalent float32 NCHW tensor."""
+        if self.training:
+            raise RuntimeError("forward_nhwc is the eval path")
+        if x.dim() != 4 or x.shape[3] != 3:
+            raise ValueError(f"expected [B, H, W, 3] images, got {tuple(x.shape)}")
+        B, H, W, _ = x.shape
+        plan = self.plan_for(B, H, W, N.NHWC, x.dtype)
+        return plan.run(x, out=torch.empty_like(plan.output))
 
     def _apply(self, fn, *args, **kwargs):
         self._plans = {}  # device / dtype changes invalidate every plan
@@ -146,6 +158,8 @@ class Yolox:
         from PIL import Image
 
         images = [im if isinstance(im, Image.Image) else Image.open(im) for im in inputs]
-        tensor = self.processor(images)
-        output = self.module(tensor)
+        # processor + module of the reference (yolox.py:47-52) with the letterboxed batch
+        # kept as uint8 NHWC on the device (bit-identical values, a quarter of the bytes)
+        batch = self.processor.images_to_device(images, "u8_nhwc")
+        output = self.module.forward_nhwc(batch)
         return self.processor.postprocess(images, output, threshold=threshold)

@@ -8,6 +8,12 @@ for hyper-parameters (lr schedules write ``param_groups[i]['lr']`` as usual) and
 checkpoints (its momentum buffers are views of the fused step's flat buffer, stored in
 ``optimizer.state[p]['momentum_buffer']``), and replaces ``optimizer.step()`` +
 ``ema.update(model)`` with one ``yxh_sgd_ema_step`` launch (csrc/optim.hip).
+
+``step(scaler)`` is the --fp16 form (trainer.py:111-114, ``scaler.step(optimizer);
+scaler.update()`` + EMA): the GradScaler's scale / growth tracker tensors are used in
+place, the inf/NaN check, the in-place unscale, the skipped-or-taken SGD update, the EMA
+update and ``_amp_update_scale_`` all run on the device in three launches, with no host
+synchronisation (torch's GradScaler.step reads found_inf with ``.item()``).
 """
 from __future__ import annotations
 
@@ -73,6 +79,7 @@ class FusedStep:
                     self.ema_only.append((e, s))
         self._key = None
         self.chunk = int(self.lib.yxh_opt_chunk_elems())
+        self.found_inf = torch.zeros(1, dtype=torch.float32, device=self.device)
 
     def _table(self):
         grads = [p.grad for p in self.params]
@@ -102,8 +109,20 @@ class FusedStep:
         self._key = key
 
     @torch.no_grad()
-    def step(self) -> None:
+    def step(self, scaler=None) -> None:
+        """optimizer.step() + ema.update(model); with an enabled torch GradScaler whose
+        scale() produced the gradients: scaler.step(optimizer) + scaler.update() + EMA."""
         self._table()
+        amp = scaler is not None and scaler.is_enabled()
+        if amp:
+            self._check_scaler(scaler)
+            st = N.stream_ptr(self.device)
+            N.check(self.lib.yxh_amp_found_inf(self.d_segs.data_ptr(), self.d_chunks.data_ptr(), self.nchunks,
+                                               self.found_inf.data_ptr(), st), "amp_found_inf")
+            if self.first:  # zero buffers: b*m + g == g exactly, the first step needs no flag
+                for p in self.params:
+                    self.opt.state[p]["momentum_buffer"] = self.bufs[id(p)]
+                self.first = False
         hp = N.OptHparams()
         for gi, g in enumerate(self.opt.param_groups):
             hp.lr[gi] = float(g["lr"])
@@ -114,8 +133,17 @@ class FusedStep:
             self.ema.updates += 1
             d = self.ema.decay(self.ema.updates)
             hp.ema_d, hp.ema_omd, hp.do_ema = float(d), float(1.0 - d), 1
+        if amp:
+            hp.amp_scale, hp.amp_found_inf = scaler._scale.data_ptr(), self.found_inf.data_ptr()
         N.check(self.lib.yxh_sgd_ema_step(self.d_segs.data_ptr(), self.d_chunks.data_ptr(), self.nchunks,
                                           C.byref(hp), N.stream_ptr(self.device)), "sgd_ema_step")
+        if amp:
+            N.check(self.lib.yxh_amp_update_scale(
+                scaler._scale.data_ptr(), scaler._growth_tracker.data_ptr(), self.found_inf.data_ptr(),
+                float(scaler._growth_factor), float(scaler._backoff_factor), int(scaler._growth_interval),
+                N.stream_ptr(self.device)), "amp_update_scale")
+            torch.autograd.graph.increment_version([scaler._scale, scaler._growth_tracker] +
+                                                   [p.grad for p in self.params])
         if self.first:
             for p in self.params:
                 self.opt.state[p]["momentum_buffer"] = self.bufs[id(p)]
@@ -124,3 +152,14 @@ class FusedStep:
         torch.autograd.graph.increment_version(self.params)
         if self.ema is not None:
             torch.autograd.graph.increment_version(list(self.ema.ema.parameters()))
+
+    def _check_scaler(self, scaler) -> None:
+        from torch.amp.grad_scaler import OptState
+        if getattr(scaler, "_scale", None) is None or getattr(scaler, "_growth_tracker", None) is None:
+            raise RuntimeError("FusedStep.step(scaler): call scaler.scale(loss) before backward")
+        for t, dt in ((scaler._scale, torch.float32), (scaler._growth_tracker, torch.int32)):
+            if t.device != self.device or t.dtype != dt or t.numel() != 1:
+                raise ValueError("FusedStep.step(scaler): scaler state must be on the parameters' device")
+        stage = scaler._per_optimizer_states[id(self.opt)]["stage"]
+        if stage is not OptState.READY:
+            raise RuntimeError("FusedStep.step(scaler): gradients were already unscaled / stepped by the scaler")

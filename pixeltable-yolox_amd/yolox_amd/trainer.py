@@ -5,8 +5,9 @@ Mirrors ``Trainer.train_one_iter`` (reference core/trainer.py:96-129): autocast 
 optimizer grouping (config.py:307-333: SGD nesterov, momentum 0.9; BN weights without
 decay, conv weights with weight decay, biases) and ModelEMA (utils/ema.py:20-58, decay
 0.9998 * (1 - exp(-updates / 2000)) over every floating state_dict entry).  The step's
-element-wise optimizer / EMA passes run as torch multi-tensor (foreach) kernels; the
-forward/backward is the HIP path (yolox_amd.train), data parallel through yolox_amd.dp.
+element-wise optimizer / EMA / GradScaler passes run fused on the device
+(yolox_amd.optim.FusedStep) or as torch multi-tensor kernels; the forward/backward is the
+HIP path (yolox_amd.train), data parallel through yolox_amd.dp.
 """
 from __future__ import annotations
 
@@ -71,13 +72,17 @@ def train_one_iter(model: nn.Module, optimizer, images: torch.Tensor, targets: t
 
     ``fused`` (yolox_amd.optim.FusedStep over the same optimizer and EMA) replaces
     ``optimizer.step()`` + ``ema.update(model)`` with one HIP pass; with a GradScaler
-    (fp16) the scaler's unscale / inf-check step runs on torch as in the reference."""
+    (--fp16) it also takes over ``scaler.step`` / ``scaler.update`` (inf check, unscale,
+    skip, scale update on the device, no host sync)."""
     with torch.autocast("cuda", dtype=amp_dtype or torch.float16, enabled=amp_dtype is not None):
         outputs = model(images, targets)
     loss = outputs["total_loss"]
     optimizer.zero_grad(set_to_none=True)
     if scaler is not None:
         scaler.scale(loss).backward()
+        if fused is not None:
+            fused.step(scaler)  # scaler.step + scaler.update + EMA in three launches
+            return outputs
         scaler.step(optimizer)
         scaler.update()
     else:

@@ -24,11 +24,14 @@ _workspaces: dict = {}
 
 
 def _workspace(device, B: int, A: int) -> torch.Tensor:
+    """Scratch for one yxh_postprocess call, cached per (device, stream): calls in flight
+    on different streams never share it, calls on one stream are ordered by it."""
     need = int(N.lib().yxh_postprocess_workspace_bytes(B, A))
-    ws = _workspaces.get(device)
+    key = (device, N.stream_ptr(device))
+    ws = _workspaces.get(key)
     if ws is None or ws.numel() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=device)
-        _workspaces[device] = ws
+        _workspaces[key] = ws
     return ws
 
 
@@ -75,8 +78,6 @@ def postprocess(prediction: torch.Tensor, num_classes: int, conf_thre: float = 0
     if pred is not prediction:
         prediction.copy_(pred)
     n = counts.cpu().tolist()
-    if any(c < 0 for c in n):
-        raise NotImplementedError("more than 16384 NMS candidates in one image")
     out = []
     for b, c in enumerate(n):
         if c == 0:

@@ -68,14 +68,41 @@ def _exec(name: str, rel: str) -> types.ModuleType:
     return mod
 
 
+# torchvision is absent: "record" keeps every candidate (pins the pre-NMS filter),
+# "oracle" substitutes the restated torchvision nms/batched_nms (oracle/postprocess_oracle.c)
+# so the reference's processor.postprocess can run end to end.
+NMS_MODE = "record"
+
+
+def _oracle_keep(boxes, scores, idxs, thr):
+    sys.path.insert(0, REPO)
+    from oracle import reference_cpu as O
+    if idxs is None:
+        keep = O.nms(boxes.numpy(), scores.numpy(), thr)
+    else:
+        keep = O.batched_nms(boxes.numpy(), scores.numpy(), idxs.numpy(), thr)
+    return torch.from_numpy(keep)
+
+
 def _recording_batched_nms(boxes, scores, idxs, thr):
     NMS_CALLS.append((boxes.clone(), scores.clone(), idxs.clone(), float(thr)))
+    if NMS_MODE == "oracle":
+        return _oracle_keep(boxes, scores, idxs, thr)
     return torch.argsort(scores, descending=True, stable=True)
 
 
 def _recording_nms(boxes, scores, thr):
     NMS_CALLS.append((boxes.clone(), scores.clone(), None, float(thr)))
+    if NMS_MODE == "oracle":
+        return _oracle_keep(boxes, scores, None, thr)
     return torch.argsort(scores, descending=True, stable=True)
+
+
+def _identity_resize(img, dsize, interpolation=None):
+    """cv2 stub: only the identity resize (r == 1) is reproducible without cv2."""
+    if tuple(dsize) != (img.shape[1], img.shape[0]):
+        raise NotImplementedError(f"cv2 absent: resize {img.shape[:2]} -> {dsize} cannot be pinned")
+    return img.copy()
 
 
 def load_reference():
@@ -112,6 +139,17 @@ def load_reference():
     models.YoloxHead = ref.head.YoloxHead
     models.YoloxModule = ref.yolox.YoloxModule
     ref.boxes = boxes
+    # the real processor (processor.py) over data_augment.ValTransform with a cv2 stub
+    cv2 = types.ModuleType("cv2")
+    cv2.INTER_LINEAR = 1
+    cv2.resize = _identity_resize
+    sys.modules["cv2"] = cv2
+    utils.xyxy2cxcywh = boxes.xyxy2cxcywh
+    ref.augment = _exec("yolox.data.data_augment", "data/data_augment.py")
+    sys.modules["yolox.data"].ValTransform = ref.augment.ValTransform
+    sys.modules["yolox"].data = sys.modules["yolox.data"]
+    sys.modules["yolox"].utils = utils
+    ref.processor = _exec("yolox.models.processor", "models/processor.py")
     return ref
 
 
@@ -352,10 +390,60 @@ def gen_postprocess(ref) -> None:
     save("postprocess_pre_nms.npz", **arrays)
 
 
+IMAGE_FILES = [os.path.join(HERE, "images", f"{n}.jpg") for n in ("000000000001", "000000000009", "000000000016")]
+PROC_THRESHOLDS = (0.65, 0.3)
+
+
+def gen_processor(ref) -> None:
+    """End to end through the reference's own Yolox / YoloxProcessor / ValTransform /
+    YoloxModule / utils.postprocess (tests/test_detections.py:7-45 call patterns) on the
+    reference's test images (copied to tests/golden/images; all give r == 1 at 640, so the
+    cv2 stub's identity resize is exact).  NMS is the restated torchvision (oracle)."""
+    import hashlib
+
+    from PIL import Image
+
+    global NMS_MODE
+    NMS_MODE = "oracle"
+    model = build(ref, "yolox_s")
+    proc = ref.processor.YoloxProcessor("yolox_s")
+    yolox = ref.yolox.Yolox(model, proc)
+    images = [Image.open(f) for f in IMAGE_FILES]
+    arrays = {}
+    for i, im in enumerate(images):
+        arrays[f"img{i}.sha256"] = np.array(hashlib.sha256(np.asarray(im).tobytes()).hexdigest())
+        arrays[f"img{i}.size"] = np.array(im.size, np.int64)
+    with torch.no_grad():
+        tensor = proc(images)
+        arrays["tensor.sha256"] = np.array(hashlib.sha256(tensor.numpy().tobytes()).hexdigest())
+        arrays["tensor.shape"] = np.array(tensor.shape, np.int64)
+        for thr in PROC_THRESHOLDS:
+            patterns = {
+                "files": yolox(IMAGE_FILES, threshold=thr),
+                "images": yolox(images, threshold=thr),
+                "separate": proc.postprocess(images, model(tensor.clone()), threshold=thr),
+                "deprecated": proc.postprocess(images, yolox(tensor.clone()), threshold=thr),
+            }
+            dets = patterns["files"]
+            for name, got in patterns.items():
+                assert got == dets, f"call pattern {name} differs"
+            for i, d in enumerate(dets):
+                arrays[f"t{thr}.img{i}.bboxes"] = np.array(d["bboxes"], np.float64).reshape(-1, 4)
+                arrays[f"t{thr}.img{i}.scores"] = np.array(d["scores"], np.float64)
+                arrays[f"t{thr}.img{i}.labels"] = np.array(d["labels"], np.int64)
+            print(f"threshold {thr}: detections per image {[len(d['labels']) for d in dets]}")
+    NMS_MODE = "record"
+    save("processor_yolox_s_640.npz", **arrays)
+
+
 def main() -> None:
     if not os.path.isdir(REF):
         sys.exit("reference not present: fixtures can only be generated in the build container")
     ref = load_reference()
+    if len(sys.argv) > 1:  # generate only the named fixtures, e.g. `make_golden.py processor`
+        for name in sys.argv[1:]:
+            globals()[f"gen_{name}"](ref)
+        return
     gen_shapes(ref)
     gen_bn_stats(ref)
     gen_forward(ref)
@@ -364,6 +452,7 @@ def main() -> None:
     gen_simota(ref)
     gen_boxes(ref)
     gen_postprocess(ref)
+    gen_processor(ref)
 
 
 if __name__ == "__main__":

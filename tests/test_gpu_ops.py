@@ -266,8 +266,10 @@ def test_letterbox_identity_and_pad():
     ref_b = np.full((3, 640, 640), 114, np.float32)
     ref_b[:, :640, :320] = b.transpose(2, 0, 1)
     assert np.array_equal(out[0].numpy(), ref_a) and np.array_equal(out[1].numpy(), ref_b)
-    u8 = letterbox_batch([a], (640, 640), out_nchw=False).cpu().numpy()
+    u8 = letterbox_batch([a], (640, 640), "u8_nhwc").cpu().numpy()
     assert np.array_equal(u8[0].transpose(2, 0, 1).astype(np.float32), ref_a)
+    bf = letterbox_batch([a, b], (640, 640), "bf16_nhwc").cpu().float().numpy()
+    assert np.array_equal(bf[1].transpose(2, 0, 1), ref_b)
 
 
 def test_letterbox_resize_cases():

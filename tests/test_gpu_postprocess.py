@@ -83,3 +83,21 @@ def test_score_ties_are_resolved_by_anchor_order(oracle):
 def test_single_class_many_overlaps(oracle):
     pred = synthetic_pred(2, 1024, 1, 5, dense=True)
     run_both(oracle, pred, 1, 0.0, 0.5)
+
+
+def test_full_1280_anchor_set_low_conf(oracle):
+    """33600 anchors (1280 input) at conf 0.01: > 16384 candidates per image, so the
+    score sort runs as LDS chunks + global merge passes (boxes.py:56-67 has no cap)."""
+    pred = synthetic_pred(2, 33600, 80, 11)
+    pred[..., 4] = np.maximum(pred[..., 4], 0.5)
+    pred[..., 5] = np.maximum(pred[..., 5], 0.2)  # every anchor passes conf 0.01
+    want = run_both(oracle, pred, 80, 0.01, 0.65)
+    assert all(w is not None for w in want)
+    run_both(oracle, pred, 80, 0.01, 0.65, agnostic=True)
+
+
+@pytest.mark.parametrize("A", [16385, 40000])
+def test_candidate_counts_past_one_sort_chunk(oracle, A):
+    """Candidate counts just past one LDS chunk and past two merge levels, few classes."""
+    pred = synthetic_pred(1, A, 3, 13)
+    run_both(oracle, pred, 3, 0.0, 0.5)
