@@ -413,6 +413,36 @@ int yxh_amp_found_inf(const yxh_opt_seg* segs, const int32_t* chunks, int32_t nc
 int yxh_amp_update_scale(float* scale, int32_t* growth_tracker, const float* found_inf, double growth_factor,
                          double backoff_factor, int32_t growth_interval, void* stream);
 
+/* ---------------------------------------------------------------- box mAP (host)
+ * yxh_coco_eval: COCO bbox evaluation as the reference's CocoEvalOpt runs it
+ * (yolox/layers/fast_coco_eval_api.py:24-149): pycocotools computeIoU (bbox, crowd-aware),
+ * the C++ EvaluateImages (yolox/layers/cocoeval/cocoeval.cpp:140-197) and Accumulate
+ * (:370-500) in one host call.  Cells p = image * num_categories + category hold ground
+ * truths gts[gt_off[p], gt_off[p+1]) and detections dts[dt_off[p], dt_off[p+1]) in any
+ * order (detection ids nonzero, as loadRes assigns 1..N).  Outputs (caller-allocated,
+ * fp64, -1 where a setting has no valid ground truth): precision and scores
+ * [T][R][K][A][M], recall [T][K][A][M] -- CocoEvalOpt.eval's arrays.  Host memory; no
+ * device work.  yxh_coco_iou: the [nd][ng] IoU matrix alone. */
+typedef struct {
+    int64_t id;
+    double score;     /* detections */
+    double area;      /* the annotation's area (detections: w * h) */
+    double box[4];    /* x, y, w, h */
+    int32_t is_crowd;
+    int32_t ignore;   /* ground truths: pycocotools' ignore (= iscrowd unless set) */
+} yxh_coco_instance;
+typedef struct {
+    int32_t num_images, num_categories, num_area_ranges, num_iou_thresholds, num_recall_thresholds, num_max_dets;
+    const double* area_ranges;        /* [A][2] */
+    const double* iou_thresholds;     /* [T] */
+    const double* recall_thresholds;  /* [R] */
+    const int32_t* max_dets;          /* [M] */
+} yxh_coco_params;
+int yxh_coco_eval(const yxh_coco_params* params, const yxh_coco_instance* gts, const int64_t* gt_off,
+                  const yxh_coco_instance* dts, const int64_t* dt_off, double* precision, double* recall,
+                  double* scores);
+int yxh_coco_iou(const yxh_coco_instance* dts, int32_t nd, const yxh_coco_instance* gts, int32_t ng, double* iou);
+
 int yxh_abi_version(void);
 const char* yxh_last_error(void);
 size_t yxh_sizeof_op(void);        /* ABI self-check for bindings */

@@ -64,6 +64,18 @@ class OptHparams(C.Structure):
                 ("amp_scale", C.c_void_p), ("amp_found_inf", C.c_void_p)]
 
 
+class CocoInstance(C.Structure):
+    _fields_ = [("id", C.c_int64), ("score", C.c_double), ("area", C.c_double), ("box", C.c_double * 4),
+                ("is_crowd", C.c_int32), ("ignore", C.c_int32)]
+
+
+class CocoParams(C.Structure):
+    _fields_ = [("num_images", C.c_int32), ("num_categories", C.c_int32), ("num_area_ranges", C.c_int32),
+                ("num_iou_thresholds", C.c_int32), ("num_recall_thresholds", C.c_int32),
+                ("num_max_dets", C.c_int32), ("area_ranges", C.c_void_p), ("iou_thresholds", C.c_void_p),
+                ("recall_thresholds", C.c_void_p), ("max_dets", C.c_void_p)]
+
+
 class WgradDesc(C.Structure):
     _fields_ = [("dtype", C.c_int32), ("batch", C.c_int32), ("in_h", C.c_int32), ("in_w", C.c_int32),
                 ("out_h", C.c_int32), ("out_w", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32),
@@ -154,6 +166,8 @@ def lib():
             "yxh_opt_chunk_elems": ([], C.c_int),
             "yxh_sgd_ema_step": ([vp, vp, i32, C.POINTER(OptHparams), vp], C.c_int),
             "yxh_amp_found_inf": ([vp, vp, i32, vp, vp], C.c_int),
+            "yxh_coco_eval": ([C.POINTER(CocoParams), vp, vp, vp, vp, vp, vp, vp], C.c_int),
+            "yxh_coco_iou": ([vp, i32, vp, i32, vp], C.c_int),
             "yxh_amp_update_scale": ([vp, vp, vp, f64, f64, i32, vp], C.c_int),
             "yxh_run_ops": ([C.POINTER(Op), i32, vp], C.c_int),
             "yxh_graph_create": ([C.POINTER(Op), i32, vp, C.POINTER(vp)], C.c_int),
@@ -180,7 +194,7 @@ EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_co
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
             "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_spp_bwd",
             "yxh_upsample_bwd", "yxh_head_decode_train", "yxh_yolox_loss_bwd", "yxh_opt_chunk_elems",
-            "yxh_sgd_ema_step", "yxh_amp_found_inf", "yxh_amp_update_scale"]
+            "yxh_sgd_ema_step", "yxh_amp_found_inf", "yxh_amp_update_scale", "yxh_coco_eval", "yxh_coco_iou"]
 
 
 def check(rc: int, what: str = "") -> None:

@@ -147,3 +147,29 @@ def test_replay_after_load_state_dict_uses_new_weights():
     want = other.forward_nhwc(x)
     assert not torch.equal(first, again)
     assert torch.equal(again, want)
+
+
+def test_box_map_parity_vs_reference_detections(golden, api):
+    """Box-mAP parity (BASELINE metric): the reference's own detections on its test images
+    (fixture, threshold 0.3) taken as ground truth; the HIP path's detections scored by the
+    mAP harness (yolox_amd.evaluators, pinned to the reference's cocoeval.cpp) must reach
+    AP@[.5:.95] = AP@.5 = 1 -- every reference box found, same class, IoU > 0.95."""
+    from yolox_amd.evaluators import COCOParams, coco_bbox_eval
+    d = golden("processor_yolox_s_640.npz")
+    yolox, _, _ = api
+    dets = yolox(FILES, threshold=0.3)
+    anns, res = [], []
+    for i in range(3):
+        for (x1, y1, x2, y2), lab in zip(d[f"t0.3.img{i}.bboxes"], d[f"t0.3.img{i}.labels"]):
+            anns.append({"id": len(anns) + 1, "image_id": i + 1, "category_id": int(lab) + 1,
+                         "bbox": [x1, y1, x2 - x1, y2 - y1], "area": (x2 - x1) * (y2 - y1), "iscrowd": 0})
+        for (x1, y1, x2, y2), s, lab in zip(dets[i]["bboxes"], dets[i]["scores"], dets[i]["labels"]):
+            res.append({"image_id": i + 1, "category_id": lab + 1, "bbox": [x1, y1, x2 - x1, y2 - y1], "score": s})
+    gt = {"images": [{"id": i + 1} for i in range(3)], "annotations": anns,
+          "categories": [{"id": c + 1} for c in range(80)]}
+    # up to ~300 boxes per image here: max-dets 1000 so no cell is cut at COCO's 100
+    # (summarize's stats[0] is pinned to maxDets 100, as pycocotools: read the array instead)
+    ev = coco_bbox_eval(gt, res, COCOParams(maxDets=[1, 10, 1000]))
+    prec = ev["precision"][:, :, :, 0, 2]
+    ap = prec[prec > -1].mean()
+    assert ap == pytest.approx(1.0) and ev["stats"][1] == pytest.approx(1.0), (ap, ev["stats"])
