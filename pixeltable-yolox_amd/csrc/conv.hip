@@ -508,7 +508,8 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         const int want_ks = (d->tile & 1) + 1;
         YXH_CHECK_ARG((tile > 0 && tile < kNumTiles) || (tile > 16 && tile < 16 + kNumTiles) ||
                           (tile > 32 && tile <= 32 + kNumRowTiles) || (tile > 64 && tile <= 64 + kNumPwTiles) ||
-                          (tile > 80 && tile <= 80 + kNumPwrTiles),
+                          (tile > 80 && tile <= 80 + kNumPwrTiles) || (tile > 96 && tile <= 96 + kNumPwfTiles) ||
+                          (tile > 112 && tile <= 112 + kNumR3Tiles),
                       "tile %d", d->tile);
         YXH_CHECK_ARG(want_ks == 1 || ks == 2, "2-slab staging not possible for this conv");
         ks = want_ks;
@@ -519,6 +520,8 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         set_error("dilated (upsample == 2) sources run on the register-staged kernel only (tile ids 1-9)");
         return YXH_EUNSUPPORTED;
     }
+    if (tile > 112) return conv_r3_dispatch(dt, tile - 112, p, st);
+    if (tile > 96) return conv_pwf_dispatch(dt, tile - 96, p, st);
     if (tile > 80) return conv_pwr_dispatch(dt, tile - 80, p, st);
     if (tile > 64) return conv_pw_dispatch(dt, tile - 64, p, ks, st);
     if (tile > 32) return conv_rows_dispatch(dt, tile - 32, p, ks, st);

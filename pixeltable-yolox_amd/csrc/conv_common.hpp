@@ -258,5 +258,11 @@ constexpr int kNumPwTiles = 6;
 // Register-operand 1x1 conv (conv_pwr.hip): tile ids 81..80+kNumPwrTiles
 int conv_pwr_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumPwrTiles = 2;
+// VALU-free-loop dense 1x1 conv (conv_pwf.hip): tile ids 97..96+kNumPwfTiles
+int conv_pwf_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
+constexpr int kNumPwfTiles = 8;
+// 3x3 conv with the branch-free buffer-LDS loader (conv_r3.hip): tile ids 113..112+kNumR3Tiles
+int conv_r3_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
+constexpr int kNumR3Tiles = 12;
 
 }  // namespace yxh

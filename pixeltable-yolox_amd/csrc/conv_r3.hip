@@ -1,0 +1,303 @@
+// conv_r3: 3x3 conv (stride 1 or 2, pad 1) with a branch-free LDS-DMA loader
+// (reference network_blocks.py:48-49 BaseConv with ksize 3: the 3x3 convs of
+// darknet.py / yolo_pafpn.py / yolo_head.py).
+//
+// Same tiling as conv_rows (a block = TN output channels x a TY x TX pixel tile of one
+// image; per K stage (channel block cb, kernel row ky) the three kx taps of the weights
+// and the TY input rows the tile reads, HX = (TX-1)*S + 3 pixels wide, land in LDS and
+// the kx taps read the row image shifted by kx), but the loader does no per-stage
+// address work:
+//  * every DMA is a buffer_load ... lds through a buffer descriptor (image / weights):
+//    the per-lane byte offset is computed ONCE per block, the stage offset (cb, ky) is a
+//    scalar soffset, and zero padding is the descriptor's range check -- a lane whose
+//    source pixel is outside the image carries an out-of-range offset and the hardware
+//    writes zeros (no select, no branch, no zero buffer);
+//  * the ky loop is unrolled against a 3-slot ring (slot = ky), so the per-lane offset
+//    for row ky is one of three precomputed registers;
+//  * instructions are A (weights) or B (pixels) per wave-uniform index, never mixed;
+//  * DMAs are issued from inline asm: hipcc's own global/buffer_load_lds makes it put
+//    s_waitcnt vmcnt(0) in front of every later ds_read (it cannot tell the ring slots
+//    apart), which would drain the ring each stage; counted vmcnt + raw s_barrier order
+//    the reads instead.
+// TN = 64 (4 waves along pixels) or 128 (2 x 2); CH 16-byte chunks (8 channels each
+// for 16-bit types) per stage.
+#include "conv_common.hpp"
+
+namespace yxh {
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int N>
+__device__ __forceinline__ void r3_wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void r3_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// raw buffer descriptor (stride 0, byte-range checked): out-of-range loads return 0
+__device__ __forceinline__ u32x4 r3_srd(const void* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    u32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu);
+    r.z = __builtin_amdgcn_readfirstlane(bytes);
+    r.w = 0x00020000u;
+    return r;
+}
+
+__device__ __forceinline__ void r3_dma(u32x4 srd, uint32_t voff, uint32_t soff, uint32_t lds) {
+    uint32_t saved;  // M0 is reserved to the compiler: save and restore it around the DMA
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(saved)
+        : "v"(voff), "s"(srd), "s"(soff), "s"(lds)
+        : "memory");
+}
+
+__device__ __forceinline__ uint32_t r3_lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+__device__ __forceinline__ int r3_xcd_remap(int id, int nblk) {
+    const int q = nblk / 8, r = nblk % 8, xcd = id % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
+}
+
+constexpr uint32_t kR3Oob = 0x80000000u;  // beyond any descriptor range: reads 0
+
+}  // namespace
+
+template <typename T, int S, int TX, int TY, int CH, int TN>
+__global__ __launch_bounds__(256) void conv_r3(ConvParams p, int tiles_x, int tiles_y, int ntn) {
+    constexpr int NBUF = 3;  // = the 3 kernel rows: ring slot of stage (cb, ky) is ky
+    constexpr int WN = TN / 64, WM = 4 / WN;
+    constexpr int EPC = Chunk<T>::N;
+    constexpr int ES = sizeof(T);
+    constexpr int KS = CH / 4;  // 64-byte slabs (one MFMA K step) per stage
+    constexpr int KST = CH * EPC;
+    constexpr int TM = TX * TY, WTM = TM / WM;
+    constexpr int FR = 4, FC = WTM / 16;
+    constexpr int HX = (TX - 1) * S + 3;
+    constexpr int A_SLOTS = 3 * TN * CH, B_SLOTS = TY * HX * CH;
+    constexpr int GA = A_SLOTS / 256, GB = (B_SLOTS + 255) / 256;
+    constexpr int G = GA + GB;  // DMA instructions per wave per stage
+    constexpr int BUF = G * 256 * 16;
+    constexpr int PXG = 16 / CH;
+    static_assert(A_SLOTS % 256 == 0, "weight slots: whole waves");
+    static_assert(TM % (16 * WM) == 0, "pixel tile must split into 16-pixel fragments per wave");
+    static_assert(G <= 20, "vmcnt range");
+    __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nblk = tiles_x * tiles_y * (p.M / p.ohw) * ntn;
+    const int bid = r3_xcd_remap(blockIdx.x, nblk);
+    const int nt = bid % ntn;
+    int t = bid / ntn;
+    const int tx_i = t % tiles_x;
+    t /= tiles_x;
+    const int ty_i = t % tiles_y;
+    const int b = t / tiles_y;
+    const int n0 = nt * TN, oy0 = ty_i * TY, ox0 = tx_i * TX;
+    const int wr = wave / WM, wc = wave % WM;
+    const int cin = p.cin, scs = p.scs[0], in_w = p.in_w, in_h = p.in_h;
+
+    const u32x4 wsrd = r3_srd(p.w, (uint32_t)((long long)p.cout * 9 * cin * ES));
+    const u32x4 xsrd = r3_srd((const T*)p.sptr[0] + (long long)b * p.sbs[0],
+                              (uint32_t)((long long)in_h * in_w * scs * ES));
+
+    // per-lane DMA offsets, fixed for the block's life
+    uint32_t aoff[GA];
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+        const int s = 64 * (wave + 4 * i) + lane;
+        const int kx = s / (CH * TN), rem = s - kx * (CH * TN);
+        const int c = rem / TN, rp = rem - c * TN;
+        const int n = min(n0 + (rp ^ (2 * (c & 3) + (c >> 2))), p.cout - 1);
+        aoff[i] = (uint32_t)(((n * 9 + kx) * cin + c * EPC) * ES);
+    }
+    uint32_t boff[GB][3];  // per kernel row ky
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+        const int sb = 64 * (wave + 4 * i) + lane;
+        const int hp = sb / CH, cp = sb - hp * CH;
+        const int c = cp ^ ((hp / PXG) & (CH - 1));
+        const int ty = hp / HX, hx = hp - ty * HX;
+        const int iy0 = (oy0 + ty) * S - 1, ix = ox0 * S - 1 + hx;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const int iy = iy0 + ky;
+            const bool ok = sb < B_SLOTS && iy >= 0 && iy < in_h && ix >= 0 && ix < in_w;
+            boff[i][ky] = ok ? (uint32_t)(((iy * in_w + ix) * scs + c * EPC) * ES) : kR3Oob;
+        }
+    }
+    const uint32_t lds0 = r3_lds_addr(smem) + (uint32_t)wave * 1024;
+
+    auto issue = [&](int cb, auto kyc) {
+        constexpr int ky = decltype(kyc)::value;
+        const uint32_t base = lds0 + ky * BUF;
+        const uint32_t soa = (uint32_t)((ky * 3 * cin + cb * KST) * ES), sob = (uint32_t)(cb * KST * ES);
+#pragma unroll
+        for (int i = 0; i < GA; ++i) r3_dma(wsrd, aoff[i], soa, base + i * 4096);
+#pragma unroll
+        for (int i = 0; i < GB; ++i) r3_dma(xsrd, boff[i][ky], sob, base + GA * 4096 + i * 4096);
+    };
+
+    f32x4 acc[FR][FC];
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float lbias[FR][4];
+    load_lane_bias<TN, WN, WM>(p, n0, lbias);
+
+    const int frow = lane & 15, fq = lane >> 4;
+    int hp0[FC];  // B-image pixel of this lane's fragment column at kx = 0
+#pragma unroll
+    for (int j = 0; j < FC; ++j) {
+        const int pl = wc * WTM + j * 16 + frow;
+        const int ty = pl / TX, tx = pl - ty * TX;
+        hp0[j] = ty * HX + tx * S;
+    }
+
+    auto compute = [&](int slot) {
+        const char* A = smem + slot * BUF;
+        const char* B = A + GA * 4096;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+#pragma unroll
+            for (int sl = 0; sl < KS; ++sl) {
+                const int chunk = sl * 4 + fq, swa = 2 * fq + sl;
+                uint4 af[FR], bf[FC];
+#pragma unroll
+                for (int i = 0; i < FR; ++i) {
+                    const int r = wr * 64 + i * 16 + frow;
+                    af[i] = *(const uint4*)(A + ((kx * CH + chunk) * TN + (r ^ swa)) * 16);
+                }
+#pragma unroll
+                for (int j = 0; j < FC; ++j) {
+                    const int hp = hp0[j] + kx;
+                    bf[j] = *(const uint4*)(B + (hp * CH + (chunk ^ ((hp / PXG) & (CH - 1)))) * 16);
+                }
+#pragma unroll
+                for (int i = 0; i < FR; ++i)
+#pragma unroll
+                    for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], af[i], bf[j]);
+            }
+        }
+    };
+
+    using K0 = std::integral_constant<int, 0>;
+    using K1 = std::integral_constant<int, 1>;
+    using K2 = std::integral_constant<int, 2>;
+    const int ncb = p.ncb;
+    issue(0, K0{});
+    issue(0, K1{});
+    // stage (cb, ky): wait for it (one younger stage may fly), barrier, issue the stage
+    // two ahead into the slot stage (cb, ky-1) just vacated, compute
+    for (int cb = 0; cb < ncb; ++cb) {
+        const bool more = cb + 1 < ncb;
+        r3_wait_vm<G>();
+        r3_barrier();
+        issue(cb, K2{});
+        compute(0);
+        r3_wait_vm<G>();
+        r3_barrier();
+        if (more) issue(cb + 1, K0{});
+        compute(1);
+        if (more) r3_wait_vm<G>();
+        else r3_wait_vm<0>();
+        r3_barrier();
+        if (more) issue(cb + 1, K1{});
+        compute(2);
+    }
+    r3_wait_vm<0>();
+    r3_barrier();
+    const int OH = p.out_h, OW = p.out_w, mb = b * p.ohw;
+    conv_epilogue_map<T, TN, TM, WN, WM, NBUF * BUF>(
+        p, acc, smem,
+        [=](int pl) {
+            const int ty = pl / TX, tx = pl - ty * TX;
+            const int oy = oy0 + ty, ox = ox0 + tx;
+            return (oy < OH && ox < OW) ? mb + oy * OW + ox : -1;
+        },
+        n0, lbias);
+}
+
+template <typename T, int S, int TX, int TY, int CH, int TN>
+static int launch_r3(const ConvParams& p, hipStream_t st) {
+    constexpr int HX = (TX - 1) * S + 3;
+    constexpr int G = 3 * TN * CH / 256 + (TY * HX * CH + 255) / 256;
+    constexpr int lds = 3 * G * 256 * 16;
+    if constexpr (lds > 160 * 1024 || G > 20) {
+        set_error("conv_r3 variant needs more than 160 KiB of LDS");
+        return YXH_EUNSUPPORTED;
+    } else {
+        if (p.stride != S) {
+            set_error("conv_r3 variant built for stride %d", S);
+            return YXH_EUNSUPPORTED;
+        }
+        const int kst = CH * Chunk<T>::N;
+        if (p.cin % kst) {
+            set_error("conv_r3: cin %d not a multiple of the %d-channel stage", p.cin, kst);
+            return YXH_EUNSUPPORTED;
+        }
+        ConvParams q = p;
+        q.ncb = p.cin / kst;
+        const int tiles_x = (p.out_w + TX - 1) / TX, tiles_y = (p.out_h + TY - 1) / TY;
+        const int ntn = (p.cout + TN - 1) / TN;
+        const long long nblk = (long long)tiles_x * tiles_y * (p.M / p.ohw) * ntn;
+        if (nblk >= (1LL << 31)) {
+            set_error("conv_r3 grid too large");
+            return YXH_EINVAL;
+        }
+        hipLaunchKernelGGL((conv_r3<T, S, TX, TY, CH, TN>), dim3((unsigned)nblk), dim3(256), 0, st, q, tiles_x,
+                           tiles_y, ntn);
+        YXH_CHECK_LAUNCH("conv_r3 launch");
+        return YXH_OK;
+    }
+}
+
+template <typename T>
+static int r3_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
+    // id -> (stride, TX, TY, CH, TN)
+    switch (id) {
+        case 1: return launch_r3<T, 1, 32, 8, 4, 64>(p, st);
+        case 2: return launch_r3<T, 1, 16, 16, 4, 64>(p, st);
+        case 3: return launch_r3<T, 1, 32, 4, 8, 64>(p, st);
+        case 4: return launch_r3<T, 1, 16, 8, 4, 128>(p, st);
+        case 5: return launch_r3<T, 1, 32, 4, 4, 128>(p, st);
+        case 6: return launch_r3<T, 1, 20, 16, 4, 64>(p, st);
+        case 7: return launch_r3<T, 1, 20, 8, 4, 128>(p, st);
+        case 8: return launch_r3<T, 1, 8, 8, 4, 128>(p, st);
+        case 9: return launch_r3<T, 2, 16, 8, 4, 64>(p, st);
+        case 10: return launch_r3<T, 2, 8, 8, 4, 128>(p, st);
+        case 11: return launch_r3<T, 2, 16, 4, 4, 128>(p, st);
+        case 12: return launch_r3<T, 2, 20, 8, 4, 128>(p, st);
+        default: set_error("conv_r3 tile id %d", id); return YXH_EINVAL;
+    }
+}
+
+int conv_r3_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st) {
+    if (p.taps != 9 || p.kw != 3 || p.pad != 1 || p.nsrc != 1 || p.sup[0] || p.sw[0] != p.in_w) {
+        set_error("conv_r3 needs a 3x3 pad-1 conv over one plain source");
+        return YXH_EUNSUPPORTED;
+    }
+    if ((long long)p.in_h * p.in_w * p.scs[0] * 2 >= (1LL << 31) || (long long)p.cout * 9 * p.cin * 2 >= (1LL << 31)) {
+        set_error("conv_r3: image / weights exceed 31-bit byte offsets");
+        return YXH_EUNSUPPORTED;
+    }
+    if (dtype == YXH_BF16) return r3_dispatch_t<bf16>(id, p, st);
+    if (dtype == YXH_F16) return r3_dispatch_t<f16>(id, p, st);
+    set_error("conv_r3 is built for bf16/f16 only");
+    return YXH_EUNSUPPORTED;
+}
+
+}  // namespace yxh

@@ -540,3 +540,89 @@ def test_register_pointwise_rejects():
     with pytest.raises(NotImplementedError, match="conv_pwr"):
         run_conv([(nhwc(torch.randn(1, 512, 4, 4), torch.bfloat16), 0, 512, 0)], big, bnb, torch.bfloat16,
                  tile=2 * 81)
+
+
+PWF_GEOMS = [  # cin, cout, H, W
+    (32, 16, 16, 16), (64, 64, 20, 20), (128, 80, 33, 17), (512, 256, 4, 4), (1024, 512, 4, 4), (256, 5, 6, 6),
+    (64, 192, 7, 9)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("geom", PWF_GEOMS)
+def test_dense_pointwise_conv_pwf(dtype, geom):
+    """conv_pwf (ids 97-104): dense 1x1 conv with the branch-free LDS-DMA loader, every
+    variant (one tile per block / persistent) vs the fp32 reference, incl. pixel and
+    channel tails; K stages of 32 or 64 channels (cin not a multiple -> rejected)."""
+    cin, cout, H, W = geom
+    conv, bn = make_conv(cin, cout, 1, 1, seed=cin + 5 * cout)
+    x = torch.randn(3, cin, H, W, generator=torch.Generator().manual_seed(11))
+    want = ref_conv(x, conv, bn, "silu")
+    X = nhwc(x, dtype)
+    ran = 0
+    for tid in range(97, 105):
+        try:
+            y = run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid)
+        except NotImplementedError as e:
+            assert "multiple" in str(e), e
+            continue
+        close(y.permute(0, 3, 1, 2), want, dtype)
+        ran += 1
+    assert ran >= 3
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_dense_pointwise_two_sources_slice_dst(dtype):
+    """conv_pwf over cat([a, b]) (split on a 64-channel stage boundary) into a channel
+    slice of a wider output buffer (the CSP concat)."""
+    a = torch.randn(2, 64, 9, 11)
+    b = torch.randn(2, 128, 9, 11)
+    conv, bn = make_conv(192, 96, 1, 1, seed=13)
+    want = ref_conv(torch.cat([a, b], 1), conv, bn, "silu")
+    A, Bt = nhwc(a, dtype), nhwc(b, dtype)
+    for tid in (99, 100, 101, 102):
+        out = torch.zeros(2, 9, 11, 160, dtype=dtype, device=DEV)
+        run_conv([(A, 0, 64, 0), (Bt, 0, 128, 0)], conv, bn, dtype, out=out, out_coff=32, tile=2 * tid)
+        close(out[..., 32:128].permute(0, 3, 1, 2), want, dtype)
+        assert out[..., :32].abs().max().item() == 0 and out[..., 128:].abs().max().item() == 0
+
+
+R3_GEOMS = [  # cin, cout, s, H, W (input)
+    (64, 96, 1, 11, 13), (32, 64, 1, 83, 41), (128, 64, 1, 20, 20), (64, 128, 2, 40, 40), (32, 48, 2, 17, 35),
+    (256, 256, 1, 10, 10), (128, 256, 2, 21, 19)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("geom", R3_GEOMS)
+def test_conv_r3_3x3(dtype, geom):
+    """conv_r3 (ids 113-124): every tile of the matching stride vs the fp32 reference;
+    zero padding comes from the buffer descriptor's range check (image borders, partial
+    spatial tiles, channel tails of cout)."""
+    cin, cout, s, H, W = geom
+    conv, bn = make_conv(cin, cout, 3, s, seed=cin + cout + 7)
+    x = torch.randn(2, cin, H, W, generator=torch.Generator().manual_seed(s + 3))
+    want = ref_conv(x, conv, bn, "silu")
+    X = nhwc(x, dtype)
+    ran = 0
+    for tid in range(113, 125):
+        try:
+            y = run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid)
+        except NotImplementedError as e:
+            assert "stride" in str(e) or "multiple" in str(e), e
+            continue
+        close(y.permute(0, 3, 1, 2), want, dtype)
+        ran += 1
+    assert ran >= 3
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16])
+def test_conv_r3_residual_and_strided_dst(dtype):
+    conv, bn = make_conv(64, 64, 3, 1, seed=3)
+    x = torch.randn(2, 64, 20, 20, generator=torch.Generator().manual_seed(4))
+    r = torch.randn(2, 64, 20, 20, generator=torch.Generator().manual_seed(5))
+    want = ref_conv(x, conv, bn, "silu") + r.to(dtype).float()
+    buf = torch.zeros(2, 20, 20, 128, dtype=dtype, device=DEV)
+    for tid in (113, 114, 118, 120):
+        buf[..., 64:] = nhwc(r, dtype)
+        y = run_conv([(nhwc(x, dtype), 0, 64, 0)], conv, bn, dtype, residual=(buf, 64), out=buf, out_coff=64,
+                     tile=2 * tid)
+        close(y[..., 64:].permute(0, 3, 1, 2), want, dtype)
