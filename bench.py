@@ -202,7 +202,8 @@ def layer_table(plan, iters=5):
             rows.append((i, f"conv k{a['k']}s{a['stride']} {a['cin']}->{a['cout']} @{a['out_h']}x{a['out_w']}",
                          tot[i], flop / tot[i] / 1e9, byt / tot[i] / 1e6))
         else:
-            rows.append((i, {N.OP_FOCUS: "focus", N.OP_SPP: "spp", N.OP_STEM: "stem (focus+conv)"}[rec.kind], tot[i],
+            rows.append((i, {N.OP_FOCUS: "focus", N.OP_SPP: "spp", N.OP_STEM: "stem (focus+conv)",
+                             N.OP_HEAD: f"head preds+decode @{a.get('h')}x{a.get('w')}"}[rec.kind], tot[i],
                          0.0, 0.0))
     print(f"{'op':>3} {'layer':<40} {'ms':>8} {'TFLOP/s':>9} {'GB/s':>8}", file=sys.stderr)
     for r in rows:

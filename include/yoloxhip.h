@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 7
+#define YXH_ABI_VERSION 8
 
 enum yxh_status {
     YXH_OK = 0,
@@ -329,7 +329,7 @@ int yxh_yolox_loss_bwd(const float* preds, const float* raw, const float* labels
  * captured once into a hipGraph and replayed (the MI355X replacement for the
  * reference's eager per-module dispatch).
  */
-enum yxh_op_kind { YXH_OP_CONV = 0, YXH_OP_FOCUS = 1, YXH_OP_SPP = 2, YXH_OP_STEM = 3 };
+enum yxh_op_kind { YXH_OP_CONV = 0, YXH_OP_FOCUS = 1, YXH_OP_SPP = 2, YXH_OP_STEM = 3, YXH_OP_HEAD = 4 };
 typedef struct {
     const void* img;
     int32_t layout, img_dtype, batch, h, w, dst_dtype;
@@ -340,6 +340,27 @@ typedef struct {
     int32_t dtype, batch, h, w, c, cstride;
     int64_t bstride;
 } yxh_spp_desc;
+/* One head level's reg_preds + obj_preds + cls_preds (1x1, with bias) + cat + sigmoid +
+ * decode (yolo_head.py:149-160, 185-187, 205-207, 233-251) in one launch: rows
+ * [a_off, a_off + h*w) of every image of the fp32 [B, A, 5+C] output (out_bstride =
+ * A*(5+C)).  w_reg [5][cin] (reg 4 + obj 1) / w_cls [C][cin] in `dtype`, fp32 biases.
+ * train != 0: obj/cls stay logits (get_output_and_grid, :213-231). */
+typedef struct {
+    int32_t dtype, batch, h, w, cin, num_classes;
+    yxh_src reg, cls;
+    const void* w_reg;
+    const float* b_reg;
+    const void* w_cls;
+    const float* b_cls;
+    float* out;
+    int64_t out_bstride;
+    int32_t a_off;
+    float stride;
+    int32_t train;
+    int32_t reserved;
+} yxh_head_desc;
+int yxh_head_pred(const yxh_head_desc* d, void* stream);
+
 typedef struct {
     int32_t kind;
     int32_t reserved;
@@ -348,6 +369,7 @@ typedef struct {
         yxh_focus_desc focus;
         yxh_spp_desc spp;
         yxh_stem_desc stem;
+        yxh_head_desc head;
     } u;
 } yxh_op;
 

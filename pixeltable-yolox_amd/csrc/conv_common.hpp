@@ -204,7 +204,7 @@ __device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&a
         __syncthreads();
         constexpr int CPO = TN * OES / 16;  // 16-byte chunks per output row
         const int ncols = min(TN, p.cout - n0) * OES / 16;
-        for (int q = tid; q < TM * CPO; q += 256) {
+        for (int q = tid; q < TM * CPO; q += 64 * WR * WC) {
             const int r = q / CPO, c = q - r * CPO;
             const int m = map(r);
             if (m < 0 || c >= ncols) continue;
@@ -263,6 +263,6 @@ int conv_pwf_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumPwfTiles = 8;
 // 3x3 conv with the branch-free buffer-LDS loader (conv_r3.hip): tile ids 113..112+kNumR3Tiles
 int conv_r3_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
-constexpr int kNumR3Tiles = 12;
+constexpr int kNumR3Tiles = 32;  // ids beyond the built ones report EINVAL
 
 }  // namespace yxh

@@ -74,10 +74,17 @@ constexpr uint32_t kR3Oob = 0x80000000u;  // beyond any descriptor range: reads 
 
 }  // namespace
 
-template <typename T, int S, int TX, int TY, int CH, int TN>
-__global__ __launch_bounds__(256) void conv_r3(ConvParams p, int tiles_x, int tiles_y, int ntn) {
-    constexpr int NBUF = 3;  // = the 3 kernel rows: ring slot of stage (cb, ky) is ky
-    constexpr int WN = TN / 64, WM = 4 / WN;
+// NBUF = 3: the ring slot of stage (cb, ky) is ky, two stages in flight;
+// NBUF = 2: slot (3 cb + ky) & 1, one stage in flight, 2/3 of the LDS (more blocks per CU);
+// waves whose share of a stage's 1 KiB wave-loads runs out skip the instruction (the
+// waits are vmcnt(0)), so the stage is exactly its A + B bytes.
+// NW waves per block (4 or 8); an 8-wave block is held to 128 registers per lane so two
+// blocks (4 waves per SIMD) fit a CU.
+template <typename T, int S, int TX, int TY, int CH, int TN, int NBUF, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 1) void conv_r3(ConvParams p, int tiles_x, int tiles_y, int ntn) {
+    static_assert(NBUF == 2 || NBUF == 3, "ring depth");
+    static_assert(NW == 4 || NW == 8, "waves per block");
+    constexpr int WN = TN / 64, WM = NW / WN;
     constexpr int EPC = Chunk<T>::N;
     constexpr int ES = sizeof(T);
     constexpr int KS = CH / 4;  // 64-byte slabs (one MFMA K step) per stage
@@ -86,11 +93,14 @@ __global__ __launch_bounds__(256) void conv_r3(ConvParams p, int tiles_x, int ti
     constexpr int FR = 4, FC = WTM / 16;
     constexpr int HX = (TX - 1) * S + 3;
     constexpr int A_SLOTS = 3 * TN * CH, B_SLOTS = TY * HX * CH;
-    constexpr int GA = A_SLOTS / 256, GB = (B_SLOTS + 255) / 256;
-    constexpr int G = GA + GB;  // DMA instructions per wave per stage
-    constexpr int BUF = G * 256 * 16;
+    constexpr int A_LOADS = A_SLOTS / 64, B_LOADS = (B_SLOTS + 63) / 64;  // 1 KiB wave-loads
+    constexpr int GA = (A_LOADS + NW - 1) / NW, GB = (B_LOADS + NW - 1) / NW;
+    constexpr int G = GA + GB;  // DMA instructions per wave per stage (at most)
+    constexpr bool EXACT = NBUF == 2;
+    constexpr int A_BYTES = (EXACT ? A_LOADS : GA * NW) * 1024;
+    constexpr int BUF = A_BYTES + (EXACT ? B_LOADS : GB * NW) * 1024;
     constexpr int PXG = 16 / CH;
-    static_assert(A_SLOTS % 256 == 0, "weight slots: whole waves");
+    static_assert(A_SLOTS % 64 == 0, "weight slots: whole wave-loads");
     static_assert(TM % (16 * WM) == 0, "pixel tile must split into 16-pixel fragments per wave");
     static_assert(G <= 20, "vmcnt range");
     __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
@@ -117,16 +127,16 @@ __global__ __launch_bounds__(256) void conv_r3(ConvParams p, int tiles_x, int ti
     uint32_t aoff[GA];
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
-        const int s = 64 * (wave + 4 * i) + lane;
+        const int s = 64 * (wave + NW * i) + lane;
         const int kx = s / (CH * TN), rem = s - kx * (CH * TN);
         const int c = rem / TN, rp = rem - c * TN;
         const int n = min(n0 + (rp ^ (2 * (c & 3) + (c >> 2))), p.cout - 1);
-        aoff[i] = (uint32_t)(((n * 9 + kx) * cin + c * EPC) * ES);
+        aoff[i] = s < A_SLOTS ? (uint32_t)(((n * 9 + kx) * cin + c * EPC) * ES) : kR3Oob;
     }
     uint32_t boff[GB][3];  // per kernel row ky
 #pragma unroll
     for (int i = 0; i < GB; ++i) {
-        const int sb = 64 * (wave + 4 * i) + lane;
+        const int sb = 64 * (wave + NW * i) + lane;
         const int hp = sb / CH, cp = sb - hp * CH;
         const int c = cp ^ ((hp / PXG) & (CH - 1));
         const int ty = hp / HX, hx = hp - ty * HX;
@@ -140,15 +150,20 @@ __global__ __launch_bounds__(256) void conv_r3(ConvParams p, int tiles_x, int ti
     }
     const uint32_t lds0 = r3_lds_addr(smem) + (uint32_t)wave * 1024;
 
-    auto issue = [&](int cb, auto kyc) {
+    auto issue_to = [&](int cb, auto kyc, uint32_t slot) {
         constexpr int ky = decltype(kyc)::value;
-        const uint32_t base = lds0 + ky * BUF;
+        const uint32_t base = lds0 + slot * BUF;
         const uint32_t soa = (uint32_t)((ky * 3 * cin + cb * KST) * ES), sob = (uint32_t)(cb * KST * ES);
 #pragma unroll
-        for (int i = 0; i < GA; ++i) r3_dma(wsrd, aoff[i], soa, base + i * 4096);
+        for (int i = 0; i < GA; ++i)
+            if (!EXACT || A_LOADS % NW == 0 || i + 1 < GA || wave + NW * i < A_LOADS)
+                r3_dma(wsrd, aoff[i], soa, base + i * NW * 1024);
 #pragma unroll
-        for (int i = 0; i < GB; ++i) r3_dma(xsrd, boff[i][ky], sob, base + GA * 4096 + i * 4096);
+        for (int i = 0; i < GB; ++i)
+            if (!EXACT || B_LOADS % NW == 0 || i + 1 < GB || wave + NW * i < B_LOADS)
+                r3_dma(xsrd, boff[i][ky], sob, base + A_BYTES + i * NW * 1024);
     };
+    auto issue = [&](int cb, auto kyc) { issue_to(cb, kyc, (uint32_t)decltype(kyc)::value); };
 
     f32x4 acc[FR][FC];
 #pragma unroll
@@ -169,7 +184,7 @@ __global__ __launch_bounds__(256) void conv_r3(ConvParams p, int tiles_x, int ti
 
     auto compute = [&](int slot) {
         const char* A = smem + slot * BUF;
-        const char* B = A + GA * 4096;
+        const char* B = A + A_BYTES;
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
 #pragma unroll
@@ -198,25 +213,46 @@ __global__ __launch_bounds__(256) void conv_r3(ConvParams p, int tiles_x, int ti
     using K1 = std::integral_constant<int, 1>;
     using K2 = std::integral_constant<int, 2>;
     const int ncb = p.ncb;
-    issue(0, K0{});
-    issue(0, K1{});
-    // stage (cb, ky): wait for it (one younger stage may fly), barrier, issue the stage
-    // two ahead into the slot stage (cb, ky-1) just vacated, compute
-    for (int cb = 0; cb < ncb; ++cb) {
-        const bool more = cb + 1 < ncb;
-        r3_wait_vm<G>();
-        r3_barrier();
-        issue(cb, K2{});
-        compute(0);
-        r3_wait_vm<G>();
-        r3_barrier();
-        if (more) issue(cb + 1, K0{});
-        compute(1);
-        if (more) r3_wait_vm<G>();
-        else r3_wait_vm<0>();
-        r3_barrier();
-        if (more) issue(cb + 1, K1{});
-        compute(2);
+    if constexpr (NBUF == 3) {
+        issue(0, K0{});
+        issue(0, K1{});
+        // stage (cb, ky): wait for it (one younger stage may fly), barrier, issue the stage
+        // two ahead into the slot stage (cb, ky-1) just vacated, compute
+        for (int cb = 0; cb < ncb; ++cb) {
+            const bool more = cb + 1 < ncb;
+            r3_wait_vm<G>();
+            r3_barrier();
+            issue(cb, K2{});
+            compute(0);
+            r3_wait_vm<G>();
+            r3_barrier();
+            if (more) issue(cb + 1, K0{});
+            compute(1);
+            if (more) r3_wait_vm<G>();
+            else r3_wait_vm<0>();
+            r3_barrier();
+            if (more) issue(cb + 1, K1{});
+            compute(2);
+        }
+    } else {
+        // stage s = 3 cb + ky in slot s & 1: wait for it, barrier (every wave is done with
+        // stage s - 1, whose slot the next stage takes), issue stage s + 1, compute
+        issue_to(0, K0{}, 0u);
+        for (int cb = 0; cb < ncb; ++cb) {
+            const uint32_t s0 = (uint32_t)(3 * cb) & 1u;
+            r3_wait_vm<0>();
+            r3_barrier();
+            issue_to(cb, K1{}, s0 ^ 1u);
+            compute((int)s0);
+            r3_wait_vm<0>();
+            r3_barrier();
+            issue_to(cb, K2{}, s0);
+            compute((int)(s0 ^ 1u));
+            r3_wait_vm<0>();
+            r3_barrier();
+            if (cb + 1 < ncb) issue_to(cb + 1, K0{}, s0 ^ 1u);
+            compute((int)s0);
+        }
     }
     r3_wait_vm<0>();
     r3_barrier();
@@ -231,11 +267,12 @@ __global__ __launch_bounds__(256) void conv_r3(ConvParams p, int tiles_x, int ti
         n0, lbias);
 }
 
-template <typename T, int S, int TX, int TY, int CH, int TN>
+template <typename T, int S, int TX, int TY, int CH, int TN, int NBUF = 3, int NW = 4>
 static int launch_r3(const ConvParams& p, hipStream_t st) {
     constexpr int HX = (TX - 1) * S + 3;
-    constexpr int G = 3 * TN * CH / 256 + (TY * HX * CH + 255) / 256;
-    constexpr int lds = 3 * G * 256 * 16;
+    constexpr int AL = 3 * TN * CH / 64, BL = (TY * HX * CH + 63) / 64;
+    constexpr int G = (AL + NW - 1) / NW + (BL + NW - 1) / NW;
+    constexpr int lds = NBUF * (NBUF == 2 ? AL + BL : G * NW) * 1024;
     if constexpr (lds > 160 * 1024 || G > 20) {
         set_error("conv_r3 variant needs more than 160 KiB of LDS");
         return YXH_EUNSUPPORTED;
@@ -258,7 +295,7 @@ static int launch_r3(const ConvParams& p, hipStream_t st) {
             set_error("conv_r3 grid too large");
             return YXH_EINVAL;
         }
-        hipLaunchKernelGGL((conv_r3<T, S, TX, TY, CH, TN>), dim3((unsigned)nblk), dim3(256), 0, st, q, tiles_x,
+        hipLaunchKernelGGL((conv_r3<T, S, TX, TY, CH, TN, NBUF, NW>), dim3((unsigned)nblk), dim3(64 * NW), 0, st, q, tiles_x,
                            tiles_y, ntn);
         YXH_CHECK_LAUNCH("conv_r3 launch");
         return YXH_OK;
@@ -281,6 +318,29 @@ static int r3_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 10: return launch_r3<T, 2, 8, 8, 4, 128>(p, st);
         case 11: return launch_r3<T, 2, 16, 4, 4, 128>(p, st);
         case 12: return launch_r3<T, 2, 20, 8, 4, 128>(p, st);
+        // 72 KiB of LDS: two blocks (8 waves) per CU
+        case 13: return launch_r3<T, 1, 16, 8, 4, 64>(p, st);
+        case 14: return launch_r3<T, 1, 32, 4, 4, 64>(p, st);
+        case 15: return launch_r3<T, 2, 16, 4, 4, 64>(p, st);
+        case 16: return launch_r3<T, 2, 8, 8, 4, 64>(p, st);
+        // two-slot ring (one stage in flight): 48 KiB -> three blocks per CU, 64-72 KiB -> two
+        case 17: return launch_r3<T, 1, 16, 8, 4, 64, 2>(p, st);
+        case 18: return launch_r3<T, 1, 32, 4, 4, 64, 2>(p, st);
+        case 19: return launch_r3<T, 1, 32, 8, 4, 64, 2>(p, st);
+        case 20: return launch_r3<T, 1, 16, 16, 4, 64, 2>(p, st);
+        case 21: return launch_r3<T, 1, 16, 8, 4, 128, 2>(p, st);
+        case 22: return launch_r3<T, 2, 16, 4, 4, 64, 2>(p, st);
+        case 23: return launch_r3<T, 2, 8, 8, 4, 64, 2>(p, st);
+        case 24: return launch_r3<T, 2, 16, 8, 4, 64, 2>(p, st);
+        // 8-wave blocks, two per CU
+        case 25: return launch_r3<T, 1, 16, 16, 4, 64, 2, 8>(p, st);
+        case 26: return launch_r3<T, 1, 32, 8, 4, 64, 2, 8>(p, st);
+        case 27: return launch_r3<T, 1, 16, 8, 4, 128, 2, 8>(p, st);
+        case 28: return launch_r3<T, 1, 8, 8, 4, 128, 2, 8>(p, st);
+        case 29: return launch_r3<T, 2, 8, 8, 4, 128, 2, 8>(p, st);
+        case 30: return launch_r3<T, 2, 16, 8, 4, 64, 2, 8>(p, st);
+        case 31: return launch_r3<T, 1, 16, 8, 4, 64, 2, 8>(p, st);
+        case 32: return launch_r3<T, 2, 8, 16, 4, 64, 2, 8>(p, st);
         default: set_error("conv_r3 tile id %d", id); return YXH_EINVAL;
     }
 }

@@ -1,0 +1,213 @@
+// head_pred: the three 1x1 pred convs of one YOLOX head level + cat + sigmoid + decode
+// in ONE kernel (reference yolo_head.py:149-160 reg_preds / obj_preds / cls_preds,
+// :185-187 cat([reg, obj.sigmoid(), cls.sigmoid()]), :205-207 flatten/permute,
+// :233-251 decode_outputs), writing the level's rows of the [B, A, 5+C] fp32 output.
+//
+// Persistent blocks (weights loaded into LDS once) walk tiles of TM = 64 consecutive
+// pixels m (image-major) of the level:
+//  * the reg_feat and cls_feat tiles [64][cin] and both weight matrices ([5][cin] reg+obj,
+//    [C][cin] cls, zero rows up to whole 16-row fragments) are staged in LDS (XOR-swizzled);
+//  * wave w computes pixel fragment w (16 pixels) x every output-channel fragment
+//    (1 reg/obj + ceil(C/16) cls) on MFMA 16x16x32 -- no block-diagonal zero work;
+//  * bias + decode in registers: ch 0-1 (v + grid) * stride, ch 2-3 exp(v) * stride,
+//    ch 4.. sigmoid (IEEE expf / divide, as the fp32 path of conv_common.hpp);
+//  * the decoded [64][5+C] tile is staged in LDS and leaves as 16-byte stores over the
+//    contiguous output rows (a level's rows of one image are consecutive; a tile
+//    straddles at most one image boundary) -- instead of 4-byte scattered stores of
+//    340-byte rows.
+#include "conv_common.hpp"
+
+namespace yxh {
+
+namespace {
+
+__device__ __forceinline__ float hd_sigmoid(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+}  // namespace
+
+// CIN: feature channels (a multiple of 32); NCF: cls output fragments (16 rows each)
+template <typename T, int CIN, int NCF>
+__global__ __launch_bounds__(256) void head_pred(yxh_head_desc d) {
+    constexpr int TM = 64;
+    constexpr int EPC = Chunk<T>::N;
+    constexpr int CPR = CIN / EPC;        // 16-byte chunks per row
+    constexpr int ROWB = CIN * sizeof(T);
+    constexpr int NF = 1 + NCF;           // output-channel fragments
+    constexpr int WROWS = NF * 16;        // weight rows in LDS
+    constexpr int XB = TM * ROWB;         // one feature tile
+    constexpr int WB = WROWS * ROWB;
+    constexpr int D = 5 + NCF * 16;       // staged row: 5 + C rounded up (C <= NCF * 16)
+    constexpr int STG = TM * D * 4;
+    __shared__ __attribute__((aligned(16))) char smem[2 * XB + WB + STG];
+    char* xr = smem;            // reg_feat tile [TM][CIN] (chunks XOR-swizzled by row)
+    char* xc = smem + XB;       // cls_feat tile
+    char* wl = smem + 2 * XB;   // weights [WROWS][CIN]: row 0-4 reg+obj, 16.. cls
+    float* stg = (float*)(smem + 2 * XB + WB);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int C = d.num_classes, hw = d.h * d.w;
+    const int M = d.batch * hw;
+    const int ntiles = (M + TM - 1) / TM;
+    auto swz = [](int r, int c) { return c ^ (r & (CPR - 1)); };
+
+    // weights once per block (the grid is persistent over pixel tiles)
+    for (int q = tid; q < WROWS * CPR; q += 256) {
+        const int r = q / CPR, c = q - r * CPR;
+        const int cs = swz(r, c);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (r < 5)
+            v = *(const uint4*)((const T*)d.w_reg + (long long)r * CIN + cs * EPC);
+        else if (r >= 16 && r - 16 < C)
+            v = *(const uint4*)((const T*)d.w_cls + (long long)(r - 16) * CIN + cs * EPC);
+        *(uint4*)(wl + q * 16) = v;
+    }
+    const int frow = lane & 15, fq = lane >> 4;
+    const int rowf = 5 + C;
+
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int m0 = tile * TM;
+        const int b0 = m0 / hw, p0 = m0 - b0 * hw;
+        // ---- feature tiles -> LDS (chunk c of row r stored at c ^ (r & (CPR - 1))): all
+        // loads of the tile issued before any LDS store
+        constexpr int NQ = TM * CPR / 256;  // 16-byte chunks per thread per tensor
+        uint4 vr[NQ], vc[NQ];
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            const int q = tid + 256 * k;
+            const int r = q / CPR, c = q - r * CPR;
+            int pix = p0 + min(r, M - 1 - m0), b = b0;
+            while (pix >= hw) {
+                pix -= hw;
+                ++b;
+            }
+            const int cs = swz(r, c);
+            vr[k] = *(const uint4*)((const T*)d.reg.ptr + (long long)b * d.reg.bstride + (long long)pix * d.reg.cstride +
+                                    cs * EPC);
+            vc[k] = *(const uint4*)((const T*)d.cls.ptr + (long long)b * d.cls.bstride + (long long)pix * d.cls.cstride +
+                                    cs * EPC);
+        }
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            const int q = tid + 256 * k;
+            *(uint4*)(xr + q * 16) = vr[k];
+            *(uint4*)(xc + q * 16) = vc[k];
+        }
+        __syncthreads();
+
+        // ---- MFMA: out[ch][pix], wave = pixel fragment
+        f32x4 acc[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int pr = wave * 16 + frow;  // tile pixel of this lane's B fragment
+#pragma unroll
+        for (int s = 0; s < CIN / 32; ++s) {
+            const int ch = s * 4 + fq;
+            const uint4 br = *(const uint4*)(xr + (pr * CPR + swz(pr, ch)) * 16);
+            const uint4 bc = *(const uint4*)(xc + (pr * CPR + swz(pr, ch)) * 16);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int wr = f * 16 + frow;
+                const uint4 a = *(const uint4*)(wl + (wr * CPR + swz(wr, ch)) * 16);
+                Mma<T>::run(acc[f], a, f == 0 ? br : bc);
+            }
+        }
+
+        // ---- bias + decode -> staged fp32 rows
+        {
+            int pix = p0 + min(pr, M - 1 - m0);
+            while (pix >= hw) pix -= hw;
+            const int gy = pix / d.w, gx = pix - gy * d.w;
+            const float st = d.stride;
+            float* row = stg + pr * D;
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int ch = f * 16 + fq * 4 + r;  // fragment row
+                    float v = acc[f][r];
+                    if (f == 0) {
+                        if (ch < 5) {
+                            v += d.b_reg[ch];
+                            if (ch < 2) v = (v + (float)(ch == 0 ? gx : gy)) * st;
+                            else if (ch < 4) v = expf(v) * st;
+                            else v = d.train ? v : hd_sigmoid(v);
+                            row[ch] = v;
+                        }
+                    } else {
+                        const int c = ch - 16;
+                        if (c < C) {
+                            v += d.b_cls[c];
+                            row[5 + c] = d.train ? v : hd_sigmoid(v);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- coalesced copy of the tile's rows: [m0, m0 + n) splits at image boundaries;
+        // each piece is contiguous in the output and 16-byte aligned
+        const int n = min(TM, M - m0);
+        int t0 = 0, b = b0, pix = p0;
+        while (t0 < n) {
+            const int cnt = min(n - t0, hw - pix);
+            float* dst = d.out + (long long)b * d.out_bstride + (long long)(d.a_off + pix) * rowf;
+            const int total = cnt * rowf;  // floats, a multiple of 4 (cnt % 4 == 0)
+            for (int q = tid * 4; q < total; q += 1024) {
+                const int r = q / rowf, c = q - r * rowf;  // staged layout has row stride D
+                float4 v;
+                float* pv = (float*)&v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    int rr = r, cc = c + e;
+                    if (cc >= rowf) {
+                        cc -= rowf;
+                        ++rr;
+                    }
+                    pv[e] = stg[(t0 + rr) * D + cc];
+                }
+                *(float4*)(dst + q) = v;
+            }
+            t0 += cnt;
+            ++b;
+            pix = 0;
+        }
+        __syncthreads();  // staging and feature tiles are reused by the next tile
+    }
+}
+
+int head_pred_launch(const yxh_head_desc* d, hipStream_t st) {
+    YXH_CHECK_ARG(d && d->out && d->cls.ptr && d->reg.ptr && d->w_reg && d->w_cls && d->b_reg && d->b_cls,
+                  "head_pred: null pointer");
+    YXH_CHECK_ARG(d->batch > 0 && d->h > 0 && d->w > 0, "head_pred: empty level");
+    YXH_CHECK_ARG(((long long)d->h * d->w) % 4 == 0 && d->a_off % 4 == 0 && d->out_bstride % 4 == 0 &&
+                      ((uintptr_t)d->out & 15) == 0,
+                  "head_pred: level rows must be 16-byte aligned (h*w, a_off multiples of 4)");
+    YXH_CHECK_ARG(d->reg.channels == d->cin && d->cls.channels == d->cin, "head_pred: feature channels");
+    const long long M = (long long)d->batch * d->h * d->w;
+    YXH_CHECK_ARG(M < (1LL << 31), "head_pred: too many pixels");
+    const long long tiles = (M + 63) / 64;
+    const unsigned grid = (unsigned)(tiles < 512 ? tiles : 512);  // persistent: weights loaded once per block
+#define YXH_HEAD(T, CIN, NCF) \
+    hipLaunchKernelGGL((head_pred<T, CIN, NCF>), dim3(grid), dim3(256), 0, st, *d)
+    const int ncf = (d->num_classes + 15) / 16;
+    if (ncf != 5) {
+        set_error("head_pred built for 65-80 classes (got %d)", d->num_classes);
+        return YXH_EUNSUPPORTED;
+    }
+    if (d->dtype == YXH_BF16 && d->cin == 128) YXH_HEAD(bf16, 128, 5);
+    else if (d->dtype == YXH_BF16 && d->cin == 64) YXH_HEAD(bf16, 64, 5);
+    else if (d->dtype == YXH_BF16 && d->cin == 256) YXH_HEAD(bf16, 256, 5);
+    else if (d->dtype == YXH_F16 && d->cin == 128) YXH_HEAD(f16, 128, 5);
+    else if (d->dtype == YXH_F16 && d->cin == 64) YXH_HEAD(f16, 64, 5);
+    else if (d->dtype == YXH_F16 && d->cin == 256) YXH_HEAD(f16, 256, 5);
+    else {
+        set_error("head_pred: dtype %d / %d channels not built", d->dtype, d->cin);
+        return YXH_EUNSUPPORTED;
+    }
+#undef YXH_HEAD
+    YXH_CHECK_LAUNCH("head_pred launch");
+    return YXH_OK;
+}
+
+}  // namespace yxh

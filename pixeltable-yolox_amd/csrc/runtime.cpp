@@ -64,6 +64,7 @@ int yolox_loss_bwd(const float* preds, const float* raw, const float* labels, in
                    void* g_cls, hipStream_t st);
 int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
                 float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st);
+int head_pred_launch(const yxh_head_desc* d, hipStream_t st);
 
 static int run_op(const yxh_op& op, hipStream_t st) {
     switch (op.kind) {
@@ -75,6 +76,8 @@ static int run_op(const yxh_op& op, hipStream_t st) {
         }
         case YXH_OP_STEM:
             return stem_launch(&op.u.stem, st);
+        case YXH_OP_HEAD:
+            return head_pred_launch(&op.u.head, st);
         case YXH_OP_SPP: {
             const yxh_spp_desc& s = op.u.spp;
             return spp_launch(s.buf, s.dtype, s.batch, s.h, s.w, s.c, s.cstride, s.bstride, st);
@@ -97,6 +100,8 @@ size_t yxh_sizeof_op(void) { return sizeof(yxh_op); }
 size_t yxh_sizeof_conv_desc(void) { return sizeof(yxh_conv_desc); }
 
 int yxh_conv2d(const yxh_conv_desc* d, void* stream) { return conv2d(d, (hipStream_t)stream); }
+
+int yxh_head_pred(const yxh_head_desc* d, void* stream) { return head_pred_launch(d, (hipStream_t)stream); }
 
 int yxh_focus_pack(const void* img, int32_t layout, int32_t img_dtype, int32_t batch, int32_t h, int32_t w,
                    void* dst, int32_t dst_dtype, void* stream) {

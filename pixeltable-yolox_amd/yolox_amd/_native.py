@@ -17,14 +17,14 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
 F32, BF16, F16, U8 = 0, 1, 2, 3
 ACT_NONE, ACT_SILU, ACT_RELU, ACT_LRELU, ACT_DECODE, ACT_DECODE_TRAIN = range(6)
 NCHW, NHWC = 0, 1
-OP_CONV, OP_FOCUS, OP_SPP, OP_STEM = 0, 1, 2, 3
+OP_CONV, OP_FOCUS, OP_SPP, OP_STEM, OP_HEAD = 0, 1, 2, 3, 4
 LB_F32_NCHW, LB_U8_NHWC, LB_BF16_NHWC = 0, 1, 2
 
 TORCH_DTYPE = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16, U8: torch.uint8}
@@ -101,8 +101,15 @@ class StemDesc(C.Structure):
                 ("reserved", C.c_int32), ("dst_bstride", C.c_int64)]
 
 
+class HeadDesc(C.Structure):
+    _fields_ = [("dtype", C.c_int32), ("batch", C.c_int32), ("h", C.c_int32), ("w", C.c_int32), ("cin", C.c_int32),
+                ("num_classes", C.c_int32), ("reg", Src), ("cls", Src), ("w_reg", C.c_void_p), ("b_reg", C.c_void_p),
+                ("w_cls", C.c_void_p), ("b_cls", C.c_void_p), ("out", C.c_void_p), ("out_bstride", C.c_int64),
+                ("a_off", C.c_int32), ("stride", C.c_float), ("train", C.c_int32), ("reserved", C.c_int32)]
+
+
 class _OpU(C.Union):
-    _fields_ = [("conv", ConvDesc), ("focus", FocusDesc), ("spp", SppDesc), ("stem", StemDesc)]
+    _fields_ = [("conv", ConvDesc), ("focus", FocusDesc), ("spp", SppDesc), ("stem", StemDesc), ("head", HeadDesc)]
 
 
 class Op(C.Structure):
@@ -138,6 +145,7 @@ def lib():
             "yxh_sizeof_op": ([], sz),
             "yxh_sizeof_conv_desc": ([], sz),
             "yxh_conv2d": ([C.POINTER(ConvDesc), vp], C.c_int),
+            "yxh_head_pred": ([C.POINTER(HeadDesc), vp], C.c_int),
             "yxh_focus_pack": ([vp, i32, i32, i32, i32, i32, vp, i32, vp], C.c_int),
             "yxh_spp_maxpool": ([vp, i32, i32, i32, i32, i32, i32, i64, vp], C.c_int),
             "yxh_stem_conv": ([C.POINTER(StemDesc), vp], C.c_int),
@@ -188,7 +196,7 @@ def lib():
     return _lib
 
 
-EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d",
+EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d", "yxh_head_pred",
             "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_postprocess_workspace_bytes",
             "yxh_postprocess", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",

@@ -213,6 +213,18 @@ class PlanCtx:
                    stride: int, train: bool) -> None:
         act = N.ACT_DECODE_TRAIN if train else N.ACT_DECODE
         h, w = cls_feat.lh, cls_feat.lw
+        C = head.num_classes
+        if (self.dtype != torch.float32 and cls_feat.ch == reg_feat.ch and cls_feat.ch in (64, 128, 256)
+                and 65 <= C <= 80 and (h * w) % 4 == 0 and a_off % 4 == 0 and out.anchors % 4 == 0
+                and not cls_feat.up and not reg_feat.up):
+            # the three preds + cat + sigmoid + decode of the level as one launch (head.hip)
+            ro = self._weights([(head.reg_preds[k], None), (head.obj_preds[k], None)], reg_feat.ch)
+            cl = self._weights([(head.cls_preds[k], None)], cls_feat.ch)
+            self.ops.append(OpRec(N.OP_HEAD, dict(reg=reg_feat, cls=cls_feat, spec_ro=ro, spec_cls=cl,
+                                                  head_out=(out, a_off, 0), h=h, w=w, cin=cls_feat.ch,
+                                                  num_classes=C, stride=float(stride), train=int(train))))
+            self.flops += 2.0 * self.batch * h * w * (5 + C) * cls_feat.ch
+            return
         for convs, feat, coff in (([(head.reg_preds[k], None), (head.obj_preds[k], None)], reg_feat, 0),
                                   ([(head.cls_preds[k], None)], cls_feat, 5)):
             spec = self._weights(convs, feat.ch)
@@ -233,10 +245,10 @@ class OutBuffer:
 # tile codes (2 * id + slabs - 1); ids 1-9 register-staged conv_igemm, 17-25 the same
 # tiles on the LDS-DMA conv_glds kernel, 33-51 the row-tiled 3x3 conv_rows kernel,
 # 65-70 the persistent streaming 1x1 conv_pw kernel, 81-82 the register-operand 1x1
-# conv_pwr kernel, 97-104 the dense 1x1 conv_pwf kernel, 113-124 the 3x3 conv_r3 kernel
+# conv_pwr kernel, 97-104 the dense 1x1 conv_pwf kernel, 113-128 the 3x3 conv_r3 kernel
 # (yoloxhip.h yxh_conv_desc.tile)
 TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
-                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 125)]
+                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 145)]
 _TUNE_CACHE: dict = {}
 _TUNE_ALL = os.environ.get("YOLOX_AMD_TUNE_ALL", "0") == "1"  # print every variant's time
 
@@ -276,6 +288,8 @@ def op_dependencies(ops) -> list:
             reads, writes = [a["buf"]], [a["buf"]]
         elif r.kind in (N.OP_FOCUS, N.OP_STEM):
             reads, writes = [], [a["dst"].buf]
+        elif r.kind == N.OP_HEAD:
+            reads, writes = [a["reg"].buf, a["cls"].buf], []
         else:
             reads = [v.buf for v in a["srcs"]]
             if a.get("residual") is not None:
@@ -379,7 +393,7 @@ class Plan:
         out_base = out_ptr + c * B * self.anchors * self.out_spec.row * 4
         for i, rec in enumerate(ctx.ops):
             a = rec.args
-            if heads_only and not (rec.kind == N.OP_CONV and a["dst_f32"]):
+            if heads_only and not (rec.kind == N.OP_HEAD or (rec.kind == N.OP_CONV and a["dst_f32"])):
                 continue
             op = self._ops[c * self._nops + i]
             op.kind = rec.kind
@@ -405,6 +419,22 @@ class Plan:
                 t.dst_cstride, t.dst_bstride = v.buf.c, v.buf.nelem_image
                 t.img = None
                 self._input_index = i
+            elif rec.kind == N.OP_HEAD:
+                hd = op.u.head
+                hd.dtype, hd.batch, hd.h, hd.w = ctx.dcode, B, a["h"], a["w"]
+                hd.cin, hd.num_classes = a["cin"], a["num_classes"]
+                for dst, v in ((hd.reg, a["reg"]), (hd.cls, a["cls"])):
+                    dst.ptr = self._ptr(v)
+                    dst.channels, dst.cstride, dst.bstride = v.ch, v.buf.c, v.buf.nelem_image
+                    dst.h, dst.w, dst.upsample = v.buf.h, v.buf.w, 0
+                hd.w_reg = self.warena.data_ptr() + a["spec_ro"].w_off
+                hd.b_reg = self.barena.data_ptr() + a["spec_ro"].b_off
+                hd.w_cls = self.warena.data_ptr() + a["spec_cls"].w_off
+                hd.b_cls = self.barena.data_ptr() + a["spec_cls"].b_off
+                out, a_off, _ = a["head_out"]
+                hd.out = out_base
+                hd.out_bstride = out.anchors * out.row
+                hd.a_off, hd.stride, hd.train = a_off, a["stride"], a["train"]
             elif rec.kind == N.OP_SPP:
                 s = op.u.spp
                 buf: Buffer = a["buf"]
