@@ -75,13 +75,14 @@ constexpr uint32_t kR3Oob = 0x80000000u;  // beyond any descriptor range: reads 
 }  // namespace
 
 // NBUF = 3: the ring slot of stage (cb, ky) is ky, two stages in flight;
-// NBUF = 2: slot (3 cb + ky) & 1, one stage in flight, 2/3 of the LDS (more blocks per CU);
-// waves whose share of a stage's 1 KiB wave-loads runs out skip the instruction (the
-// waits are vmcnt(0)), so the stage is exactly its A + B bytes.
-// NW waves per block (4 or 8); an 8-wave block is held to 128 registers per lane so two
-// blocks (4 waves per SIMD) fit a CU.
-template <typename T, int S, int TX, int TY, int CH, int TN, int NBUF, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 1) void conv_r3(ConvParams p, int tiles_x, int tiles_y, int ntn) {
+// NBUF = 2: slot (3 cb + ky) & 1, one stage in flight, 2/3 of the LDS (more blocks per CU).
+// A stage is exactly its A + B bytes: its 1 KiB wave-loads are dealt round-robin over
+// the waves, and a wave whose share runs out skips the instruction (its counted vmcnt
+// waits use its own per-stage count).
+// NW waves per block (4 or 8); MINW = waves per SIMD the register budget must allow
+// (8-wave blocks: 4 = two blocks per CU).
+template <typename T, int S, int TX, int TY, int CH, int TN, int NBUF, int NW, int MINW>
+__global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles_x, int tiles_y, int ntn) {
     static_assert(NBUF == 2 || NBUF == 3, "ring depth");
     static_assert(NW == 4 || NW == 8, "waves per block");
     constexpr int WN = TN / 64, WM = NW / WN;
@@ -96,9 +97,9 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 1) void conv_r3(ConvParams p
     constexpr int A_LOADS = A_SLOTS / 64, B_LOADS = (B_SLOTS + 63) / 64;  // 1 KiB wave-loads
     constexpr int GA = (A_LOADS + NW - 1) / NW, GB = (B_LOADS + NW - 1) / NW;
     constexpr int G = GA + GB;  // DMA instructions per wave per stage (at most)
-    constexpr bool EXACT = NBUF == 2;
-    constexpr int A_BYTES = (EXACT ? A_LOADS : GA * NW) * 1024;
-    constexpr int BUF = A_BYTES + (EXACT ? B_LOADS : GB * NW) * 1024;
+    constexpr int A_PART = A_LOADS % NW, B_PART = B_LOADS % NW;  // waves in a partial last group
+    constexpr int A_BYTES = A_LOADS * 1024;
+    constexpr int BUF = A_BYTES + B_LOADS * 1024;
     constexpr int PXG = 16 / CH;
     static_assert(A_SLOTS % 64 == 0, "weight slots: whole wave-loads");
     static_assert(TM % (16 * WM) == 0, "pixel tile must split into 16-pixel fragments per wave");
@@ -156,11 +157,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 1) void conv_r3(ConvParams p
         const uint32_t soa = (uint32_t)((ky * 3 * cin + cb * KST) * ES), sob = (uint32_t)(cb * KST * ES);
 #pragma unroll
         for (int i = 0; i < GA; ++i)
-            if (!EXACT || A_LOADS % NW == 0 || i + 1 < GA || wave + NW * i < A_LOADS)
+            if (A_PART == 0 || i + 1 < GA || wave < A_PART)
                 r3_dma(wsrd, aoff[i], soa, base + i * NW * 1024);
 #pragma unroll
         for (int i = 0; i < GB; ++i)
-            if (!EXACT || B_LOADS % NW == 0 || i + 1 < GB || wave + NW * i < B_LOADS)
+            if (B_PART == 0 || i + 1 < GB || wave < B_PART)
                 r3_dma(xsrd, boff[i][ky], sob, base + A_BYTES + i * NW * 1024);
     };
     auto issue = [&](int cb, auto kyc) { issue_to(cb, kyc, (uint32_t)decltype(kyc)::value); };
@@ -213,6 +214,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 1) void conv_r3(ConvParams p
     using K1 = std::integral_constant<int, 1>;
     using K2 = std::integral_constant<int, 2>;
     const int ncb = p.ncb;
+    // this wave's DMA instructions per stage, and "wait until one younger stage remains"
+    const int cnt = G - (A_PART && wave >= A_PART ? 1 : 0) - (B_PART && wave >= B_PART ? 1 : 0);
+    auto wait_younger = [&]() {
+        if (cnt == G) r3_wait_vm<G>();
+        else if (cnt == G - 1) r3_wait_vm<G - 1>();
+        else r3_wait_vm<G - 2>();
+    };
     if constexpr (NBUF == 3) {
         issue(0, K0{});
         issue(0, K1{});
@@ -220,15 +228,15 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 1) void conv_r3(ConvParams p
         // two ahead into the slot stage (cb, ky-1) just vacated, compute
         for (int cb = 0; cb < ncb; ++cb) {
             const bool more = cb + 1 < ncb;
-            r3_wait_vm<G>();
+            wait_younger();
             r3_barrier();
             issue(cb, K2{});
             compute(0);
-            r3_wait_vm<G>();
+            wait_younger();
             r3_barrier();
             if (more) issue(cb + 1, K0{});
             compute(1);
-            if (more) r3_wait_vm<G>();
+            if (more) wait_younger();
             else r3_wait_vm<0>();
             r3_barrier();
             if (more) issue(cb + 1, K1{});
@@ -267,12 +275,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 1) void conv_r3(ConvParams p
         n0, lbias);
 }
 
-template <typename T, int S, int TX, int TY, int CH, int TN, int NBUF = 3, int NW = 4>
+template <typename T, int S, int TX, int TY, int CH, int TN, int NBUF = 3, int NW = 4, int MINW = NW == 8 ? 4 : 1>
 static int launch_r3(const ConvParams& p, hipStream_t st) {
     constexpr int HX = (TX - 1) * S + 3;
     constexpr int AL = 3 * TN * CH / 64, BL = (TY * HX * CH + 63) / 64;
     constexpr int G = (AL + NW - 1) / NW + (BL + NW - 1) / NW;
-    constexpr int lds = NBUF * (NBUF == 2 ? AL + BL : G * NW) * 1024;
+    constexpr int lds = NBUF * (AL + BL) * 1024;
     if constexpr (lds > 160 * 1024 || G > 20) {
         set_error("conv_r3 variant needs more than 160 KiB of LDS");
         return YXH_EUNSUPPORTED;
@@ -295,7 +303,7 @@ static int launch_r3(const ConvParams& p, hipStream_t st) {
             set_error("conv_r3 grid too large");
             return YXH_EINVAL;
         }
-        hipLaunchKernelGGL((conv_r3<T, S, TX, TY, CH, TN, NBUF, NW>), dim3((unsigned)nblk), dim3(64 * NW), 0, st, q, tiles_x,
+        hipLaunchKernelGGL((conv_r3<T, S, TX, TY, CH, TN, NBUF, NW, MINW>), dim3((unsigned)nblk), dim3(64 * NW), 0, st, q, tiles_x,
                            tiles_y, ntn);
         YXH_CHECK_LAUNCH("conv_r3 launch");
         return YXH_OK;
@@ -304,43 +312,41 @@ static int launch_r3(const ConvParams& p, hipStream_t st) {
 
 template <typename T>
 static int r3_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
-    // id -> (stride, TX, TY, CH, TN)
+    // id -> (stride, TX, TY, CH, TN, ring slots, waves, min waves per SIMD)
     switch (id) {
-        case 1: return launch_r3<T, 1, 32, 8, 4, 64>(p, st);
-        case 2: return launch_r3<T, 1, 16, 16, 4, 64>(p, st);
-        case 3: return launch_r3<T, 1, 32, 4, 8, 64>(p, st);
-        case 4: return launch_r3<T, 1, 16, 8, 4, 128>(p, st);
-        case 5: return launch_r3<T, 1, 32, 4, 4, 128>(p, st);
-        case 6: return launch_r3<T, 1, 20, 16, 4, 64>(p, st);
-        case 7: return launch_r3<T, 1, 20, 8, 4, 128>(p, st);
-        case 8: return launch_r3<T, 1, 8, 8, 4, 128>(p, st);
-        case 9: return launch_r3<T, 2, 16, 8, 4, 64>(p, st);
-        case 10: return launch_r3<T, 2, 8, 8, 4, 128>(p, st);
-        case 11: return launch_r3<T, 2, 16, 4, 4, 128>(p, st);
-        case 12: return launch_r3<T, 2, 20, 8, 4, 128>(p, st);
-        // 72 KiB of LDS: two blocks (8 waves) per CU
-        case 13: return launch_r3<T, 1, 16, 8, 4, 64>(p, st);
-        case 14: return launch_r3<T, 1, 32, 4, 4, 64>(p, st);
-        case 15: return launch_r3<T, 2, 16, 4, 4, 64>(p, st);
-        case 16: return launch_r3<T, 2, 8, 8, 4, 64>(p, st);
-        // two-slot ring (one stage in flight): 48 KiB -> three blocks per CU, 64-72 KiB -> two
-        case 17: return launch_r3<T, 1, 16, 8, 4, 64, 2>(p, st);
-        case 18: return launch_r3<T, 1, 32, 4, 4, 64, 2>(p, st);
-        case 19: return launch_r3<T, 1, 32, 8, 4, 64, 2>(p, st);
-        case 20: return launch_r3<T, 1, 16, 16, 4, 64, 2>(p, st);
-        case 21: return launch_r3<T, 1, 16, 8, 4, 128, 2>(p, st);
-        case 22: return launch_r3<T, 2, 16, 4, 4, 64, 2>(p, st);
-        case 23: return launch_r3<T, 2, 8, 8, 4, 64, 2>(p, st);
-        case 24: return launch_r3<T, 2, 16, 8, 4, 64, 2>(p, st);
-        // 8-wave blocks, two per CU
-        case 25: return launch_r3<T, 1, 16, 16, 4, 64, 2, 8>(p, st);
-        case 26: return launch_r3<T, 1, 32, 8, 4, 64, 2, 8>(p, st);
-        case 27: return launch_r3<T, 1, 16, 8, 4, 128, 2, 8>(p, st);
-        case 28: return launch_r3<T, 1, 8, 8, 4, 128, 2, 8>(p, st);
-        case 29: return launch_r3<T, 2, 8, 8, 4, 128, 2, 8>(p, st);
-        case 30: return launch_r3<T, 2, 16, 8, 4, 64, 2, 8>(p, st);
-        case 31: return launch_r3<T, 1, 16, 8, 4, 64, 2, 8>(p, st);
-        case 32: return launch_r3<T, 2, 8, 16, 4, 64, 2, 8>(p, st);
+        // 4 waves, three-slot ring: 63 KiB -> two blocks per CU
+        case 1: return launch_r3<T, 1, 16, 8, 4, 64>(p, st);
+        case 2: return launch_r3<T, 1, 32, 4, 4, 64>(p, st);
+        case 3: return launch_r3<T, 2, 16, 4, 4, 64>(p, st);
+        case 4: return launch_r3<T, 2, 8, 8, 4, 64>(p, st);
+        // 4 waves, two-slot ring (one stage in flight): 42 KiB -> three blocks, 58-66 KiB -> two
+        case 5: return launch_r3<T, 1, 16, 8, 4, 64, 2>(p, st);
+        case 6: return launch_r3<T, 1, 32, 4, 4, 64, 2>(p, st);
+        case 7: return launch_r3<T, 1, 32, 8, 4, 64, 2>(p, st);
+        case 8: return launch_r3<T, 1, 16, 16, 4, 64, 2>(p, st);
+        case 9: return launch_r3<T, 1, 16, 8, 4, 128, 2>(p, st);
+        case 10: return launch_r3<T, 2, 16, 4, 4, 64, 2>(p, st);
+        case 11: return launch_r3<T, 2, 8, 8, 4, 64, 2>(p, st);
+        case 12: return launch_r3<T, 2, 16, 8, 4, 64, 2>(p, st);
+        // 8-wave blocks, two-slot ring, two blocks per CU
+        case 13: return launch_r3<T, 1, 16, 16, 4, 64, 2, 8>(p, st);
+        case 14: return launch_r3<T, 1, 32, 8, 4, 64, 2, 8>(p, st);
+        case 15: return launch_r3<T, 1, 16, 8, 4, 128, 2, 8>(p, st);
+        case 16: return launch_r3<T, 1, 8, 8, 4, 128, 2, 8>(p, st);
+        case 17: return launch_r3<T, 2, 8, 8, 4, 128, 2, 8>(p, st);
+        case 18: return launch_r3<T, 2, 16, 8, 4, 64, 2, 8>(p, st);
+        case 19: return launch_r3<T, 1, 16, 8, 4, 64, 2, 8>(p, st);
+        case 20: return launch_r3<T, 2, 8, 16, 4, 64, 2, 8>(p, st);
+        // 8 waves, three-slot ring (two stages in flight)
+        case 21: return launch_r3<T, 1, 16, 8, 4, 64, 3, 8>(p, st);
+        case 22: return launch_r3<T, 1, 32, 4, 4, 64, 3, 8>(p, st);
+        // 8 waves held to 80 registers: three blocks (6 waves per SIMD)
+        case 23: return launch_r3<T, 1, 16, 8, 4, 64, 2, 8, 6>(p, st);
+        case 24: return launch_r3<T, 1, 32, 4, 4, 64, 2, 8, 6>(p, st);
+        case 25: return launch_r3<T, 1, 8, 16, 4, 64, 2, 8, 6>(p, st);
+        // one block per CU, wide tiles (small late layers)
+        case 26: return launch_r3<T, 1, 20, 16, 4, 64>(p, st);
+        case 27: return launch_r3<T, 2, 20, 8, 4, 128>(p, st);
         default: set_error("conv_r3 tile id %d", id); return YXH_EINVAL;
     }
 }
