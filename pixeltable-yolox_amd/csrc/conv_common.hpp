@@ -263,6 +263,6 @@ int conv_pwf_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumPwfTiles = 8;
 // 3x3 conv with the branch-free buffer-LDS loader (conv_r3.hip): tile ids 113..112+kNumR3Tiles
 int conv_r3_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
-constexpr int kNumR3Tiles = 32;  // ids beyond the built ones report EINVAL
+constexpr int kNumR3Tiles = 48;  // ids beyond the built ones report EINVAL
 
 }  // namespace yxh

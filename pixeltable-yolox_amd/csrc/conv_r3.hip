@@ -72,6 +72,11 @@ __device__ __forceinline__ int r3_xcd_remap(int id, int nblk) {
 
 constexpr uint32_t kR3Oob = 0x80000000u;  // beyond any descriptor range: reads 0
 
+// Probe builds only (tools/r3_split.sh): 1 = no MFMA / LDS reads, 2 = no DMA
+#ifndef YXH_R3_PROBE
+#define YXH_R3_PROBE 0
+#endif
+
 }  // namespace
 
 // NBUF = 3: the ring slot of stage (cb, ky) is ky, two stages in flight;
@@ -84,14 +89,15 @@ constexpr uint32_t kR3Oob = 0x80000000u;  // beyond any descriptor range: reads 
 template <typename T, int S, int TX, int TY, int CH, int TN, int NBUF, int NW, int MINW>
 __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles_x, int tiles_y, int ntn) {
     static_assert(NBUF == 2 || NBUF == 3, "ring depth");
-    static_assert(NW == 4 || NW == 8, "waves per block");
-    constexpr int WN = TN / 64, WM = NW / WN;
+    static_assert(NW == 4 || NW == 8 || NW == 16, "waves per block");
+    constexpr int WN = TN >= 64 ? TN / 64 : 1, WM = NW / WN;  // wave grid: WN along channels
+    constexpr int WTN = TN / WN;                               // 64 (or TN = 32)
     constexpr int EPC = Chunk<T>::N;
     constexpr int ES = sizeof(T);
     constexpr int KS = CH / 4;  // 64-byte slabs (one MFMA K step) per stage
     constexpr int KST = CH * EPC;
     constexpr int TM = TX * TY, WTM = TM / WM;
-    constexpr int FR = 4, FC = WTM / 16;
+    constexpr int FR = WTN / 16, FC = WTM / 16;
     constexpr int HX = (TX - 1) * S + 3;
     constexpr int A_SLOTS = 3 * TN * CH, B_SLOTS = TY * HX * CH;
     constexpr int A_LOADS = A_SLOTS / 64, B_LOADS = (B_SLOTS + 63) / 64;  // 1 KiB wave-loads
@@ -153,6 +159,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
 
     auto issue_to = [&](int cb, auto kyc, uint32_t slot) {
         constexpr int ky = decltype(kyc)::value;
+        if constexpr (YXH_R3_PROBE == 2) return;
         const uint32_t base = lds0 + slot * BUF;
         const uint32_t soa = (uint32_t)((ky * 3 * cin + cb * KST) * ES), sob = (uint32_t)(cb * KST * ES);
 #pragma unroll
@@ -184,6 +191,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
     }
 
     auto compute = [&](int slot) {
+        if constexpr (YXH_R3_PROBE == 1) return;
         const char* A = smem + slot * BUF;
         const char* B = A + A_BYTES;
 #pragma unroll
@@ -194,7 +202,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
                 uint4 af[FR], bf[FC];
 #pragma unroll
                 for (int i = 0; i < FR; ++i) {
-                    const int r = wr * 64 + i * 16 + frow;
+                    const int r = wr * WTN + i * 16 + frow;
                     af[i] = *(const uint4*)(A + ((kx * CH + chunk) * TN + (r ^ swa)) * 16);
                 }
 #pragma unroll
@@ -275,7 +283,213 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
         n0, lbias);
 }
 
-template <typename T, int S, int TX, int TY, int CH, int TN, int NBUF = 3, int NW = 4, int MINW = NW == 8 ? 4 : 1>
+// conv_r3h: the same conv with the pixel operand staged ONCE per channel block.
+// conv_r3 stages, per (cb, ky), the TY input rows that kernel row ky reads: every input row
+// is fetched three times.  Here a stage of channel block cb is the whole halo tile
+// (HY = (TY-1)*S + 3 rows x HX pixels x 32 channels, one B slot of two, by cb parity) and
+// the weights of ONE kernel row (3 taps x TN x 32 channels, A ring of three, slot ky):
+//   stage (cb, 0): A(cb, 0) + B(cb);  stage (cb, 1): A(cb, 1);  stage (cb, 2): A(cb, 2)
+// and kernel row ky reads B rows ty*S + ky.  Two stages stay in flight (the A ring of
+// three); the DMA bytes per channel block drop from 3*TY*HX to HY*HX pixel chunks, which
+// matters because the LDS-DMA path (~10 TB/s chip-wide, MI355X_MICROARCH.md ldsdma-fill)
+// is what bounds conv_r3 (probe: DMA alone 117 us of a 145 us 80x80 128->256 launch).
+__device__ __forceinline__ void r3_wait_dyn(int n) {
+    switch (n) {
+#define YXH_W(k) \
+    case k: r3_wait_vm<k>(); break;
+        YXH_W(1) YXH_W(2) YXH_W(3) YXH_W(4) YXH_W(5) YXH_W(6) YXH_W(7) YXH_W(8) YXH_W(9) YXH_W(10)
+        YXH_W(11) YXH_W(12) YXH_W(13) YXH_W(14) YXH_W(15)
+#undef YXH_W
+        default: r3_wait_vm<0>(); break;
+    }
+}
+
+template <typename T, int S, int TX, int TY, int TN, int NW, int MINW>
+__global__ __launch_bounds__(64 * NW, MINW) void conv_r3h(ConvParams p, int tiles_x, int tiles_y, int ntn) {
+    constexpr int CH = 4;  // 16-byte chunks (32 channels) per channel block
+    constexpr int WN = TN >= 64 ? TN / 64 : 1, WM = NW / WN, WTN = TN / WN;
+    constexpr int EPC = Chunk<T>::N;
+    constexpr int ES = sizeof(T);
+    constexpr int KST = CH * EPC;
+    constexpr int TM = TX * TY, WTM = TM / WM;
+    constexpr int FR = WTN / 16, FC = WTM / 16;
+    constexpr int HX = (TX - 1) * S + 3, HY = (TY - 1) * S + 3;
+    constexpr int A_SLOTS = 3 * TN * CH, B_SLOTS = HY * HX * CH;
+    constexpr int A_LOADS = A_SLOTS / 64, B_LOADS = (B_SLOTS + 63) / 64;
+    constexpr int GA = (A_LOADS + NW - 1) / NW, GB = (B_LOADS + NW - 1) / NW;
+    constexpr int A_PART = A_LOADS % NW, B_PART = B_LOADS % NW;
+    constexpr int ABUF = A_LOADS * 1024, BBUF = B_LOADS * 1024;
+    constexpr int SMEM = 3 * ABUF + 2 * BBUF;
+    static_assert(A_SLOTS % 64 == 0 && TM % (16 * WM) == 0 && GA + GB <= 15, "tile");
+    static_assert(SMEM <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nblk = tiles_x * tiles_y * (p.M / p.ohw) * ntn;
+    const int bid = r3_xcd_remap(blockIdx.x, nblk);
+    const int nt = bid % ntn;
+    int t = bid / ntn;
+    const int tx_i = t % tiles_x;
+    t /= tiles_x;
+    const int ty_i = t % tiles_y;
+    const int b = t / tiles_y;
+    const int n0 = nt * TN, oy0 = ty_i * TY, ox0 = tx_i * TX;
+    const int wr = wave / WM, wc = wave % WM;
+    const int cin = p.cin, scs = p.scs[0], in_w = p.in_w, in_h = p.in_h;
+
+    const u32x4 wsrd = r3_srd(p.w, (uint32_t)((long long)p.cout * 9 * cin * ES));
+    const u32x4 xsrd = r3_srd((const T*)p.sptr[0] + (long long)b * p.sbs[0],
+                              (uint32_t)((long long)in_h * in_w * scs * ES));
+    uint32_t aoff[GA];
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+        const int s = 64 * (wave + NW * i) + lane;
+        const int kx = s / (CH * TN), rem = s - kx * (CH * TN);
+        const int c = rem / TN, rp = rem - c * TN;
+        const int n = min(n0 + (rp ^ (2 * c)), p.cout - 1);
+        aoff[i] = s < A_SLOTS ? (uint32_t)(((n * 9 + kx) * cin + c * EPC) * ES) : kR3Oob;
+    }
+    uint32_t boff[GB];
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+        const int sb = 64 * (wave + NW * i) + lane;
+        const int hp = sb / CH, cp = sb - hp * CH;
+        const int c = cp ^ ((hp >> 2) & 3);
+        const int hy = hp / HX, hx = hp - hy * HX;
+        const int iy = oy0 * S - 1 + hy, ix = ox0 * S - 1 + hx;
+        const bool ok = sb < B_SLOTS && iy >= 0 && iy < in_h && ix >= 0 && ix < in_w;
+        boff[i] = ok ? (uint32_t)(((iy * in_w + ix) * scs + c * EPC) * ES) : kR3Oob;
+    }
+    const uint32_t lds0 = r3_lds_addr(smem) + (uint32_t)wave * 1024;
+    // this wave's share of a stage's wave-loads
+    const int cnt_a = GA - (A_PART && wave >= A_PART ? 1 : 0);
+    const int cnt_b = GB - (B_PART && wave >= B_PART ? 1 : 0);
+
+    auto issue_a = [&](int cb, int ky) {
+        if constexpr (YXH_R3_PROBE == 2) return;
+        const uint32_t base = lds0 + (uint32_t)(ky * ABUF);
+        const uint32_t soa = (uint32_t)((ky * 3 * cin + cb * KST) * ES);
+#pragma unroll
+        for (int i = 0; i < GA; ++i)
+            if (A_PART == 0 || i + 1 < GA || wave < A_PART) r3_dma(wsrd, aoff[i], soa, base + i * NW * 1024);
+    };
+    auto issue_b = [&](int cb) {
+        if constexpr (YXH_R3_PROBE == 2) return;
+        const uint32_t base = lds0 + (uint32_t)(3 * ABUF + (cb & 1) * BBUF);
+        const uint32_t sob = (uint32_t)(cb * KST * ES);
+#pragma unroll
+        for (int i = 0; i < GB; ++i)
+            if (B_PART == 0 || i + 1 < GB || wave < B_PART) r3_dma(xsrd, boff[i], sob, base + i * NW * 1024);
+    };
+
+    f32x4 acc[FR][FC];
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float lbias[FR][4];
+    load_lane_bias<TN, WN, WM>(p, n0, lbias);
+
+    const int frow = lane & 15, fq = lane >> 4;
+    int hp0[FC];  // halo-tile pixel of this lane's fragment column at (ky, kx) = (0, 0)
+#pragma unroll
+    for (int j = 0; j < FC; ++j) {
+        const int pl = wc * WTM + j * 16 + frow;
+        const int ty = pl / TX, tx = pl - ty * TX;
+        hp0[j] = ty * S * HX + tx * S;
+    }
+
+    auto compute = [&](int cb, auto kyc) {
+        if constexpr (YXH_R3_PROBE == 1) return;
+        constexpr int ky = decltype(kyc)::value;
+        const char* A = smem + ky * ABUF;
+        const char* B = smem + 3 * ABUF + (cb & 1) * BBUF;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            uint4 af[FR], bf[FC];
+#pragma unroll
+            for (int i = 0; i < FR; ++i) {
+                const int r = wr * WTN + i * 16 + frow;
+                af[i] = *(const uint4*)(A + ((kx * CH + fq) * TN + (r ^ (2 * fq))) * 16);
+            }
+#pragma unroll
+            for (int j = 0; j < FC; ++j) {
+                const int hp = hp0[j] + ky * HX + kx;
+                bf[j] = *(const uint4*)(B + (hp * CH + (fq ^ ((hp >> 2) & 3))) * 16);
+            }
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], af[i], bf[j]);
+        }
+    };
+
+    using K0 = std::integral_constant<int, 0>;
+    using K1 = std::integral_constant<int, 1>;
+    using K2 = std::integral_constant<int, 2>;
+    const int ncb = p.ncb;
+    issue_a(0, 0);
+    issue_b(0);
+    issue_a(0, 1);
+    for (int cb = 0; cb < ncb; ++cb) {
+        const bool more = cb + 1 < ncb;
+        r3_wait_dyn(cnt_a);  // stage (cb, 0) landed; (cb, 1) may fly
+        r3_barrier();
+        issue_a(cb, 2);
+        compute(cb, K0{});
+        r3_wait_dyn(cnt_a);  // (cb, 1) landed; (cb, 2) may fly
+        r3_barrier();
+        if (more) {
+            issue_a(cb + 1, 0);
+            issue_b(cb + 1);
+        }
+        compute(cb, K1{});
+        r3_wait_dyn(more ? cnt_a + cnt_b : 0);  // (cb, 2) landed; (cb + 1, 0) may fly
+        r3_barrier();
+        if (more) issue_a(cb + 1, 1);
+        compute(cb, K2{});
+    }
+    r3_wait_vm<0>();
+    r3_barrier();
+    const int OH = p.out_h, OW = p.out_w, mb = b * p.ohw;
+    conv_epilogue_map<T, TN, TM, WN, WM, SMEM>(
+        p, acc, smem,
+        [=](int pl) {
+            const int ty = pl / TX, tx = pl - ty * TX;
+            const int oy = oy0 + ty, ox = ox0 + tx;
+            return (oy < OH && ox < OW) ? mb + oy * OW + ox : -1;
+        },
+        n0, lbias);
+}
+
+template <typename T, int S, int TX, int TY, int TN, int NW, int MINW = NW >= 8 ? 4 : 1>
+static int launch_r3h(const ConvParams& p, hipStream_t st) {
+    if (p.stride != S) {
+        set_error("conv_r3h variant built for stride %d", S);
+        return YXH_EUNSUPPORTED;
+    }
+    const int kst = 4 * Chunk<T>::N;
+    if (p.cin % kst) {
+        set_error("conv_r3h: cin %d not a multiple of the %d-channel stage", p.cin, kst);
+        return YXH_EUNSUPPORTED;
+    }
+    ConvParams q = p;
+    q.ncb = p.cin / kst;
+    const int tiles_x = (p.out_w + TX - 1) / TX, tiles_y = (p.out_h + TY - 1) / TY;
+    const int ntn = (p.cout + TN - 1) / TN;
+    const long long nblk = (long long)tiles_x * tiles_y * (p.M / p.ohw) * ntn;
+    if (nblk >= (1LL << 31)) {
+        set_error("conv_r3h grid too large");
+        return YXH_EINVAL;
+    }
+    hipLaunchKernelGGL((conv_r3h<T, S, TX, TY, TN, NW, MINW>), dim3((unsigned)nblk), dim3(64 * NW), 0, st, q, tiles_x,
+                       tiles_y, ntn);
+    YXH_CHECK_LAUNCH("conv_r3h launch");
+    return YXH_OK;
+}
+
+template <typename T, int S, int TX, int TY, int CH, int TN, int NBUF = 3, int NW = 4, int MINW = NW >= 8 ? 4 : 1>
 static int launch_r3(const ConvParams& p, hipStream_t st) {
     constexpr int HX = (TX - 1) * S + 3;
     constexpr int AL = 3 * TN * CH / 64, BL = (TY * HX * CH + 63) / 64;
@@ -347,6 +561,19 @@ static int r3_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         // one block per CU, wide tiles (small late layers)
         case 26: return launch_r3<T, 1, 20, 16, 4, 64>(p, st);
         case 27: return launch_r3<T, 2, 20, 8, 4, 128>(p, st);
+        // 32 output channels per block (cout = 32 layers)
+        case 28: return launch_r3<T, 1, 32, 8, 4, 32, 2, 8>(p, st);
+        // conv_r3h: halo tile staged once per channel block -> (stride, TX, TY, TN, waves)
+        case 29: return launch_r3h<T, 1, 16, 16, 64, 8>(p, st);
+        case 30: return launch_r3h<T, 1, 32, 8, 64, 8>(p, st);
+        case 31: return launch_r3h<T, 1, 16, 8, 64, 4>(p, st);
+        case 32: return launch_r3h<T, 1, 32, 8, 32, 8>(p, st);
+        case 33: return launch_r3h<T, 2, 8, 8, 64, 4>(p, st);
+        case 34: return launch_r3h<T, 2, 16, 8, 64, 8, 2>(p, st);
+        case 35: return launch_r3h<T, 2, 8, 16, 64, 8, 2>(p, st);
+        case 36: return launch_r3h<T, 1, 16, 16, 128, 8, 2>(p, st);
+        case 37: return launch_r3h<T, 1, 32, 16, 64, 16>(p, st);
+        case 38: return launch_r3h<T, 1, 16, 8, 64, 8>(p, st);
         default: set_error("conv_r3 tile id %d", id); return YXH_EINVAL;
     }
 }

@@ -603,7 +603,7 @@ def test_conv_r3_3x3(dtype, geom):
     want = ref_conv(x, conv, bn, "silu")
     X = nhwc(x, dtype)
     ran = 0
-    for tid in range(113, 140):
+    for tid in range(113, 151):
         try:
             y = run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid)
         except NotImplementedError as e:
@@ -621,7 +621,7 @@ def test_conv_r3_residual_and_strided_dst(dtype):
     r = torch.randn(2, 64, 20, 20, generator=torch.Generator().manual_seed(5))
     want = ref_conv(x, conv, bn, "silu") + r.to(dtype).float()
     buf = torch.zeros(2, 20, 20, 128, dtype=dtype, device=DEV)
-    for tid in (113, 117, 125, 126, 127, 133, 135, 138):
+    for tid in (113, 117, 125, 126, 127, 133, 135, 138, 140, 141, 142, 144, 150):
         buf[..., 64:] = nhwc(r, dtype)
         y = run_conv([(nhwc(x, dtype), 0, 64, 0)], conv, bn, dtype, residual=(buf, 64), out=buf, out_coff=64,
                      tile=2 * tid)

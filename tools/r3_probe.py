@@ -19,7 +19,7 @@ SHAPES = [(1, 160, 32, 32), (1, 80, 64, 64), (1, 40, 128, 128), (1, 20, 256, 256
           (1, 80, 128, 256), (1, 40, 128, 256), (1, 20, 128, 128), (2, 320, 32, 64), (2, 160, 64, 128),
           (2, 80, 128, 256), (2, 40, 256, 512), (2, 80, 128, 128), (2, 40, 256, 256)]
 OLD = [t for t in TILE_CANDIDATES if (t >> 1) < 97]
-NEW = [2 * i for i in range(113, 140)]
+NEW = [2 * i for i in range(113, 151)]
 TILES = [int(t) for t in sys.argv[1:]] or OLD + NEW
 
 
@@ -68,7 +68,7 @@ for S, H, K, Nc in SHAPES:
     old = [r for r in res if r[1] in OLD]
     new = [r for r in res if r[1] in NEW]
     bad = [r for r in res if r[2] > 2e-2]
-    fmt = lambda r: f"t{r[1] >> 1}/{(r[1] & 1) + 1} {r[0]:.1f}us {flop / r[0] / 1e6:.0f}TF"  # noqa: E731
+    fmt = lambda r: f"r{(r[1] >> 1) - 112}:{r[0]:.1f}us/{flop / r[0] / 1e6:.0f}TF"  # noqa: E731
     print(f"s{S} {H}->{Ho} {K}->{Nc}: best old {fmt(old[0]) if old else '-'} | new " +
-          " ".join(fmt(r) for r in new[:4]) + (f" | BAD {[(r[1] >> 1, r[2]) for r in bad]}" if bad else ""),
+          " ".join(fmt(r) for r in new) + (f" | BAD {[(r[1] >> 1, r[2]) for r in bad]}" if bad else ""),
           flush=True)
