@@ -578,18 +578,35 @@ static int r3_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
     }
 }
 
+// fp32 (the training path at BASELINE configs[2]): the halo-tile kernel only; a stage is
+// 16 channels (4 fp32 per 16-byte chunk) and each fragment pair is 4 x v_mfma_f32_16x16x4f32,
+// so the kernel is MFMA-bound where its 16-bit form is DMA-bound.
+static int r3h_dispatch_f32(int id, const ConvParams& p, hipStream_t st) {
+    switch (id) {
+        case 29: return launch_r3h<float, 1, 16, 16, 64, 8>(p, st);
+        case 30: return launch_r3h<float, 1, 32, 8, 64, 8>(p, st);
+        case 31: return launch_r3h<float, 1, 16, 8, 64, 4>(p, st);
+        case 32: return launch_r3h<float, 1, 32, 8, 32, 8>(p, st);
+        case 33: return launch_r3h<float, 2, 8, 8, 64, 4>(p, st);
+        case 38: return launch_r3h<float, 1, 16, 8, 64, 8>(p, st);
+        default: set_error("conv_r3 tile id %d is built for bf16/f16 only", id); return YXH_EUNSUPPORTED;
+    }
+}
+
 int conv_r3_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st) {
     if (p.taps != 9 || p.kw != 3 || p.pad != 1 || p.nsrc != 1 || p.sup[0] || p.sw[0] != p.in_w) {
         set_error("conv_r3 needs a 3x3 pad-1 conv over one plain source");
         return YXH_EUNSUPPORTED;
     }
-    if ((long long)p.in_h * p.in_w * p.scs[0] * 2 >= (1LL << 31) || (long long)p.cout * 9 * p.cin * 2 >= (1LL << 31)) {
+    const long long es = dtype == YXH_F32 ? 4 : 2;
+    if ((long long)p.in_h * p.in_w * p.scs[0] * es >= (1LL << 31) || (long long)p.cout * 9 * p.cin * es >= (1LL << 31)) {
         set_error("conv_r3: image / weights exceed 31-bit byte offsets");
         return YXH_EUNSUPPORTED;
     }
     if (dtype == YXH_BF16) return r3_dispatch_t<bf16>(id, p, st);
     if (dtype == YXH_F16) return r3_dispatch_t<f16>(id, p, st);
-    set_error("conv_r3 is built for bf16/f16 only");
+    if (dtype == YXH_F32) return r3h_dispatch_f32(id, p, st);
+    set_error("conv_r3: dtype %d", dtype);
     return YXH_EUNSUPPORTED;
 }
 

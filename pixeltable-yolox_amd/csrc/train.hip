@@ -207,22 +207,45 @@ struct FinArgs {
     float* coef;         // BWD out [3][C]: dx = k1*dz + k2*(y - mean) + k3
 };
 
-// 8 channels per block, 32 lanes per channel sum the per-block partials (strided, in
-// double), then a fixed-order tree over the lanes: deterministic.
+// 4 channels per block, a wave per channel: each lane sums its strided share of the
+// per-block partials in double (four independent chains, so the loads of four rows are in
+// flight at once: the kernel is latency-bound, ~1024 partials per channel), then a
+// fixed-order tree over the lanes: deterministic.
 __global__ __launch_bounds__(256) void chan_finalize(FinArgs f) {
     __shared__ double red[2][256];
-    const int j = threadIdx.x >> 5, lane = threadIdx.x & 31;
-    const int c = blockIdx.x * 8 + j;
-    double t1 = 0.0, t2 = 0.0;
-    if (c < f.C)
-        for (int b = lane; b < f.nblk; b += 32) {
-            t1 += f.partial[((long long)b * 2) * f.C + c];
-            t2 += f.partial[((long long)b * 2 + 1) * f.C + c];
+    const int j = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + j;
+    double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
+    if (c < f.C) {
+        const long long rs = 2LL * f.C;  // partial row stride (one block's [2][C])
+        const float* p0 = f.partial + c;
+        int b = lane;
+        for (; b + 192 < f.nblk; b += 256) {
+            float v1[4], v2[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                v1[u] = p0[(long long)(b + 64 * u) * rs];
+                v2[u] = p0[(long long)(b + 64 * u) * rs + f.C];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a1[u] += v1[u];
+                a2[u] += v2[u];
+            }
         }
-    red[0][threadIdx.x] = t1;
-    red[1][threadIdx.x] = t2;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int bb = b + 64 * u;
+            if (bb < f.nblk) {
+                a1[u] += p0[(long long)bb * rs];
+                a2[u] += p0[(long long)bb * rs + f.C];
+            }
+        }
+    }
+    red[0][threadIdx.x] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+    red[1][threadIdx.x] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
     __syncthreads();
-    for (int s = 16; s > 0; s >>= 1) {
+    for (int s = 32; s > 0; s >>= 1) {
         if (lane < s) {
             red[0][threadIdx.x] += red[0][threadIdx.x + s];
             red[1][threadIdx.x] += red[1][threadIdx.x + s];
@@ -230,6 +253,7 @@ __global__ __launch_bounds__(256) void chan_finalize(FinArgs f) {
         __syncthreads();
     }
     if (lane != 0 || c >= f.C) return;
+    double t1, t2;
     t1 = red[0][threadIdx.x];
     t2 = red[1][threadIdx.x];
     if (f.mode == RED_STATS) {
@@ -518,6 +542,185 @@ __global__ __launch_bounds__(256) void conv_wgrad(WgradParams p) {
                     atomicAdd(p.dw + (((long long)n * p.cin_store + c) * p.kh + ky) * p.kw + kx, acc[i][j][r]);
             }
         }
+}
+
+// ------------------------------------------------------------------ weight gradient, all nine taps
+// fp32 3x3 (pad 1, stride S) weight gradient with the nine taps of one block sharing its
+// staged operands: conv_wgrad stages dy and x once PER TAP (nine blocks re-read the same
+// pixels; the 320x320 stem took 0.9 ms at 1.5 TB/s of re-reads).  Here a block owns
+// dW[n0, n0+TN) x [c0, c0+TC) x 9 taps and walks pixel tiles of TY output rows x 16
+// columns of one image:
+//  * dy tile -> LDS transposed, [TN][TM] (pixel-major rows: an MFMA K step = 4 pixels);
+//    x halo tile ((TY-1)*S+3 rows x 15*S+3 columns) -> LDS transposed, [TC][row][col];
+//    next tile's global loads are in registers while this tile computes;
+//  * per output row: the A fragments (dy) are read once and serve all nine taps; the B
+//    fragment of tap (ky, kx) is the halo row ty*S + ky at columns tx*S + kx;
+//  * wave (wn, wc) owns a TN/WN x TC/WC slice of every tap: no cross-wave reduction;
+//    the block's totals go to dW (torch layout) with fp32 atomics (dW pre-zeroed).
+// v_mfma_f32_16x16x4f32 (Mma<float>): 4 MFMAs per 16-pixel row and fragment pair.
+template <int S, int TN, int TC, int WN, int WC, int TY>
+__global__ __launch_bounds__(64 * WN * WC) void conv_wgrad9(WgradParams p, int tiles_x, int tiles_y, int tpb) {
+    constexpr int NT = 64 * WN * WC, TX = 16, TM = TX * TY;
+    constexpr int HX = (TX - 1) * S + 3, HY = (TY - 1) * S + 3;
+    constexpr int DYS = TM + 4;        // dyT row stride (floats; 16-byte aligned rows)
+    constexpr int XRS = HX + 1;        // xT row stride
+    constexpr int XCS = HY * XRS + 4;  // xT channel stride
+    constexpr int WTN = TN / WN, WTC = TC / WC, FRN = WTN / 16, FRC = WTC / 16;
+    constexpr int N4 = TN / 4, C4 = TC / 4;
+    constexpr int NDY = TM * N4, NX = HY * HX * C4;
+    constexpr int IDY = (NDY + NT - 1) / NT, IX = (NX + NT - 1) / NT;
+    static_assert(FRN >= 1 && FRC >= 1 && WTN % 16 == 0 && WTC % 16 == 0, "tile");
+    __shared__ __attribute__((aligned(16))) float dyT[TN * DYS];
+    __shared__ __attribute__((aligned(16))) float xT[TC * XCS];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wn = wave / WC, wc = wave % WC;
+    const int n0 = blockIdx.y * TN, c0 = blockIdx.z * TC;
+    const int per_img = tiles_y * tiles_x;
+    const int T = p.B * per_img;
+    const int t0 = blockIdx.x * tpb, t1 = min(T, t0 + tpb);
+    const int OH = p.out_h, OW = p.out_w;
+    const float* dyp = (const float*)p.dy;
+    const float* xp = (const float*)p.sptr[0];
+    const int scs = p.scs[0], sw = p.sw[0];
+
+    float4 rdy[IDY], rx[IX];
+    auto gload = [&](int t) {
+        const int b = t / per_img, r = t - b * per_img;
+        const int tyi = r / tiles_x, txi = r - tyi * tiles_x;
+        const int oy0 = tyi * TY, ox0 = txi * TX;
+#pragma unroll
+        for (int i = 0; i < IDY; ++i) {
+            const int q = tid + NT * i;
+            const int pl = q / N4, n = n0 + 4 * (q - pl * N4);
+            const int oy = oy0 + pl / TX, ox = ox0 + pl % TX;
+            const bool ok = q < NDY && oy < OH && ox < OW && n < p.dych;
+            rdy[i] = ok ? *(const float4*)(dyp + (long long)b * p.dybs + (long long)(oy * OW + ox) * p.dycs + n)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < IX; ++i) {
+            const int q = tid + NT * i;
+            const int hp = q / C4, c = c0 + 4 * (q - hp * C4);
+            const int hy = hp / HX, hx = hp - hy * HX;
+            const int iy = oy0 * S - 1 + hy, ix = ox0 * S - 1 + hx;
+            const bool ok = q < NX && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w && c < p.cin;
+            rx[i] = ok ? *(const float4*)(xp + (long long)b * p.sbs[0] + (long long)(iy * sw + ix) * scs + c)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < IDY; ++i) {
+            const int q = tid + NT * i;
+            if (q >= NDY) continue;
+            const int pl = q / N4, n = 4 * (q - pl * N4);
+            dyT[(n + 0) * DYS + pl] = rdy[i].x;
+            dyT[(n + 1) * DYS + pl] = rdy[i].y;
+            dyT[(n + 2) * DYS + pl] = rdy[i].z;
+            dyT[(n + 3) * DYS + pl] = rdy[i].w;
+        }
+#pragma unroll
+        for (int i = 0; i < IX; ++i) {
+            const int q = tid + NT * i;
+            if (q >= NX) continue;
+            const int hp = q / C4, c = 4 * (q - hp * C4);
+            const int hy = hp / HX, hx = hp - hy * HX;
+            const int o = hy * XRS + hx;
+            xT[(c + 0) * XCS + o] = rx[i].x;
+            xT[(c + 1) * XCS + o] = rx[i].y;
+            xT[(c + 2) * XCS + o] = rx[i].z;
+            xT[(c + 3) * XCS + o] = rx[i].w;
+        }
+    };
+
+    f32x4 acc[9][FRN][FRC];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < FRN; ++i)
+#pragma unroll
+            for (int j = 0; j < FRC; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int frow = lane & 15, fq = lane >> 4;
+
+    auto compute = [&]() {
+        for (int ty = 0; ty < TY; ++ty) {
+            uint4 af[FRN];
+#pragma unroll
+            for (int i = 0; i < FRN; ++i)
+                af[i] = *(const uint4*)&dyT[(wn * WTN + i * 16 + frow) * DYS + ty * TX + 4 * fq];
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+#pragma unroll
+                    for (int j = 0; j < FRC; ++j) {
+                        const float* xr = &xT[(wc * WTC + j * 16 + frow) * XCS + (ty * S + ky) * XRS + 4 * fq * S + kx];
+                        const uint4 bf = make_uint4(__float_as_uint(xr[0]), __float_as_uint(xr[S]),
+                                                    __float_as_uint(xr[2 * S]), __float_as_uint(xr[3 * S]));
+#pragma unroll
+                        for (int i = 0; i < FRN; ++i) Mma<float>::run(acc[ky * 3 + kx][i][j], af[i], bf);
+                    }
+                }
+        }
+    };
+
+    if (t0 < t1) {
+        gload(t0);
+        lstore();
+        __syncthreads();
+        for (int t = t0; t < t1; ++t) {
+            if (t + 1 < t1) gload(t + 1);
+            compute();
+            __syncthreads();
+            if (t + 1 < t1) {
+                lstore();
+                __syncthreads();
+            }
+        }
+    }
+    // dW (torch layout [cout][cin_store][3][3]) += acc
+#pragma unroll
+    for (int i = 0; i < FRN; ++i)
+#pragma unroll
+        for (int j = 0; j < FRC; ++j) {
+            const int c = c0 + wc * WTC + j * 16 + frow;
+            if (c >= p.cin_store) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n0 + wn * WTN + i * 16 + fq * 4 + r;
+                if (n >= p.cout) continue;
+                float* d = p.dw + ((long long)n * p.cin_store + c) * 9;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) atomicAdd(d + t, acc[t][i][j][r]);
+            }
+        }
+}
+
+template <int S, int TN, int TC, int WN, int WC, int TY>
+int launch_wgrad9_t(const WgradParams& p, hipStream_t st) {
+    if (p.kh != 3 || p.kw != 3 || p.pad != 1 || p.stride != S || p.nsrc != 1 || p.sup[0] || p.sw[0] != p.in_w) {
+        set_error("wgrad tiles 11-16 (all nine taps per block) need a 3x3 pad-1 stride-%d conv over one plain source", S);
+        return YXH_EUNSUPPORTED;
+    }
+    if (p.cin % 4 || p.dych % 4 || p.dycs % 4 || p.scs[0] % 4) {
+        set_error("wgrad tiles 11-16: channels must be whole 4-float chunks");
+        return YXH_EUNSUPPORTED;
+    }
+    const int tiles_x = (p.out_w + 15) / 16, tiles_y = (p.out_h + TY - 1) / TY;
+    const long long T = (long long)p.B * tiles_x * tiles_y;
+    const int ntn = (p.cout + TN - 1) / TN, ntc = (p.cin + TC - 1) / TC;
+    YXH_CHECK_ARG(T < (1LL << 31) && ntn < 65536 && ntc < 65536, "wgrad grid");
+    // about two blocks per CU over the grid, at least two pixel tiles per block
+    long long splits = (512 + (long long)ntn * ntc - 1) / ((long long)ntn * ntc);
+    if (splits > (T + 1) / 2) splits = (T + 1) / 2;
+    if (splits < 1) splits = 1;
+    const int tpb = (int)((T + splits - 1) / splits);
+    splits = (T + tpb - 1) / tpb;
+    hipLaunchKernelGGL((conv_wgrad9<S, TN, TC, WN, WC, TY>), dim3((unsigned)splits, ntn, ntc), dim3(64 * WN * WC), 0,
+                       st, p, tiles_x, tiles_y, tpb);
+    YXH_CHECK_LAUNCH("conv_wgrad9");
+    return YXH_OK;
 }
 
 // ------------------------------------------------------------------ weight gradient, LDS-DMA + transposed reads
@@ -938,7 +1141,7 @@ int run_reduce(int mode, int dt, int B, const yxh_src* x, const yxh_src* g, cons
     f.C = C;
     f.M = a.M;
     f.mode = mode;
-    hipLaunchKernelGGL(chan_finalize, dim3((C + 7) / 8), dim3(256), 0, st, f);
+    hipLaunchKernelGGL(chan_finalize, dim3((C + 3) / 4), dim3(256), 0, st, f);
     YXH_CHECK_LAUNCH("chan_finalize");
     return YXH_OK;
 }
@@ -1096,6 +1299,21 @@ int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
         case 8: return launch_wgrad2_t<T, 64, 64, 2>(p, st);
         case 9: return launch_wgrad2_t<T, 128, 64, 3>(p, st);
         case 10: return launch_wgrad2_t<T, 64, 128, 3>(p, st);
+        case 11: case 12: case 13: case 14: case 15: case 16:
+            if constexpr (sizeof(T) != 4) {
+                set_error("wgrad tiles 11-16 (all nine taps per block) are built for fp32 only");
+                return YXH_EUNSUPPORTED;
+            } else {
+                const bool s2 = p.stride == 2;
+                switch (tile) {
+                    case 11: return s2 ? launch_wgrad9_t<2, 32, 32, 2, 2, 4>(p, st) : launch_wgrad9_t<1, 32, 32, 2, 2, 8>(p, st);
+                    case 12: return s2 ? launch_wgrad9_t<2, 64, 32, 2, 2, 4>(p, st) : launch_wgrad9_t<1, 64, 32, 2, 2, 8>(p, st);
+                    case 13: return s2 ? launch_wgrad9_t<2, 64, 64, 2, 2, 2>(p, st) : launch_wgrad9_t<1, 64, 64, 2, 2, 4>(p, st);
+                    case 14: return s2 ? launch_wgrad9_t<2, 32, 16, 2, 1, 4>(p, st) : launch_wgrad9_t<1, 32, 16, 2, 1, 8>(p, st);
+                    case 15: return s2 ? launch_wgrad9_t<2, 32, 32, 2, 2, 2>(p, st) : launch_wgrad9_t<1, 32, 32, 2, 2, 4>(p, st);
+                    default: return s2 ? launch_wgrad9_t<2, 64, 16, 4, 1, 4>(p, st) : launch_wgrad9_t<1, 64, 16, 4, 1, 8>(p, st);
+                }
+            }
         default: set_error("wgrad tile %d", tile); return YXH_EINVAL;
     }
 }

@@ -65,6 +65,16 @@ class Act:
                                     device=self.t.device)
         return self.grad
 
+    def grad_target(self) -> tuple:
+        """(gradient buffer, accumulate?) for a writer that covers every element: the first
+        writer of the reverse pass stores into uninitialised memory instead of a zero fill +
+        accumulate."""
+        if self.grad is None:
+            self.grad = torch.empty(self.t.shape[0], self.h, self.w, self.ch, dtype=torch.float32,
+                                    device=self.t.device)
+            return self.grad, False
+        return self.grad, True
+
 
 def dense_src(t: torch.Tensor, up: int = 0) -> N.Src:
     """View of a dense [B, h, w, C] tensor."""
@@ -117,11 +127,13 @@ class GradBuffer:
 # Tiles of the training convolutions, picked on the device the first time a shape runs
 # (HIP events around each candidate, outputs redirected to scratch) and cached for the
 # process.  Forward/data-gradient convs: the conv_igemm, conv_glds and conv_rows
-# families (tile codes as engine.TILE_CANDIDATES); weight gradients: yxh_wgrad_desc
+# families, plus the conv_r3h tiles on fp32 (tile codes as engine.TILE_CANDIDATES); weight
+# gradients: yxh_wgrad_desc
 # tiles 1-10.  YOLOX_AMD_TRAIN_TUNE=0 keeps the by-shape defaults.
 CONV_TUNE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
                    for k in (0, 1)]
-WGRAD_TUNE_TILES = list(range(1, 11))
+CONV_TUNE_TILES_F32 = CONV_TUNE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)]
+WGRAD_TUNE_TILES = list(range(1, 11)) + (list(range(11, 17)))
 _TRAIN_TILES: dict = {}
 
 
@@ -203,7 +215,7 @@ class TrainGraph:
         key = ("conv", self.dcode, batch, in_h, in_w, out_h, out_w, cin, cout, k, stride, pad, int(dst_f32),
                dst_cs, d.flags) + tuple(_src_key(q) for q in srcs)
         d.tile = self._tile(key, d, self.lib.yxh_conv2d, "dst", batch * dst_bs * (4 if dst_f32 else self.esize),
-                            CONV_TUNE_TILES)
+                            CONV_TUNE_TILES_F32 if self.dtype == torch.float32 else CONV_TUNE_TILES)
         self._chk(self.lib.yxh_conv2d(C.byref(d), self.stream), "conv")
 
     def _wgrad(self, srcs: list, cin: int, cin_store: int, cout: int, k: int, stride: int, pad: int, dy: N.Src,
@@ -274,10 +286,12 @@ class TrainGraph:
                 conv.weight.detach().data_ptr(), conv.out_channels, conv.in_channels, kh, kh, cb, cs, cout_pad,
                 self.dcode, wt.data_ptr(), self.stream), "pack dgrad")
             in_h, in_w = act.h << up, act.w << up  # the conv's logical input size
-            dst = (torch.zeros(batch, in_h, in_w, cs, dtype=torch.float32, device=self.device) if up
-                   else act.ensure_grad())
+            if up:  # the conv writes every element of the temporary; upsample_bwd accumulates
+                dst, acc = torch.empty(batch, in_h, in_w, cs, dtype=torch.float32, device=self.device), False
+            else:
+                dst, acc = act.grad_target()
             self._conv([dy], cout_pad, cs, kh, 1, pad, wt.data_ptr(), self.zero_bias.data_ptr(), dst.data_ptr(),
-                       True, cs, in_h * in_w * cs, in_h, in_w, in_h, in_w, batch, accumulate=True)
+                       True, cs, in_h * in_w * cs, in_h, in_w, in_h, in_w, batch, accumulate=acc)
             if up:
                 g = act.ensure_grad()
                 self._chk(self.lib.yxh_upsample_bwd(dst.data_ptr(), batch, act.h, act.w, cs, g.data_ptr(),
@@ -332,7 +346,10 @@ class TrainGraph:
                 self.ws.numel(), self.stream), "bn act bwd")
             self._ready(bn.weight, bn.bias)
             if residual is not None and residual.needs_grad:
-                residual.ensure_grad().add_(out.grad)
+                if residual.grad is None:  # first writer: take over out.grad (consumed above)
+                    residual.grad = out.grad
+                else:
+                    residual.grad.add_(out.grad)
             self._wgrad(srcs, cin, cin_store, cout, k, s, p, dense_src(dy), gb.of(conv.weight), in_h, in_w, oh, ow,
                         B)
             self._ready(conv.weight)
@@ -506,9 +523,9 @@ class TrainGraph:
                     self._chk(self.lib.yxh_pack_dgrad_weight(
                         wm.data_ptr(), cout, feat.ch, 1, 1, 0, feat.ch, ch, self.dcode, wt.data_ptr(), self.stream),
                         "pack pred dgrad")
-                    g = feat.ensure_grad()
+                    g, acc = feat.grad_target()
                     self._conv([dys], ch, feat.ch, 1, 1, 0, wt.data_ptr(), self.zero_bias.data_ptr(), g.data_ptr(),
-                               True, feat.ch, h * w * feat.ch, h, w, h, w, B, accumulate=True)
+                               True, feat.ch, h * w * feat.ch, h, w, h, w, B, accumulate=acc)
 
         self.tape.append(backward)
         return {k: losses[i] for i, k in enumerate(LOSS_KEYS)}

@@ -74,7 +74,7 @@ def ref_conv(x, conv, bn, act):
     return {"silu": F.silu, "relu": F.relu, "lrelu": lambda t: F.leaky_relu(t, 0.1), "none": lambda t: t}[act](y)
 
 
-def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_coff=0, out_c=None, tile=0):
+def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_coff=0, out_c=None, tile=0, flags=0):
     """srcs: list of (nhwc tensor [B,h,w,C], coff, ch, upsample)."""
     n = N()
     B = srcs[0][0].shape[0]
@@ -106,6 +106,7 @@ def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_cof
     d.dst_cstride, d.dst_bstride = out.shape[3], out.shape[1] * out.shape[2] * out.shape[3]
     d.act = n.ACT_CODE[act]
     d.tile = tile
+    d.flags = flags
     n.check(n.lib().yxh_conv2d(ctypes.byref(d), n.stream_ptr()), "conv2d")
     torch.cuda.synchronize()
     return out
@@ -591,10 +592,10 @@ R3_GEOMS = [  # cin, cout, s, H, W (input)
     (256, 256, 1, 10, 10), (128, 256, 2, 21, 19)]
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("geom", R3_GEOMS)
 def test_conv_r3_3x3(dtype, geom):
-    """conv_r3 (ids 113-128): every tile of the matching stride vs the fp32 reference;
+    """conv_r3 / conv_r3h (ids 113-150; fp32: the conv_r3h tiles): every tile of the matching stride vs the fp32 reference;
     zero padding comes from the buffer descriptor's range check (image borders, partial
     spatial tiles, channel tails of cout)."""
     cin, cout, s, H, W = geom
@@ -607,11 +608,35 @@ def test_conv_r3_3x3(dtype, geom):
         try:
             y = run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid)
         except NotImplementedError as e:
-            assert "stride" in str(e) or "multiple" in str(e), e
+            assert "stride" in str(e) or "multiple" in str(e) or (dtype == torch.float32 and "only" in str(e)), e
             continue
         close(y.permute(0, 3, 1, 2), want, dtype)
         ran += 1
-    assert ran >= 3
+    assert ran >= (1 if dtype == torch.float32 else 3)
+
+
+@pytest.mark.parametrize("s", [1, 2])
+def test_conv_r3h_fp32_accumulate(s):
+    """The training data-gradient form: fp32 conv_r3h accumulating into an fp32 dst
+    (YXH_CONV_ACCUMULATE), no bias/act, vs torch fp32."""
+    n = N()
+    conv, bn = make_conv(64, 48, 3, s, seed=11)
+    x = torch.randn(2, 64, 18, 22, generator=torch.Generator().manual_seed(12))
+    want_conv = ref_conv(x, conv, bn, "none")
+    base = torch.randn(want_conv.shape, generator=torch.Generator().manual_seed(13))
+    out = nhwc(base, torch.float32).contiguous()
+    ran = 0
+    for tid in (141, 142, 143, 144, 145, 150):
+        out.copy_(nhwc(base, torch.float32))
+        try:
+            run_conv([(nhwc(x, torch.float32), 0, 64, 0)], conv, bn, torch.float32, act="none", out=out, tile=2 * tid,
+                     flags=n.CONV_ACCUMULATE)
+        except NotImplementedError as e:
+            assert "stride" in str(e), e
+            continue
+        close(out.permute(0, 3, 1, 2), base + want_conv, torch.float32)
+        ran += 1
+    assert ran >= 1
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16])

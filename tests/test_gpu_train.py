@@ -239,6 +239,35 @@ def test_conv_wgrad_tiles(tile, dtype, cin0, cin1, up1, cout, k, s, H, B):
     assert rel(dw, wr.grad) < 1e-4  # fp32 accumulation of exact products: order-only differences
 
 
+@pytest.mark.parametrize("tile", [11, 12, 13, 14, 15, 16])
+@pytest.mark.parametrize("cin0,cin1,up1,cout,k,s,H,B", WG_TILE_CASES + [(16, 0, 0, 32, 3, 1, 40, 2)])
+def test_conv_wgrad9_fp32_tiles(tile, cin0, cin1, up1, cout, k, s, H, B):
+    """fp32 all-nine-taps weight gradient (tiles 11-16) against torch autograd: partial
+    pixel tiles at the image edges, cout / cin tails, stride 2; other geometries are
+    rejected (NotImplementedError) and run on tiles 1-4."""
+    g = torch.Generator().manual_seed(cin0 * 5 + cout + H + tile)
+    W = H + 4
+    p = (k - 1) // 2
+    x0 = torch.randn(B, H, W, cin0, generator=g)
+    oh, ow = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dyc = (cout + 3) // 4 * 4
+    dy = torch.randn(B, oh, ow, dyc, generator=g)
+    x0d, dyd = x0.cuda(), dy.cuda()
+    srcs = [src(x0d)]
+    if cin1:
+        srcs.append(src(torch.randn(B, H >> up1, W >> up1, cin1, generator=g).cuda(), up=up1))
+    try:
+        dw = wgrad(torch.float32, srcs, src(dyd), cout, cin0 + cin1, k, s, p, (H, W), (oh, ow), B, tile=tile)
+    except NotImplementedError as e:
+        assert k != 3 or cin1, e
+        return
+    assert k == 3 and not cin1
+    torch.cuda.synchronize()
+    wr = torch.zeros(cout, cin0, k, k, requires_grad=True)
+    F.conv2d(x0.permute(0, 3, 1, 2), wr, stride=s, padding=p).backward(dy[..., :cout].permute(0, 3, 1, 2))
+    assert rel(dw, wr.grad) < 1e-4
+
+
 def test_wgrad_cin_store_and_strided_dy():
     """Focus stem: 16 packed channels, gradient of the 12 real ones; dy read through a
     strided view (the head's [B, A, 8] pred-gradient rows)."""
