@@ -125,6 +125,13 @@ __global__ __launch_bounds__(256) void conv_pwf(ConvParams p, int ntn, int nk, i
     }
     const int k_split = nsrc == 2 ? p.src0_ch / (KCH * Chunk<T>::N) : nk;
     const int M = p.M;
+    // source 0 may be a nearest-x2 upsampled view (PAFPN cat(upsample(x), skip)): its rows
+    // are not linear in m, so each lane's row offsets are recomputed once per pixel tile
+    // (at the tile's first stage) instead of per stage
+    const bool up0 = p.sup[0] != 0;
+    uint32_t boffu[GB];
+#pragma unroll
+    for (int i = 0; i < GB; ++i) boffu[i] = 0;
 
     auto issue = [&](int st) {
         const int tl = st / nk, k = st - tl * nk;
@@ -135,8 +142,26 @@ __global__ __launch_bounds__(256) void conv_pwf(ConvParams p, int ntn, int nk, i
         for (int i = 0; i < GA; ++i) pwf_glds(wa, aoff[i], lbase + i * 4096);
         const bool s1 = k >= k_split;
         const uint32_t rb = s1 ? rb1 : rb0;
-        const char* xb = (const char*)p.sptr[s1 ? 1 : 0] + (long long)m0 * rb + (long long)(s1 ? k - k_split : k) * KSTB;
         const uint32_t lb = lbase + A_BYTES;
+        if (up0 && !s1) {
+            if (k == 0) {
+#pragma unroll
+                for (int i = 0; i < GB; ++i) {
+                    const int r = (wave + 4 * i) * RPI + prow;
+                    const int m = min(m0 + r, M - 1);
+                    const int b = m / p.ohw, pix = m - b * p.ohw;
+                    const int y = pix / p.out_w, x = pix - y * p.out_w;
+                    boffu[i] = (uint32_t)(((long long)b * p.sbs[0] + (long long)((y >> 1) * p.sw[0] + (x >> 1)) * p.scs[0]) *
+                                          ES) +
+                               (uint32_t)((pch ^ pwf_swz<KCH>(r)) * 16);
+                }
+            }
+            const char* xb = (const char*)p.sptr[0] + (long long)k * KSTB;
+#pragma unroll
+            for (int i = 0; i < GB; ++i) pwf_glds(xb, boffu[i], lb + i * 4096);
+            return;
+        }
+        const char* xb = (const char*)p.sptr[s1 ? 1 : 0] + (long long)m0 * rb + (long long)(s1 ? k - k_split : k) * KSTB;
         if (m0 + TM <= M) {
 #pragma unroll
             for (int i = 0; i < GB; ++i) pwf_glds(xb, s1 ? boff1[i] : boff0[i], lb + i * 4096);
@@ -293,13 +318,19 @@ static int pwf_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
 int conv_pwf_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st) {
     bool dense = p.taps == 1 && p.stride == 1 && p.pad == 0 && !p.dst_f32 && p.act < YXH_ACT_DECODE && p.dst_dense &&
                  (!p.res || p.res_dense) && p.vec_store && (!p.res || p.vec_res);
-    for (int s = 0; s < p.nsrc; ++s)
-        dense &= !p.sup[s] && p.sw[s] == p.out_w && p.sbs[s] == (long long)p.ohw * p.scs[s];
+    for (int s = 0; s < p.nsrc; ++s) {
+        if (s == 0 && p.sup[0] == 1)  // nearest-x2 upsampled first source: any image stride
+            dense &= p.sw[0] * 2 == p.out_w;
+        else
+            dense &= !p.sup[s] && p.sw[s] == p.out_w && p.sbs[s] == (long long)p.ohw * p.scs[s];
+    }
     if (!dense) {
-        set_error("conv_pwf needs a 1x1 s1 conv over dense sources into a dense 16-bit dst");
+        set_error("conv_pwf needs a 1x1 s1 conv over dense sources (the first may be x2 upsampled) into a dense "
+                  "16-bit dst");
         return YXH_EUNSUPPORTED;
     }
-    if ((long long)p.M * p.scs[0] * 2 >= (1LL << 32) || (p.nsrc == 2 && (long long)p.M * p.scs[1] * 2 >= (1LL << 32))) {
+    const long long img0 = p.sup[0] ? (p.M / p.ohw) * p.sbs[0] : (long long)p.M * p.scs[0];
+    if (img0 * 2 >= (1LL << 32) || (p.nsrc == 2 && (long long)p.M * p.scs[1] * 2 >= (1LL << 32))) {
         set_error("conv_pwf: source exceeds 32-bit byte offsets");
         return YXH_EUNSUPPORTED;
     }

@@ -21,7 +21,11 @@ namespace yxh {
 
 namespace {
 
-__device__ __forceinline__ float hd_sigmoid(float v) { return 1.0f / (1.0f + expf(-v)); }
+// The fused head runs on the 16-bit inference path only (the fp32 parity path keeps the
+// decode convs and their IEEE exp / divide): hardware exp2 + reciprocal (~1 ulp each), as
+// the bf16 SiLU -- the per-element exp / divide sequences were most of this kernel's VALU.
+__device__ __forceinline__ float hd_exp(float v) { return __builtin_amdgcn_exp2f(v * 1.4426950408889634f); }
+__device__ __forceinline__ float hd_sigmoid(float v) { return __builtin_amdgcn_rcpf(1.0f + hd_exp(-v)); }
 
 }  // namespace
 
@@ -36,8 +40,7 @@ __global__ __launch_bounds__(256) void head_pred(yxh_head_desc d) {
     constexpr int WROWS = NF * 16;        // weight rows in LDS
     constexpr int XB = TM * ROWB;         // one feature tile
     constexpr int WB = WROWS * ROWB;
-    constexpr int D = 5 + NCF * 16;       // staged row: 5 + C rounded up (C <= NCF * 16)
-    constexpr int STG = TM * D * 4;
+    constexpr int STG = TM * (5 + NCF * 16) * 4;  // staged rows, stride 5 + C (<= 5 + NCF * 16)
     __shared__ __attribute__((aligned(16))) char smem[2 * XB + WB + STG];
     char* xr = smem;            // reg_feat tile [TM][CIN] (chunks XOR-swizzled by row)
     char* xc = smem + XB;       // cls_feat tile
@@ -76,7 +79,7 @@ __global__ __launch_bounds__(256) void head_pred(yxh_head_desc d) {
             const int q = tid + 256 * k;
             const int r = q / CPR, c = q - r * CPR;
             int pix = p0 + min(r, M - 1 - m0), b = b0;
-            while (pix >= hw) {
+            while (pix >= hw) {  // levels smaller than a tile: several images per tile
                 pix -= hw;
                 ++b;
             }
@@ -118,7 +121,7 @@ __global__ __launch_bounds__(256) void head_pred(yxh_head_desc d) {
             while (pix >= hw) pix -= hw;
             const int gy = pix / d.w, gx = pix - gy * d.w;
             const float st = d.stride;
-            float* row = stg + pr * D;
+            float* row = stg + pr * rowf;
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
 #pragma unroll
@@ -129,7 +132,7 @@ __global__ __launch_bounds__(256) void head_pred(yxh_head_desc d) {
                         if (ch < 5) {
                             v += d.b_reg[ch];
                             if (ch < 2) v = (v + (float)(ch == 0 ? gx : gy)) * st;
-                            else if (ch < 4) v = expf(v) * st;
+                            else if (ch < 4) v = hd_exp(v) * st;
                             else v = d.train ? v : hd_sigmoid(v);
                             row[ch] = v;
                         }
@@ -145,29 +148,17 @@ __global__ __launch_bounds__(256) void head_pred(yxh_head_desc d) {
         }
         __syncthreads();
 
-        // ---- coalesced copy of the tile's rows: [m0, m0 + n) splits at image boundaries;
-        // each piece is contiguous in the output and 16-byte aligned
+        // ---- the staged rows have the output's row stride, so each piece of the tile (it
+        // splits at an image boundary) is one contiguous, 16-byte aligned run in both LDS and
+        // the output: a plain float4 copy
         const int n = min(TM, M - m0);
         int t0 = 0, b = b0, pix = p0;
         while (t0 < n) {
             const int cnt = min(n - t0, hw - pix);
             float* dst = d.out + (long long)b * d.out_bstride + (long long)(d.a_off + pix) * rowf;
+            const float* src = stg + t0 * rowf;
             const int total = cnt * rowf;  // floats, a multiple of 4 (cnt % 4 == 0)
-            for (int q = tid * 4; q < total; q += 1024) {
-                const int r = q / rowf, c = q - r * rowf;  // staged layout has row stride D
-                float4 v;
-                float* pv = (float*)&v;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    int rr = r, cc = c + e;
-                    if (cc >= rowf) {
-                        cc -= rowf;
-                        ++rr;
-                    }
-                    pv[e] = stg[(t0 + rr) * D + cc];
-                }
-                *(float4*)(dst + q) = v;
-            }
+            for (int q = tid * 4; q < total; q += 1024) *(float4*)(dst + q) = *(const float4*)(src + q);
             t0 += cnt;
             ++b;
             pix = 0;

@@ -587,6 +587,30 @@ def test_dense_pointwise_two_sources_slice_dst(dtype):
         assert out[..., :32].abs().max().item() == 0 and out[..., 128:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_pointwise_pwf_upsampled_first_source(dtype):
+    """conv_pwf over cat([upsample2x(a), b]) -- the PAFPN lateral 1x1 -- with `a` a channel
+    slice of a wider buffer: the upsampled source's row offsets are rebuilt per pixel tile
+    (incl. the pixel tail of the last tile)."""
+    a = torch.randn(3, 128, 5, 7)
+    b = torch.randn(3, 64, 10, 14)
+    conv, bn = make_conv(192, 64, 1, 1, seed=17)
+    want = ref_conv(torch.cat([F.interpolate(a, scale_factor=2, mode="nearest"), b], 1), conv, bn, "silu")
+    wide = torch.zeros(3, 5, 7, 192, dtype=dtype, device=DEV)
+    wide[..., 32:160] = nhwc(a, dtype)
+    Bt = nhwc(b, dtype)
+    ran = 0
+    for tid in range(97, 105):
+        try:
+            y = run_conv([(wide, 32, 128, 1), (Bt, 0, 64, 0)], conv, bn, dtype, tile=2 * tid)
+        except NotImplementedError as e:
+            assert "multiple" in str(e), e
+            continue
+        close(y.permute(0, 3, 1, 2), want, dtype)
+        ran += 1
+    assert ran >= 4
+
+
 R3_GEOMS = [  # cin, cout, s, H, W (input)
     (64, 96, 1, 11, 13), (32, 64, 1, 83, 41), (128, 64, 1, 20, 20), (64, 128, 2, 40, 40), (32, 48, 2, 17, 35),
     (256, 256, 1, 10, 10), (128, 256, 2, 21, 19)]
