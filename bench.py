@@ -322,7 +322,7 @@ def main_train(args, world, rank):
     dt = time.perf_counter() - t0
     dt_max = max_over_ranks(dt, world)
     gpu_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    loss = float(out["total_loss"])
+    loss = float(out["total_loss"].detach())
     if rank != 0:
         if world > 1:
             import torch.distributed as dist
