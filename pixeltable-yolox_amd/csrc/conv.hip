@@ -6,7 +6,7 @@
 //                 of one input pixel (bf16/f16; 4 for fp32).
 //  dwconv       : depthwise 3x3 (DWConv.dconv, nano) -- HBM-bound, VALU.
 //  focus_pack   : Focus space-to-depth of the network input into 16-ch NHWC.
-//  spp_maxpool  : SPP 5/9/13 max pools, separable, one LDS plane per 16-B chunk.
+//  spp_maxpool  : SPP 5/9/13 max pools, separable, LDS planes of 1-4 16-B chunks per pixel.
 //  fold_bn_pack : BN folding + [cout][kh][kw][cin] repack of the weights.
 //
 // Reference call sites: network_blocks.py:27-208 (BaseConv, DWConv, Bottleneck,
@@ -262,37 +262,44 @@ __device__ __forceinline__ uint4 vmax(uint4 a, uint4 b) {
     return r;
 }
 
-// One block per (16-byte channel chunk, image): horizontal 5/9/13 maxima into LDS,
-// then vertical.  max_pool2d pads with -inf, i.e. out-of-range taps are skipped.
-template <typename T>
+// One block per (CPB consecutive 16-byte channel chunks, image): horizontal 5/9/13 maxima
+// into LDS, then vertical.  max_pool2d pads with -inf, i.e. out-of-range taps are skipped.
+// Lanes run over (pixel, chunk) with the chunk fastest, so each pixel's CPB chunks are one
+// contiguous 16*CPB-byte segment of the NHWC row (one 16-byte chunk per block read and
+// wrote 400 scattered 16-byte pieces per plane: 36 us for a 6.5 MB tensor).
+template <typename T, int CPB>
 __global__ __launch_bounds__(256) void spp_maxpool(T* buf, int H, int W, int C, int cs, long long bs) {
     constexpr int EPC = Chunk<T>::N;
     extern __shared__ __attribute__((aligned(16))) uint4 sm[];
-    const int HW = H * W;
-    uint4* P = sm;
-    uint4* H5 = sm + HW;
-    uint4* H9 = sm + 2 * HW;
-    uint4* H13 = sm + 3 * HW;
-    const int c0 = blockIdx.x * EPC;
+    const int HW = H * W, N = HW * CPB;
+    uint4* P = sm;  // [pixel][chunk]
+    uint4* H5 = sm + N;
+    uint4* H9 = sm + 2 * N;
+    uint4* H13 = sm + 3 * N;
+    const int c0 = blockIdx.x * EPC * CPB;
     T* base = buf + blockIdx.y * bs;
-    for (int q = threadIdx.x; q < HW; q += blockDim.x) P[q] = *(const uint4*)(base + (long long)q * cs + c0);
+    for (int q = threadIdx.x; q < N; q += blockDim.x) {
+        const int px = q / CPB, ch = q - px * CPB;
+        P[q] = *(const uint4*)(base + (long long)px * cs + c0 + ch * EPC);
+    }
     __syncthreads();
-    for (int q = threadIdx.x; q < HW; q += blockDim.x) {
-        const int y = q / W, x = q - y * W;
+    for (int q = threadIdx.x; q < N; q += blockDim.x) {
+        const int px = q / CPB;
+        const int y = px / W, x = px - y * W;
         uint4 m5 = P[q];
         for (int d = 1; d <= 2; ++d) {
-            if (x - d >= 0) m5 = vmax<T>(m5, P[q - d]);
-            if (x + d < W) m5 = vmax<T>(m5, P[q + d]);
+            if (x - d >= 0) m5 = vmax<T>(m5, P[q - d * CPB]);
+            if (x + d < W) m5 = vmax<T>(m5, P[q + d * CPB]);
         }
         uint4 m9 = m5;
         for (int d = 3; d <= 4; ++d) {
-            if (x - d >= 0) m9 = vmax<T>(m9, P[q - d]);
-            if (x + d < W) m9 = vmax<T>(m9, P[q + d]);
+            if (x - d >= 0) m9 = vmax<T>(m9, P[q - d * CPB]);
+            if (x + d < W) m9 = vmax<T>(m9, P[q + d * CPB]);
         }
         uint4 m13 = m9;
         for (int d = 5; d <= 6; ++d) {
-            if (x - d >= 0) m13 = vmax<T>(m13, P[q - d]);
-            if (x + d < W) m13 = vmax<T>(m13, P[q + d]);
+            if (x - d >= 0) m13 = vmax<T>(m13, P[q - d * CPB]);
+            if (x + d < W) m13 = vmax<T>(m13, P[q + d * CPB]);
         }
         (void)y;
         H5[q] = m5;
@@ -300,26 +307,28 @@ __global__ __launch_bounds__(256) void spp_maxpool(T* buf, int H, int W, int C, 
         H13[q] = m13;
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < HW; q += blockDim.x) {
-        const int y = q / W;
+    const int row = W * CPB;
+    for (int q = threadIdx.x; q < N; q += blockDim.x) {
+        const int px = q / CPB, ch = q - px * CPB;
+        const int y = px / W;
         uint4 o5 = H5[q], o9 = H9[q], o13 = H13[q];
         for (int d = 1; d <= 6; ++d) {
             const bool up = y - d >= 0, dn = y + d < H;
             if (d <= 2) {
-                if (up) o5 = vmax<T>(o5, H5[q - d * W]);
-                if (dn) o5 = vmax<T>(o5, H5[q + d * W]);
+                if (up) o5 = vmax<T>(o5, H5[q - d * row]);
+                if (dn) o5 = vmax<T>(o5, H5[q + d * row]);
             }
             if (d <= 4) {
-                if (up) o9 = vmax<T>(o9, H9[q - d * W]);
-                if (dn) o9 = vmax<T>(o9, H9[q + d * W]);
+                if (up) o9 = vmax<T>(o9, H9[q - d * row]);
+                if (dn) o9 = vmax<T>(o9, H9[q + d * row]);
             }
-            if (up) o13 = vmax<T>(o13, H13[q - d * W]);
-            if (dn) o13 = vmax<T>(o13, H13[q + d * W]);
+            if (up) o13 = vmax<T>(o13, H13[q - d * row]);
+            if (dn) o13 = vmax<T>(o13, H13[q + d * row]);
         }
-        T* px = base + (long long)q * cs + c0;
-        *(uint4*)(px + C) = o5;
-        *(uint4*)(px + 2 * C) = o9;
-        *(uint4*)(px + 3 * C) = o13;
+        T* pp = base + (long long)px * cs + c0 + ch * EPC;
+        *(uint4*)(pp + C) = o5;
+        *(uint4*)(pp + 2 * C) = o9;
+        *(uint4*)(pp + 3 * C) = o13;
     }
 }
 
@@ -562,18 +571,35 @@ int spp_launch(void* buf, int dt, int B, int H, int W, int C, int cs, long long 
     const int es = elem_size(dt), epc = 16 / es;
     YXH_CHECK_ARG(dt == YXH_F32 || dt == YXH_BF16 || dt == YXH_F16, "spp dtype");
     YXH_CHECK_ARG(C % epc == 0 && cs % epc == 0 && bs % epc == 0 && cs >= 4 * C, "spp channels/strides");
-    const size_t lds = (size_t)4 * H * W * 16;
-    YXH_CHECK_ARG(lds <= 160 * 1024, "spp plane %dx%d too large for LDS", H, W);
-    dim3 grid(C / epc, B);
-#define YXH_SPP(T)                                                                                       \
+    const int nch = C / epc;
+    const size_t plane = (size_t)4 * H * W * 16;
+    YXH_CHECK_ARG(plane <= 160 * 1024, "spp plane %dx%d too large for LDS", H, W);
+    // chunks per block: the widest of 4 / 2 that divides the channels, fits LDS and still
+    // leaves >= 512 blocks (two per CU); else 1
+    int cpb = 1;
+    for (int c = 4; c >= 2; c /= 2)
+        if (nch % c == 0 && c * plane <= 160 * 1024 && (long long)(nch / c) * B >= 512) {
+            cpb = c;
+            break;
+        }
+    const size_t lds = plane * cpb;
+    dim3 grid(nch / cpb, B);
+#define YXH_SPP(T, CPB)                                                                                  \
     do {                                                                                                 \
-        (void)hipFuncSetAttribute((const void*)spp_maxpool<T>,                                         \
+        (void)hipFuncSetAttribute((const void*)spp_maxpool<T, CPB>,                                    \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                    \
-        hipLaunchKernelGGL(spp_maxpool<T>, grid, dim3(256), lds, st, (T*)buf, H, W, C, cs, bs);          \
+        hipLaunchKernelGGL((spp_maxpool<T, CPB>), grid, dim3(256), lds, st, (T*)buf, H, W, C, cs, bs);   \
     } while (0)
-    if (dt == YXH_BF16) YXH_SPP(bf16);
-    else if (dt == YXH_F16) YXH_SPP(f16);
-    else YXH_SPP(float);
+#define YXH_SPP_T(T)                 \
+    do {                             \
+        if (cpb == 4) YXH_SPP(T, 4);     \
+        else if (cpb == 2) YXH_SPP(T, 2); \
+        else YXH_SPP(T, 1);          \
+    } while (0)
+    if (dt == YXH_BF16) YXH_SPP_T(bf16);
+    else if (dt == YXH_F16) YXH_SPP_T(f16);
+    else YXH_SPP_T(float);
+#undef YXH_SPP_T
 #undef YXH_SPP
     YXH_CHECK_LAUNCH("spp launch");
     return YXH_OK;

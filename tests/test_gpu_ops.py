@@ -183,15 +183,16 @@ def test_depthwise(dtype, s):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("hw", [(20, 20), (13, 7), (40, 40)])
-def test_spp_maxpool(dtype, hw):
+@pytest.mark.parametrize("hw,B,C", [((20, 20), 2, 32), ((13, 7), 2, 32), ((40, 40), 2, 32),
+                                    ((20, 20), 32, 256), ((20, 20), 64, 512)])
+def test_spp_maxpool(dtype, hw, B, C):
+    """bit-exact vs torch max_pool2d; the batch-32/64 cases take the 2- and 4-chunk blocks."""
     n = N()
     H, W = hw
-    C = 32
-    x = torch.randn(2, C, H, W)
-    buf = torch.zeros(2, H, W, 4 * C, dtype=dtype, device=DEV)
+    x = torch.randn(B, C, H, W)
+    buf = torch.zeros(B, H, W, 4 * C, dtype=dtype, device=DEV)
     buf[..., :C] = nhwc(x, dtype)
-    n.check(n.lib().yxh_spp_maxpool(buf.data_ptr(), n.DTYPE_CODE[dtype], 2, H, W, C, 4 * C, H * W * 4 * C,
+    n.check(n.lib().yxh_spp_maxpool(buf.data_ptr(), n.DTYPE_CODE[dtype], B, H, W, C, 4 * C, H * W * 4 * C,
                                     n.stream_ptr()), "spp")
     torch.cuda.synchronize()
     xr = x.to(dtype).float()
