@@ -518,7 +518,7 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         YXH_CHECK_ARG((tile > 0 && tile < kNumTiles) || (tile > 16 && tile < 16 + kNumTiles) ||
                           (tile > 32 && tile <= 32 + kNumRowTiles) || (tile > 64 && tile <= 64 + kNumPwTiles) ||
                           (tile > 80 && tile <= 80 + kNumPwrTiles) || (tile > 96 && tile <= 96 + kNumPwfTiles) ||
-                          (tile > 112 && tile <= 112 + kNumR3Tiles),
+                          (tile > 112 && tile <= 112 + kNumR3Tiles) || (tile > 160 && tile <= 160 + kNumWsTiles),
                       "tile %d", d->tile);
         YXH_CHECK_ARG(want_ks == 1 || ks == 2, "2-slab staging not possible for this conv");
         ks = want_ks;
@@ -529,6 +529,7 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         set_error("dilated (upsample == 2) sources run on the register-staged kernel only (tile ids 1-9)");
         return YXH_EUNSUPPORTED;
     }
+    if (tile > 160) return conv_ws_dispatch(dt, tile - 160, p, st);
     if (tile > 112) return conv_r3_dispatch(dt, tile - 112, p, st);
     if (tile > 96) return conv_pwf_dispatch(dt, tile - 96, p, st);
     if (tile > 80) return conv_pwr_dispatch(dt, tile - 80, p, st);

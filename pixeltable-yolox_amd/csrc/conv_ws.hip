@@ -1,0 +1,314 @@
+// conv_ws: weight-stationary 3x3 conv (stride 1 or 2, pad 1) for 16-bit types.
+// Reference: network_blocks.py:48-49 (BaseConv, ksize 3) as used by darknet.py:148-156
+// (stage downsampling), network_blocks.py:77-99 (Bottleneck conv2), yolo_pafpn.py:55-80
+// (bu_conv1/2) and yolo_head.py:57-104 (cls/reg convs).
+//
+// conv_r3 / conv_r3h stream the weights of their TN output channels through LDS for
+// every pixel tile, and that weight DMA is what bounds them. Here a block
+// is persistent and keeps its weights in VGPRs for its whole life: it loads them once,
+// then walks pixel tiles. Per tile the only DMA is the input halo and the only LDS reads
+// are the pixel fragments (half a ds_read_b128 per MFMA at FR = 2).
+//
+// Block: NW = WN x WK x WM waves. Wave (wn, wk, wm) holds output channels
+// n0 + wn*WTN .. +WTN (FR = WTN/16 fragments) x input channel blocks wk*WCB .. +WCB
+// (32 channels each) x all nine taps = FR*9*WCB*4 VGPRs, and computes pixel fragments
+// wm*FC .. +FC of the TX x TY output tile. WK > 1 splits K: partial sums meet in LDS and
+// each of the WK waves finishes every WK-th pixel fragment.
+// Halo image in LDS: pixel (hy, hx) at hp = hy*HXP + hx, PS 16-byte slots per pixel.
+// PS = 2 x odd (stride 1) / odd (stride 2) and HXP = TX mod 8 when fragments cross tile
+// rows make the 16 pixels of a fragment hit distinct bank groups of ds_read_b128.
+// Two halo buffers: tile k+1 lands by LDS-DMA while tile k computes.
+#include "conv_common.hpp"
+#include "lds_dma.hpp"
+
+namespace yxh {
+
+namespace {
+
+constexpr int ws_ps(int c16, int s) {
+    return s == 1 ? c16 + (6 - c16 % 4) % 4 : (c16 % 2 ? c16 : c16 + 1);
+}
+constexpr int ws_hxp(int tx, int s) {
+    const int hx = (tx - 1) * s + 3;
+    if (tx % 16 == 0) return hx;
+    int h = hx;
+    while (h % 8 != tx % 8) ++h;
+    return h;
+}
+
+}  // namespace
+
+template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM>
+__global__ __launch_bounds__(64 * WN * WK * WM, 1) void conv_ws(ConvParams p, int tiles_x, int tiles_y,
+                                                                 int ntiles, int ntn, int nwork) {
+    static_assert(sizeof(T) == 2, "16-bit operands");
+    constexpr int NW = WN * WK * WM;
+    constexpr int NCB = CIN / 32, WCB = NCB / WK;
+    constexpr int WTN = TN / WN, FR = WTN / 16;
+    constexpr int TM = TX * TY, WTM = TM / WM, FC = WTM / 16;
+    constexpr int HX = (TX - 1) * S + 3, HY = (TY - 1) * S + 3, HXP = ws_hxp(TX, S);
+    constexpr int C16 = CIN / 8, PS = ws_ps(C16, S), PSB = PS * 16;
+    constexpr int SLOTS = HY * HXP * PS, LOADS = (SLOTS + 63) / 64, GB = (LOADS + NW - 1) / NW;
+    constexpr int HBYTES = LOADS * 1024;
+    // partial sums: fragment j of wave group (wn, wm) is finished by wave wk = j % WK; the
+    // WK - 1 others each leave their part in a slot of their own
+    constexpr int RBYTES = WK > 1 ? WN * WM * FR * FC * (WK - 1) * 1024 : 0;
+    constexpr int SMEM = 2 * HBYTES + RBYTES;
+    static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0 && TM % (16 * WM) == 0, "tile");
+    static_assert(FR * 9 * WCB * 4 <= 160, "weights must stay in VGPRs");
+    static_assert(SMEM <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave % WN, wk = (wave / WN) % WK, wm = wave / (WN * WK);
+    const int frow = lane & 15, fq = lane >> 4;
+    const int bid = dma::xcd_remap(blockIdx.x, gridDim.x);
+    const int nt = bid % ntn, worker = bid / ntn;
+    const int n0 = nt * TN;
+    const int tile = worker;
+    if (tile >= ntiles) return;  // block-uniform
+
+    const int cin_ = p.cin, cout = p.cout, in_w = p.in_w, in_h = p.in_h, scs = p.scs[0];
+    const int OH = p.out_h, OW = p.out_w, ohw = p.ohw;
+    (void)cin_;
+
+    // ---- stationary weights: a[i][tap][c] = 16 channels x 32 K of fragment i
+    uint4 a[FR][9][WCB];
+    {
+        const T* w = (const T*)p.w;
+#pragma unroll
+        for (int i = 0; i < FR; ++i) {
+            const int n = min(n0 + wn * WTN + i * 16 + frow, cout - 1);
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+                for (int c = 0; c < WCB; ++c)
+                    a[i][tap][c] = *(const uint4*)(w + ((long long)n * 9 + tap) * CIN + (wk * WCB + c) * 32 + fq * 8);
+        }
+    }
+    float bias[FR][4];
+#pragma unroll
+    for (int i = 0; i < FR; ++i) {
+        const int n = n0 + wn * WTN + i * 16 + fq * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[i][r] = n + r < cout ? p.bias[n + r] : 0.0f;
+    }
+
+    // ---- this lane's LDS byte offsets of its pixel fragments at tap (0, 0), channel block 0
+    uint32_t boff[FC];
+#pragma unroll
+    for (int j = 0; j < FC; ++j) {
+        const int pl = (wm * FC + j) * 16 + frow;
+        const int ty = pl / TX, tx = pl - ty * TX;
+        boff[j] = (uint32_t)((ty * S * HXP + tx * S) * PSB + (wk * WCB * 4 + fq) * 16);
+    }
+
+    const uint32_t lds0 = dma::lds_addr(smem);
+    const uint32_t bytes = (uint32_t)((long long)in_h * in_w * scs * 2);
+
+    auto issue_halo = [&](int t, int kb) {
+        const int tx_i = t % tiles_x, r = t / tiles_x;
+        const int ty_i = r % tiles_y, b = r / tiles_y;
+        const int iy0 = ty_i * TY * S - 1, ix0 = tx_i * TX * S - 1;
+        const dma::u32x4 rsrc = dma::srd((const T*)p.sptr[0] + (long long)b * p.sbs[0], bytes);
+#pragma unroll
+        for (int i = 0; i < GB; ++i) {
+            const int L = wave + NW * i;
+            if (LOADS % NW == 0 || i + 1 < GB || L < LOADS) {
+                const int s = 64 * L + lane;
+                const int hp = s / PS, c16 = s - hp * PS;
+                const int hy = hp / HXP, hx = hp - hy * HXP;
+                const int iy = iy0 + hy, ix = ix0 + hx;
+                const bool ok = s < SLOTS && c16 < C16 && hx < HX && iy >= 0 && iy < in_h && ix >= 0 && ix < in_w;
+                const uint32_t voff = ok ? (uint32_t)(((iy * in_w + ix) * scs + c16 * 8) * 2) : dma::kOob;
+                dma::load16(rsrc, voff, 0u, __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(kb * HBYTES + L * 1024)));
+            }
+        }
+    };
+
+    const bool silu = p.act == YXH_ACT_SILU;
+    const T* res = (const T*)p.res;
+    T* dst = (T*)p.dst;
+
+    // one tile: wait for its halo, start the next tile's halo, MMA, (K-split reduce), epilogue
+    auto tile_step = [&](const int tile, const int k) -> int {
+        const int kb = k & 1;
+        const int next = tile + nwork;
+        dma::wait_vm<0>();
+        dma::barrier();
+        if (next < ntiles) issue_halo(next, kb ^ 1);
+
+        f32x4 acc[FR][FC];
+#pragma unroll
+        for (int i = 0; i < FR; ++i)
+#pragma unroll
+            for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* hb = smem + kb * HBYTES;
+        // K steps s = (channel block c, tap); the pixel fragments of step s + 1 are read
+        // before the MFMAs of step s, so the LDS latency hides behind them
+        constexpr int NS = WCB * 9;
+        uint4 bf[2][FC];
+        auto load_b = [&](int s, uint4 (&d)[FC]) {
+            const int c = s / 9, tap = s - 9 * (s / 9);
+            const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+            const int so = (ky * HXP + kx) * PSB + c * 64;
+#pragma unroll
+            for (int j = 0; j < FC; ++j) d[j] = *(const uint4*)(hb + boff[j] + so);
+        };
+        load_b(0, bf[0]);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (s + 1 < NS) load_b(s + 1, bf[(s + 1) & 1]);
+            const int c = s / 9, tap = s - 9 * (s / 9);
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], a[i][tap][c], bf[s & 1][j]);
+        }
+
+        // ---- K-split: partial sums of the fragments other waves finish go through LDS
+        if constexpr (WK > 1) {
+            char* red = smem + 2 * HBYTES;
+            const int grp = wm * WN + wn;  // waves sharing (wn, wm)
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j) {
+                    const int own = j % WK;
+                    if (own != wk) {
+                        const int slot = wk < own ? wk : wk - 1;
+                        *(f32x4*)(red + (((grp * FR + i) * FC + j) * (WK - 1) + slot) * 1024 + lane * 16) = acc[i][j];
+                    }
+                }
+            dma::barrier();
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j)
+                    if (j % WK == wk) {
+#pragma unroll
+                        for (int o = 0; o < WK - 1; ++o) {
+                            const f32x4 v = *(const f32x4*)(red + (((grp * FR + i) * FC + j) * (WK - 1) + o) * 1024 + lane * 16);
+                            acc[i][j] += v;
+                        }
+                    }
+        }
+
+        // ---- epilogue: bias, SiLU, residual, 8-byte stores of 4 channels (dispatch checks
+        // the dtype / alignment / activation this form assumes)
+        const int tx_i = tile % tiles_x, r = tile / tiles_x;
+        const int ty_i = r % tiles_y, b = r / tiles_y;
+        const int oy0 = ty_i * TY, ox0 = tx_i * TX;
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+            if (WK > 1 && j % WK != wk) continue;
+            const int pl = (wm * FC + j) * 16 + frow;
+            const int ty = pl / TX, tx = pl - ty * TX;
+            const int oy = oy0 + ty, ox = ox0 + tx;
+            if (oy >= OH || ox >= OW) continue;
+            const int pix = oy * OW + ox;
+#pragma unroll
+            for (int i = 0; i < FR; ++i) {
+                const int n = n0 + wn * WTN + i * 16 + fq * 4;
+                if (n >= cout) continue;
+                float v[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    v[q] = acc[i][j][q] + bias[i][q];
+                    if (silu) v[q] = yxh::silu<false>(v[q]);
+                }
+                if (res) {
+                    const uint2 u = *(const uint2*)(res + (long long)b * p.res_bs + (long long)pix * p.res_cs + n);
+                    T t[4];
+                    __builtin_memcpy(t, &u, 8);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] += to_f32(t[q]);
+                }
+                T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
+                uint2 u;
+                __builtin_memcpy(&u, t, 8);
+                *(uint2*)(dst + (long long)b * p.dst_bs + (long long)pix * p.dst_cs + n) = u;
+            }
+        }
+        return next;
+    };
+
+    issue_halo(tile, 0);
+    // the first tile is peeled off the loop: it consumes the weight loads, so the loop body
+    // carries no compiler-visible pending load whose wait would also drain the halo DMA
+    int next = tile_step(tile, 0);
+    for (int k = 1; next < ntiles; ++k) next = tile_step(next, k);
+    (void)ohw;
+}
+
+template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC = 1>
+static int launch_ws(const ConvParams& p, hipStream_t st) {
+    if (p.stride != S || p.cin != CIN) {
+        set_error("conv_ws variant built for stride %d, %d input channels", S, CIN);
+        return YXH_EUNSUPPORTED;
+    }
+    if (p.dst_f32 || p.accum || (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) || !p.vec_store ||
+        (p.res && !p.vec_res) || p.cout % 4) {
+        set_error("conv_ws: 16-bit dst, SiLU/no activation, 8-byte aligned dst/residual rows only");
+        return YXH_EUNSUPPORTED;
+    }
+    const int tiles_x = (p.out_w + TX - 1) / TX, tiles_y = (p.out_h + TY - 1) / TY;
+    const long long ntiles = (long long)tiles_x * tiles_y * (p.M / p.ohw);
+    const int ntn = (p.cout + TN - 1) / TN;
+    if (ntiles >= (1LL << 30)) {
+        set_error("conv_ws: too many tiles");
+        return YXH_EINVAL;
+    }
+    const int nwork = (int)std::min<long long>(ntiles, std::max(1, 256 * BPC / ntn));
+    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM>), dim3((unsigned)(nwork * ntn)),
+                       dim3(64 * WN * WK * WM), 0, st, p, tiles_x, tiles_y, (int)ntiles, ntn, nwork);
+    YXH_CHECK_LAUNCH("conv_ws launch");
+    return YXH_OK;
+}
+
+template <typename T>
+static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
+    // id -> (CIN, stride, TX, TY, TN, WN, WK, WM[, blocks per CU])
+    switch (id) {
+        // 32 input channels: dark2 bottleneck 3x3 (160x160), dark2 downsample (s2 -> 64)
+        case 1: return launch_ws<T, 32, 1, 16, 8, 32, 1, 1, 4>(p, st);
+        case 2: return launch_ws<T, 32, 1, 16, 16, 32, 1, 1, 8>(p, st);
+        case 3: return launch_ws<T, 32, 2, 16, 8, 64, 2, 1, 4>(p, st);
+        case 4: return launch_ws<T, 32, 2, 16, 4, 64, 2, 1, 2, 2>(p, st);
+        // 64 input channels: dark3 bottleneck 3x3 (80x80), dark3 downsample (s2 -> 128)
+        case 5: return launch_ws<T, 64, 1, 16, 8, 64, 2, 1, 4>(p, st);
+        case 6: return launch_ws<T, 64, 1, 16, 4, 64, 2, 1, 2, 2>(p, st);
+        case 7: return launch_ws<T, 64, 2, 16, 4, 128, 4, 1, 2>(p, st);
+        case 8: return launch_ws<T, 64, 2, 16, 2, 128, 4, 1, 1, 2>(p, st);
+        // 128 input channels: 40x40 / 80x80 / 20x20 3x3s (dark4, PAFPN, head), s2 128 -> 128/256
+        case 9: return launch_ws<T, 128, 1, 16, 4, 128, 4, 2, 1>(p, st);
+        case 10: return launch_ws<T, 128, 1, 16, 8, 64, 2, 2, 1>(p, st);
+        case 11: return launch_ws<T, 128, 1, 8, 4, 128, 4, 2, 1>(p, st);
+        case 12: return launch_ws<T, 128, 1, 8, 8, 64, 2, 2, 1>(p, st);
+        case 13: return launch_ws<T, 128, 2, 16, 2, 128, 4, 2, 1>(p, st);
+        case 14: return launch_ws<T, 128, 2, 8, 4, 128, 4, 2, 1>(p, st);
+        case 15: return launch_ws<T, 128, 1, 16, 4, 64, 2, 2, 1>(p, st);
+        // 256 input channels: dark5 / PAFPN / yolox_l head 3x3s (K split four ways)
+        case 16: return launch_ws<T, 256, 1, 8, 4, 64, 2, 4, 1>(p, st);
+        case 17: return launch_ws<T, 256, 1, 16, 2, 64, 2, 4, 1>(p, st);
+        default: set_error("conv_ws tile id %d", id); return YXH_EINVAL;
+    }
+}
+
+int conv_ws_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st) {
+    if (p.taps != 9 || p.kw != 3 || p.pad != 1 || p.nsrc != 1 || p.sup[0] || p.sw[0] != p.in_w) {
+        set_error("conv_ws needs a 3x3 pad-1 conv over one plain source");
+        return YXH_EUNSUPPORTED;
+    }
+    if ((long long)p.in_h * p.in_w * p.scs[0] * 2 >= (1LL << 31)) {
+        set_error("conv_ws: image exceeds 31-bit byte offsets");
+        return YXH_EUNSUPPORTED;
+    }
+    if (dtype == YXH_BF16) return ws_dispatch_t<bf16>(id, p, st);
+    if (dtype == YXH_F16) return ws_dispatch_t<f16>(id, p, st);
+    set_error("conv_ws is built for bf16/f16");
+    return YXH_EUNSUPPORTED;
+}
+
+}  // namespace yxh

@@ -678,6 +678,50 @@ def test_conv_r3_residual_and_strided_dst(dtype):
         close(y[..., 64:].permute(0, 3, 1, 2), want, dtype)
 
 
+WS_GEOMS = [  # cin, cout, s, H, W (input), batch
+    (32, 32, 1, 37, 45, 3), (32, 64, 2, 66, 70, 2), (64, 64, 1, 80, 80, 8), (64, 128, 2, 42, 38, 2),
+    (128, 128, 1, 40, 40, 16), (128, 256, 1, 20, 22, 2), (128, 96, 2, 41, 40, 2), (256, 256, 1, 20, 20, 4),
+    (256, 64, 1, 9, 11, 2)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("geom", WS_GEOMS)
+def test_conv_ws_3x3(dtype, geom):
+    """conv_ws (ids 161-177): weight-stationary persistent 3x3 conv, every variant built for
+    this (cin, stride) vs the fp32 reference: partial spatial tiles, cout tails, several
+    tiles per persistent block, K split over waves, a channel-slice source."""
+    cin, cout, s, H, W, B = geom
+    conv, bn = make_conv(cin, cout, 3, s, seed=cin + cout + s)
+    x = torch.randn(B, cin, H, W, generator=torch.Generator().manual_seed(H + W))
+    want = ref_conv(x, conv, bn, "silu")
+    wide = torch.zeros(B, H, W, cin + 32, dtype=dtype, device=DEV)
+    wide[..., 16:16 + cin] = nhwc(x, dtype)
+    ran = 0
+    for tid in range(161, 178):
+        try:
+            y = run_conv([(wide, 16, cin, 0)], conv, bn, dtype, tile=2 * tid)
+        except NotImplementedError as e:
+            assert "input channels" in str(e), e
+            continue
+        close(y.permute(0, 3, 1, 2), want, dtype)
+        ran += 1
+    assert ran >= 1
+
+
+def test_conv_ws_residual_and_strided_dst():
+    dtype = torch.bfloat16
+    conv, bn = make_conv(64, 64, 3, 1, seed=3)
+    x = torch.randn(3, 64, 24, 40, generator=torch.Generator().manual_seed(4))
+    r = torch.randn(3, 64, 24, 40, generator=torch.Generator().manual_seed(5))
+    want = ref_conv(x, conv, bn, "silu") + r.to(dtype).float()
+    buf = torch.zeros(3, 24, 40, 128, dtype=dtype, device=DEV)
+    for tid in (165, 166):
+        buf[..., 64:] = nhwc(r, dtype)
+        y = run_conv([(nhwc(x, dtype), 0, 64, 0)], conv, bn, dtype, residual=(buf, 64), out=buf, out_coff=64,
+                     tile=2 * tid)
+        close(y[..., 64:].permute(0, 3, 1, 2), want, dtype)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("cin,h,w,train", [(128, 8, 12, 0), (64, 20, 20, 0), (256, 4, 8, 1), (128, 10, 10, 1)])
 def test_head_pred_fused_level(dtype, cin, h, w, train):
