@@ -266,6 +266,6 @@ int conv_r3_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumR3Tiles = 48;  // ids beyond the built ones report EINVAL
 // Weight-stationary persistent 3x3 conv (conv_ws.hip): tile ids 161..160+kNumWsTiles
 int conv_ws_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
-constexpr int kNumWsTiles = 17;
+constexpr int kNumWsTiles = 24;
 
 }  // namespace yxh

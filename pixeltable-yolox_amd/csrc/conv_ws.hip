@@ -21,6 +21,12 @@
 #include "conv_common.hpp"
 #include "lds_dma.hpp"
 
+// Probe builds only (tools/ws_split.sh): 1 = no epilogue stores, 2 = no halo DMA after the
+// first tile, 3 = both
+#ifndef YXH_WS_PROBE
+#define YXH_WS_PROBE 0
+#endif
+
 namespace yxh {
 
 namespace {
@@ -38,8 +44,8 @@ constexpr int ws_hxp(int tx, int s) {
 
 }  // namespace
 
-template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM>
-__global__ __launch_bounds__(64 * WN * WK * WM, 1) void conv_ws(ConvParams p, int tiles_x, int tiles_y,
+template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC>
+__global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, int tiles_x, int tiles_y,
                                                                  int ntiles, int ntn, int nwork) {
     static_assert(sizeof(T) == 2, "16-bit operands");
     constexpr int NW = WN * WK * WM;
@@ -53,7 +59,13 @@ __global__ __launch_bounds__(64 * WN * WK * WM, 1) void conv_ws(ConvParams p, in
     // partial sums: fragment j of wave group (wn, wm) is finished by wave wk = j % WK; the
     // WK - 1 others each leave their part in a slot of their own
     constexpr int RBYTES = WK > 1 ? WN * WM * FR * FC * (WK - 1) * 1024 : 0;
-    constexpr int SMEM = 2 * HBYTES + RBYTES;
+    // residual tile staging (stride-1 variants: the Bottleneck's shortcut): TM pixels x TN
+    // channels by LDS-DMA with the halo, one 16-byte pad slot per pixel row, a ring of three
+    // (the epilogue of tile k-1 runs during tile k while tile k+1 lands)
+    constexpr int RS = TN / 8 + 1, RSLOTS = S == 1 ? TM * RS : 0;
+    constexpr int RLOADS = (RSLOTS + 63) / 64, GR = (RLOADS + NW - 1) / NW, RTB = RLOADS * 1024;
+    constexpr int SMEM = 2 * HBYTES + RBYTES + 3 * RTB;
+    constexpr int FCO = (FC + WK - 1) / WK;  // pixel fragments this wave finishes
     static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0 && TM % (16 * WM) == 0, "tile");
     static_assert(FR * 9 * WCB * 4 <= 160, "weights must stay in VGPRs");
     static_assert(SMEM <= 160 * 1024, "LDS");
@@ -107,37 +119,143 @@ __global__ __launch_bounds__(64 * WN * WK * WM, 1) void conv_ws(ConvParams p, in
     const uint32_t lds0 = dma::lds_addr(smem);
     const uint32_t bytes = (uint32_t)((long long)in_h * in_w * scs * 2);
 
-    auto issue_halo = [&](int t, int kb) {
-        const int tx_i = t % tiles_x, r = t / tiles_x;
-        const int ty_i = r % tiles_y, b = r / tiles_y;
-        const int iy0 = ty_i * TY * S - 1, ix0 = tx_i * TX * S - 1;
-        const dma::u32x4 rsrc = dma::srd((const T*)p.sptr[0] + (long long)b * p.sbs[0], bytes);
+    // per-lane halo slot geometry, fixed for the block's life: the slot's pixel (hy, hx)
+    // in the halo and its source byte offset relative to the halo's top-left pixel
+    int hrel[GB], hyx[GB];
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+        const int L = wave + NW * i;
+        const int s = 64 * L + lane;
+        const int hp = s / PS, c16 = s - hp * PS;
+        const int hy = hp / HXP, hx = hp - hy * HXP;
+        const bool st = L < LOADS && s < SLOTS && c16 < C16 && hx < HX;
+        hyx[i] = st ? (hy | (hx << 16)) : 0x7fff7fff;  // 0x7fff fails every range check
+        hrel[i] = ((hy * in_w + hx) * scs + c16 * 8) * 2;
+    }
+
+    struct TileC { int b, oy0, ox0; };
+    const unsigned txy = (unsigned)(tiles_x * tiles_y);
+    auto coords = [&](int t) -> TileC {
+        const unsigned b = (unsigned)t / txy, r = (unsigned)t - b * txy;
+        const unsigned ty = r / (unsigned)tiles_x, tx = r - ty * (unsigned)tiles_x;
+        return TileC{(int)b, (int)ty * TY, (int)tx * TX};
+    };
+
+    auto issue_halo = [&](const TileC& c, int kb) {
+        const int iy0 = c.oy0 * S - 1, ix0 = c.ox0 * S - 1;
+        const int base = (iy0 * in_w + ix0) * scs * 2;
+        const dma::u32x4 rsrc = dma::srd((const T*)p.sptr[0] + (long long)c.b * p.sbs[0], bytes);
 #pragma unroll
         for (int i = 0; i < GB; ++i) {
             const int L = wave + NW * i;
             if (LOADS % NW == 0 || i + 1 < GB || L < LOADS) {
-                const int s = 64 * L + lane;
-                const int hp = s / PS, c16 = s - hp * PS;
-                const int hy = hp / HXP, hx = hp - hy * HXP;
-                const int iy = iy0 + hy, ix = ix0 + hx;
-                const bool ok = s < SLOTS && c16 < C16 && hx < HX && iy >= 0 && iy < in_h && ix >= 0 && ix < in_w;
-                const uint32_t voff = ok ? (uint32_t)(((iy * in_w + ix) * scs + c16 * 8) * 2) : dma::kOob;
+                const int iy = iy0 + (hyx[i] & 0xffff), ix = ix0 + (hyx[i] >> 16);
+                const bool ok = (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w;
+                const uint32_t voff = ok ? (uint32_t)(base + hrel[i]) : dma::kOob;
                 dma::load16(rsrc, voff, 0u, __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(kb * HBYTES + L * 1024)));
             }
         }
     };
 
     const bool silu = p.act == YXH_ACT_SILU;
-    const T* res = (const T*)p.res;
-    T* dst = (T*)p.dst;
+    const bool has_res = p.res != nullptr;
+    const uint32_t dbytes = (uint32_t)((long long)ohw * p.dst_cs * 2);
+    const uint32_t rbytes = (uint32_t)((long long)ohw * p.res_cs * 2);
+    const int dcs = p.dst_cs, rcs = p.res_cs;
+    const uint32_t res_lds = lds0 + (uint32_t)(2 * HBYTES + RBYTES);
 
-    // one tile: wait for its halo, start the next tile's halo, MMA, (K-split reduce), epilogue
-    auto tile_step = [&](const int tile, const int k) -> int {
+    // residual staging: per-lane slot geometry (pixel ty/tx of the tile, 8-channel chunk)
+    int rgeo[GR > 0 ? GR : 1];
+#pragma unroll
+    for (int i = 0; i < GR; ++i) {
+        const int L = wave + NW * i;
+        const int sl = 64 * L + lane;
+        const int pl = sl / RS, ch = sl - pl * RS;
+        const int ty = pl / TX, tx = pl - ty * TX;
+        const bool st = L < RLOADS && sl < RSLOTS && ch < TN / 8 && n0 + ch * 8 < cout;
+        rgeo[i] = st ? (ty | (tx << 10) | (ch << 20)) : -1;
+    }
+    auto issue_res = [&](const TileC& c, int slot) {
+        if constexpr (GR > 0) {
+            const dma::u32x4 rsrc = dma::srd((const T*)p.res + (long long)c.b * p.res_bs, rbytes);
+#pragma unroll
+            for (int i = 0; i < GR; ++i) {
+                const int L = wave + NW * i;
+                if (RLOADS % NW == 0 || i + 1 < GR || L < RLOADS) {
+                    const int g = rgeo[i];
+                    const int oy = c.oy0 + (g & 1023), ox = c.ox0 + ((g >> 10) & 1023);
+                    const bool ok = g >= 0 && oy < OH && ox < OW;
+                    const uint32_t voff = ok ? (uint32_t)(((oy * OW + ox) * rcs + n0 + (g >> 20) * 8) * 2) : dma::kOob;
+                    dma::load16(rsrc, voff, 0u, __builtin_amdgcn_readfirstlane(res_lds + (uint32_t)(slot * RTB + L * 1024)));
+                }
+            }
+        }
+    };
+
+    // epilogue of a finished tile: bias, SiLU, residual (from the LDS staging slot), 8-byte
+    // stores of 4 channels through a buffer descriptor (an invalid pixel / channel carries an
+    // out-of-range offset: no branch, so the scheduler can spread it over the next tile's
+    // MFMAs); dispatch checks the dtype / alignment / activation this form assumes
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    struct EpiCtx { __amdgpu_buffer_rsrc_t dsrd; const char* rl; TileC c; };
+    auto epi_ctx = [&](const TileC c, const int k) -> EpiCtx {
+        return EpiCtx{__builtin_amdgcn_make_buffer_rsrc((void*)((T*)p.dst + (long long)c.b * p.dst_bs), (short)0,
+                                                        (int)dbytes, 0x00020000),
+                      smem + 2 * HBYTES + RBYTES + (k % 3) * RTB, c};
+    };
+    // one (pixel fragment o, channel fragment i) piece of the epilogue
+    auto epi_piece = [&](const EpiCtx& e, const f32x4 (&ap)[FR][FCO], const int o, const int i) {
+        const int j = wk + WK * o;
+        const int pl = (wm * FC + j) * 16 + frow;
+        const int ty = pl / TX, tx = pl - ty * TX;
+        const int oy = e.c.oy0 + ty, ox = e.c.ox0 + tx;
+        const int nl = wn * WTN + i * 16 + fq * 4, n = n0 + nl;
+        const bool ok = j < FC && oy < OH && ox < OW && n < cout;
+        const int od = ok ? ((oy * OW + ox) * dcs + n) * 2 : (int)dma::kOob;
+        u32x2 rv = {0u, 0u};
+        if constexpr (GR > 0) rv = *(const u32x2*)(e.rl + (pl * RS + (nl >> 3)) * 16 + (nl & 7) * 2);
+        T rt[4];
+        __builtin_memcpy(rt, &rv, 8);
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float x = ap[i][o][q] + bias[i][q];
+            const float y = silu ? yxh::silu<false>(x) : x;
+            v[q] = has_res ? y + to_f32(rt[q]) : y;
+        }
+        T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
+        u32x2 u;
+        __builtin_memcpy(&u, t, 8);
+        if (!(YXH_WS_PROBE & 1) || p.act == 12345) __builtin_amdgcn_raw_buffer_store_b64(u, e.dsrd, od, 0, 0);
+    };
+    auto epilogue = [&](const TileC c, const int k, const f32x4 (&ap)[FR][FCO]) {
+        const EpiCtx e = epi_ctx(c, k);
+#pragma unroll
+        for (int o = 0; o < FCO; ++o)
+#pragma unroll
+            for (int i = 0; i < FR; ++i) epi_piece(e, ap, o, i);
+    };
+
+    f32x4 accp[FR][FCO];  // owned fragments of the previous tile, waiting for their epilogue
+    constexpr int NS = WCB * 9;
+    constexpr int NP = FR * FCO;  // epilogue pieces, one per K step while they last
+
+    // one tile: wait for its halo, start tile k+1's halo (+ residual), MMA of tile k with the
+    // epilogue of tile k-1 spread over it, then the K-split reduce of tile k into accp
+    auto tile_step = [&](const TileC cur, const int tile, const int k, TileC& cnext, const TileC prev,
+                         auto epi) -> int {
+        constexpr bool EPI = decltype(epi)::value;
         const int kb = k & 1;
         const int next = tile + nwork;
         dma::wait_vm<0>();
         dma::barrier();
-        if (next < ntiles) issue_halo(next, kb ^ 1);
+        if (next < ntiles) {
+            cnext = coords(next);
+            if (!(YXH_WS_PROBE & 2)) {
+                issue_halo(cnext, kb ^ 1);
+                if (has_res) issue_res(cnext, (k + 1) % 3);
+            }
+        }
 
         f32x4 acc[FR][FC];
 #pragma unroll
@@ -147,7 +265,6 @@ __global__ __launch_bounds__(64 * WN * WK * WM, 1) void conv_ws(ConvParams p, in
         const char* hb = smem + kb * HBYTES;
         // K steps s = (channel block c, tap); the pixel fragments of step s + 1 are read
         // before the MFMAs of step s, so the LDS latency hides behind them
-        constexpr int NS = WCB * 9;
         uint4 bf[2][FC];
         auto load_b = [&](int s, uint4 (&d)[FC]) {
             const int c = s / 9, tap = s - 9 * (s / 9);
@@ -157,6 +274,9 @@ __global__ __launch_bounds__(64 * WN * WK * WM, 1) void conv_ws(ConvParams p, in
             for (int j = 0; j < FC; ++j) d[j] = *(const uint4*)(hb + boff[j] + so);
         };
         load_b(0, bf[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);
+        EpiCtx e{};
+        if constexpr (EPI) e = epi_ctx(prev, k - 1);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             if (s + 1 < NS) load_b(s + 1, bf[(s + 1) & 1]);
@@ -165,7 +285,21 @@ __global__ __launch_bounds__(64 * WN * WK * WM, 1) void conv_ws(ConvParams p, in
             for (int i = 0; i < FR; ++i)
 #pragma unroll
                 for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], a[i][tap][c], bf[s & 1][j]);
+            // piece s of the previous tile's epilogue rides on this step's MFMAs
+            if constexpr (EPI)
+                if (s < NP) epi_piece(e, accp, s / FR, s % FR);
+            // keep the one-step-ahead read distance (the scheduler would otherwise pull each
+            // read down next to its first MFMA) and put two VALU ops in each MFMA's shadow
+            if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);  // DS reads
+#pragma unroll
+            for (int m = 0; m < FR * FC; ++m) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                if constexpr (EPI) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+            }
         }
+        if constexpr (EPI)
+#pragma unroll
+            for (int q = NS; q < NP; ++q) epi_piece(e, accp, q / FR, q % FR);
 
         // ---- K-split: partial sums of the fragments other waves finish go through LDS
         if constexpr (WK > 1) {
@@ -187,58 +321,34 @@ __global__ __launch_bounds__(64 * WN * WK * WM, 1) void conv_ws(ConvParams p, in
 #pragma unroll
                 for (int j = 0; j < FC; ++j)
                     if (j % WK == wk) {
+                        f32x4 v = acc[i][j];
 #pragma unroll
-                        for (int o = 0; o < WK - 1; ++o) {
-                            const f32x4 v = *(const f32x4*)(red + (((grp * FR + i) * FC + j) * (WK - 1) + o) * 1024 + lane * 16);
-                            acc[i][j] += v;
-                        }
+                        for (int o = 0; o < WK - 1; ++o)
+                            v += *(const f32x4*)(red + (((grp * FR + i) * FC + j) * (WK - 1) + o) * 1024 + lane * 16);
+                        accp[i][j / WK] = v;
                     }
-        }
-
-        // ---- epilogue: bias, SiLU, residual, 8-byte stores of 4 channels (dispatch checks
-        // the dtype / alignment / activation this form assumes)
-        const int tx_i = tile % tiles_x, r = tile / tiles_x;
-        const int ty_i = r % tiles_y, b = r / tiles_y;
-        const int oy0 = ty_i * TY, ox0 = tx_i * TX;
+        } else {
 #pragma unroll
-        for (int j = 0; j < FC; ++j) {
-            if (WK > 1 && j % WK != wk) continue;
-            const int pl = (wm * FC + j) * 16 + frow;
-            const int ty = pl / TX, tx = pl - ty * TX;
-            const int oy = oy0 + ty, ox = ox0 + tx;
-            if (oy >= OH || ox >= OW) continue;
-            const int pix = oy * OW + ox;
+            for (int i = 0; i < FR; ++i)
 #pragma unroll
-            for (int i = 0; i < FR; ++i) {
-                const int n = n0 + wn * WTN + i * 16 + fq * 4;
-                if (n >= cout) continue;
-                float v[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    v[q] = acc[i][j][q] + bias[i][q];
-                    if (silu) v[q] = yxh::silu<false>(v[q]);
-                }
-                if (res) {
-                    const uint2 u = *(const uint2*)(res + (long long)b * p.res_bs + (long long)pix * p.res_cs + n);
-                    T t[4];
-                    __builtin_memcpy(t, &u, 8);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) v[q] += to_f32(t[q]);
-                }
-                T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
-                uint2 u;
-                __builtin_memcpy(&u, t, 8);
-                *(uint2*)(dst + (long long)b * p.dst_bs + (long long)pix * p.dst_cs + n) = u;
-            }
+                for (int j = 0; j < FC; ++j) accp[i][j] = acc[i][j];
         }
         return next;
     };
 
-    issue_halo(tile, 0);
+    TileC cur = coords(tile), cnext{0, 0, 0};
+    issue_halo(cur, 0);
+    if (has_res) issue_res(cur, 0);
     // the first tile is peeled off the loop: it consumes the weight loads, so the loop body
     // carries no compiler-visible pending load whose wait would also drain the halo DMA
-    int next = tile_step(tile, 0);
-    for (int k = 1; next < ntiles; ++k) next = tile_step(next, k);
+    int next = tile_step(cur, tile, 0, cnext, cur, std::false_type{});
+    int k = 1;
+    for (; next < ntiles; ++k) {
+        const TileC prev = cur;
+        cur = cnext;
+        next = tile_step(cur, next, k, cnext, prev, std::true_type{});
+    }
+    epilogue(cur, k - 1, accp);
     (void)ohw;
 }
 
@@ -249,8 +359,9 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
         return YXH_EUNSUPPORTED;
     }
     if (p.dst_f32 || p.accum || (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) || !p.vec_store ||
-        (p.res && !p.vec_res) || p.cout % 4) {
-        set_error("conv_ws: 16-bit dst, SiLU/no activation, 8-byte aligned dst/residual rows only");
+        p.cout % 8 || (p.res && (S != 1 || ((uintptr_t)p.res % 16) || p.res_cs % 8 || p.res_bs % 8))) {
+        set_error("conv_ws: 16-bit dst, SiLU/no activation, 8-byte aligned dst rows, 16-byte residual rows "
+                  "(stride-1 variants) only");
         return YXH_EUNSUPPORTED;
     }
     const int tiles_x = (p.out_w + TX - 1) / TX, tiles_y = (p.out_h + TY - 1) / TY;
@@ -261,7 +372,7 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
         return YXH_EINVAL;
     }
     const int nwork = (int)std::min<long long>(ntiles, std::max(1, 256 * BPC / ntn));
-    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM>), dim3((unsigned)(nwork * ntn)),
+    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM, BPC>), dim3((unsigned)(nwork * ntn)),
                        dim3(64 * WN * WK * WM), 0, st, p, tiles_x, tiles_y, (int)ntiles, ntn, nwork);
     YXH_CHECK_LAUNCH("conv_ws launch");
     return YXH_OK;
@@ -283,7 +394,7 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 8: return launch_ws<T, 64, 2, 16, 2, 128, 4, 1, 1, 2>(p, st);
         // 128 input channels: 40x40 / 80x80 / 20x20 3x3s (dark4, PAFPN, head), s2 128 -> 128/256
         case 9: return launch_ws<T, 128, 1, 16, 4, 128, 4, 2, 1>(p, st);
-        case 10: return launch_ws<T, 128, 1, 16, 8, 64, 2, 2, 1>(p, st);
+        case 10: return launch_ws<T, 32, 1, 32, 8, 32, 1, 1, 4, 2>(p, st);
         case 11: return launch_ws<T, 128, 1, 8, 4, 128, 4, 2, 1>(p, st);
         case 12: return launch_ws<T, 128, 1, 8, 8, 64, 2, 2, 1>(p, st);
         case 13: return launch_ws<T, 128, 2, 16, 2, 128, 4, 2, 1>(p, st);
@@ -292,6 +403,15 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         // 256 input channels: dark5 / PAFPN / yolox_l head 3x3s (K split four ways)
         case 16: return launch_ws<T, 256, 1, 8, 4, 64, 2, 4, 1>(p, st);
         case 17: return launch_ws<T, 256, 1, 16, 2, 64, 2, 4, 1>(p, st);
+        // 4-wave blocks held to 256 registers, two resident per CU: one block's
+        // barriers / epilogue overlap the other's MFMAs
+        case 18: return launch_ws<T, 32, 1, 16, 8, 32, 1, 1, 4, 2>(p, st);
+        case 19: return launch_ws<T, 64, 1, 32, 2, 64, 2, 1, 2, 2>(p, st);
+        case 20: return launch_ws<T, 128, 1, 16, 2, 64, 2, 2, 1, 2>(p, st);
+        case 21: return launch_ws<T, 128, 1, 8, 4, 64, 2, 2, 1, 2>(p, st);
+        case 22: return launch_ws<T, 128, 2, 16, 1, 64, 2, 2, 1, 2>(p, st);
+        case 23: return launch_ws<T, 256, 1, 8, 2, 32, 1, 4, 1, 2>(p, st);
+        case 24: return launch_ws<T, 64, 2, 16, 2, 64, 2, 1, 2, 2>(p, st);
         default: set_error("conv_ws tile id %d", id); return YXH_EINVAL;
     }
 }

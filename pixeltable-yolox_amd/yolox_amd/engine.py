@@ -248,7 +248,7 @@ class OutBuffer:
 # conv_pwr kernel, 97-104 the dense 1x1 conv_pwf kernel, 113-150 the 3x3 conv_r3 kernel
 # (yoloxhip.h yxh_conv_desc.tile)
 TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
-                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 178)]
+                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 185)]
 _TUNE_CACHE: dict = {}
 _TUNE_ALL = os.environ.get("YOLOX_AMD_TUNE_ALL", "0") == "1"  # print every variant's time
 

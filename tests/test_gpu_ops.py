@@ -687,7 +687,7 @@ WS_GEOMS = [  # cin, cout, s, H, W (input), batch
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("geom", WS_GEOMS)
 def test_conv_ws_3x3(dtype, geom):
-    """conv_ws (ids 161-177): weight-stationary persistent 3x3 conv, every variant built for
+    """conv_ws (ids 161-184): weight-stationary persistent 3x3 conv, every variant built for
     this (cin, stride) vs the fp32 reference: partial spatial tiles, cout tails, several
     tiles per persistent block, K split over waves, a channel-slice source."""
     cin, cout, s, H, W, B = geom
@@ -697,7 +697,7 @@ def test_conv_ws_3x3(dtype, geom):
     wide = torch.zeros(B, H, W, cin + 32, dtype=dtype, device=DEV)
     wide[..., 16:16 + cin] = nhwc(x, dtype)
     ran = 0
-    for tid in range(161, 178):
+    for tid in range(161, 185):
         try:
             y = run_conv([(wide, 16, cin, 0)], conv, bn, dtype, tile=2 * tid)
         except NotImplementedError as e:
