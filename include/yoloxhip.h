@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 8
+#define YXH_ABI_VERSION 9
 
 enum yxh_status {
     YXH_OK = 0,
@@ -107,6 +107,14 @@ typedef struct {
                             kernel, id 65-70 the persistent streaming 1x1 kernel;
                             chosen by the planner's on-device autotune                   */
     int32_t flags;       /* YXH_CONV_ACCUMULATE: f32 dst += result (gradient accumulation) */
+    int32_t reserved0;
+    /* Fused Bottleneck (network_blocks.py:77-99): when pre_weight is set, the source is the
+     * Bottleneck input x and the 3x3 conv reads t = act(pre_weight . x + pre_bias) (its
+     * conv1, a 1x1 cin -> cin, BatchNorm folded), computed per pixel tile on the halo in LDS
+     * and never written to memory.  3x3 s1 16-bit convs on the conv_ws fused tiles only;
+     * dst must not alias the source (tile halos are read while other tiles write). */
+    const void* pre_weight; /* [cin][cin] in dtype                                          */
+    const float* pre_bias;  /* fp32 [cin]                                                    */
 } yxh_conv_desc;
 
 #define YXH_CONV_ACCUMULATE 1

@@ -491,6 +491,17 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         p.src_dense &= !p.sup[s] && p.sw[s] == p.out_w && p.sbs[s] == (long long)p.ohw * p.scs[s];
     p.dst_dense = d->dst_bstride == (long long)p.ohw * d->dst_cstride;
     p.res_dense = d->residual && d->res_bstride == (long long)p.ohw * d->res_cstride;
+    p.pw1 = d->pre_weight;
+    p.pb1 = d->pre_bias;
+    YXH_CHECK_ARG(!d->pre_weight || (d->pre_bias && aligned16(d->pre_weight) && d->kh == 3 && d->stride == 1 &&
+                                     d->pad == 1 && d->groups == 1 && d->nsrc == 1 && dt != YXH_F32),
+                  "fused Bottleneck: 16-bit 3x3 s1 conv over one source with a pre_bias");
+    if (d->pre_weight && d->tile == 0)  // default fused tile per channel count
+        return conv_ws_dispatch(dt, d->cin == 32 ? 191 - 160 : d->cin == 64 ? 194 - 160 : 195 - 160, p, st);
+    if (d->pre_weight && (d->tile >> 1) <= 160 + 30) {
+        set_error("fused Bottleneck runs on the conv_ws fused tiles (ids 191-196) only");
+        return YXH_EUNSUPPORTED;
+    }
     p.vec16 = d->dst_dtype == dt && ((uintptr_t)d->dst % 16) == 0 && (d->dst_cstride * des) % 16 == 0 &&
               (d->dst_bstride * des) % 16 == 0 && (d->cout * des) % 16 == 0;
 

@@ -27,6 +27,8 @@ struct ConvParams {
     int dst_dense, res_dense;
     int src_dense;  // 1x1 s1 p0 over sources without upsample whose pixel m is at m * scs
     float dstride;
+    const void* pw1;  // fused Bottleneck conv1 (1x1, cin -> cin) ahead of the 3x3: conv_ws only
+    const float* pb1;
 };
 
 // ---------------------------------------------------------------- MFMA step
@@ -266,6 +268,6 @@ int conv_r3_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumR3Tiles = 48;  // ids beyond the built ones report EINVAL
 // Weight-stationary persistent 3x3 conv (conv_ws.hip): tile ids 161..160+kNumWsTiles
 int conv_ws_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
-constexpr int kNumWsTiles = 24;
+constexpr int kNumWsTiles = 36;  // 31..36: fused Bottleneck (pre_weight)
 
 }  // namespace yxh

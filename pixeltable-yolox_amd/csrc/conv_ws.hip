@@ -44,7 +44,7 @@ constexpr int ws_hxp(int tx, int s) {
 
 }  // namespace
 
-template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC>
+template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC, bool F1>
 __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, int tiles_x, int tiles_y,
                                                                  int ntiles, int ntn, int nwork) {
     static_assert(sizeof(T) == 2, "16-bit operands");
@@ -64,10 +64,17 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     // (the epilogue of tile k-1 runs during tile k while tile k+1 lands)
     constexpr int RS = TN / 8 + 1, RSLOTS = S == 1 ? TM * RS : 0;
     constexpr int RLOADS = (RSLOTS + 63) / 64, GR = (RLOADS + NW - 1) / NW, RTB = RLOADS * 1024;
-    constexpr int SMEM = 2 * HBYTES + RBYTES + 3 * RTB;
+    // fused Bottleneck (F1): t = act(W1 . x + b1) of the halo tile, computed into one more
+    // halo-shaped LDS image that the 3x3 then reads; wave w computes t channels
+    // 32 (w % NG) .. +32 of every R-th 16-pixel halo fragment
+    constexpr int NG = CIN / 32, R1 = NW / NG, NPA = (HY * HXP + 15) / 16;
+    constexpr int TOFF = 2 * HBYTES + RBYTES + 3 * RTB;
+    constexpr int SMEM = TOFF + (F1 ? HBYTES : 0);
+    static_assert(!F1 || (S == 1 && NW % NG == 0), "fused Bottleneck tile");
     constexpr int FCO = (FC + WK - 1) / WK;  // pixel fragments this wave finishes
     static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0 && TM % (16 * WM) == 0, "tile");
-    static_assert(FR * 9 * WCB * 4 <= 160, "weights must stay in VGPRs");
+    // weights must stay in VGPRs: 160 of 256 (2 waves per SIMD), 288 of 512 (one 4-wave block per CU)
+    static_assert(FR * 9 * WCB * 4 <= (NW == 4 && BPC == 1 ? 288 : 160), "weights must stay in VGPRs");
     static_assert(SMEM <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -105,6 +112,21 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         const int n = n0 + wn * WTN + i * 16 + fq * 4;
 #pragma unroll
         for (int r = 0; r < 4; ++r) bias[i][r] = n + r < cout ? p.bias[n + r] : 0.0f;
+    }
+
+    uint4 a1[F1 ? 2 : 1][F1 ? NG : 1];
+    float b1[2][4];
+    if constexpr (F1) {
+        const T* w1 = (const T*)p.pw1;
+        const int g = wave % NG;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+            for (int cb = 0; cb < NG; ++cb)
+                a1[i][cb] = *(const uint4*)(w1 + (g * 32 + i * 16 + frow) * CIN + cb * 32 + fq * 8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) b1[i][r] = p.pb1[g * 32 + i * 16 + fq * 4 + r];
+        }
     }
 
     // ---- this lane's LDS byte offsets of its pixel fragments at tap (0, 0), channel block 0
@@ -257,12 +279,47 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             }
         }
 
+        if constexpr (F1) {
+            // Bottleneck conv1 over the halo: t = act(W1 . x + b1), zero outside the image
+            // (it is the 3x3's zero padding), into the t image
+            const char* hx_img = smem + kb * HBYTES;
+            char* timg = smem + TOFF;
+            const int g = wave % NG;
+            for (int fa = wave / NG; fa < NPA; fa += R1) {
+                const int hq = fa * 16 + frow;
+                const int hpr = min(hq, HY * HXP - 1);
+                f32x4 t2[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+                for (int cb = 0; cb < NG; ++cb) {
+                    const uint4 xb = *(const uint4*)(hx_img + hpr * PSB + (cb * 4 + fq) * 16);
+                    Mma<T>::run(t2[0], a1[0][cb], xb);
+                    Mma<T>::run(t2[1], a1[1][cb], xb);
+                }
+                const int hy = hq / HXP, hx = hq - hy * HXP;
+                const int iy = cur.oy0 - 1 + hy, ix = cur.ox0 - 1 + hx;
+                const bool valid = hx < HX && (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    T t[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float x = t2[i][q] + b1[i][q];
+                        t[q] = from_f32<T>(valid ? (silu ? yxh::silu<false>(x) : x) : 0.0f);
+                    }
+                    u32x2 u;
+                    __builtin_memcpy(&u, t, 8);
+                    if (hq < HY * HXP) *(u32x2*)(timg + hq * PSB + (g * 32 + i * 16 + fq * 4) * 2) = u;
+                }
+            }
+            dma::barrier();
+        }
+
         f32x4 acc[FR][FC];
 #pragma unroll
         for (int i = 0; i < FR; ++i)
 #pragma unroll
             for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const char* hb = smem + kb * HBYTES;
+        const char* hb = F1 ? smem + TOFF : smem + kb * HBYTES;
         // K steps s = (channel block c, tap); the pixel fragments of step s + 1 are read
         // before the MFMAs of step s, so the LDS latency hides behind them
         uint4 bf[2][FC];
@@ -352,10 +409,16 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     (void)ohw;
 }
 
-template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC = 1>
+template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC = 1, bool F1 = false>
 static int launch_ws(const ConvParams& p, hipStream_t st) {
     if (p.stride != S || p.cin != CIN) {
         set_error("conv_ws variant built for stride %d, %d input channels", S, CIN);
+        return YXH_EUNSUPPORTED;
+    }
+    if ((p.pw1 != nullptr) != F1) {
+        set_error(F1 ? "conv_ws fused-Bottleneck variant (%d input channels) needs pre_weight"
+                     : "conv_ws plain variant (%d input channels) with a pre_weight",
+                  CIN);
         return YXH_EUNSUPPORTED;
     }
     if (p.dst_f32 || p.accum || (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) || !p.vec_store ||
@@ -372,7 +435,7 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
         return YXH_EINVAL;
     }
     const int nwork = (int)std::min<long long>(ntiles, std::max(1, 256 * BPC / ntn));
-    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM, BPC>), dim3((unsigned)(nwork * ntn)),
+    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM, BPC, F1>), dim3((unsigned)(nwork * ntn)),
                        dim3(64 * WN * WK * WM), 0, st, p, tiles_x, tiles_y, (int)ntiles, ntn, nwork);
     YXH_CHECK_LAUNCH("conv_ws launch");
     return YXH_OK;
@@ -412,6 +475,22 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 22: return launch_ws<T, 128, 2, 16, 1, 64, 2, 2, 1, 2>(p, st);
         case 23: return launch_ws<T, 256, 1, 8, 2, 32, 1, 4, 1, 2>(p, st);
         case 24: return launch_ws<T, 64, 2, 16, 2, 64, 2, 1, 2, 2>(p, st);
+        // one 4-wave block per CU with 512 registers: 128 channels x all of K per block, no
+        // K split (no reduce barrier)
+        case 25: return launch_ws<T, 128, 1, 16, 4, 128, 4, 1, 1>(p, st);
+        case 26: return launch_ws<T, 128, 1, 16, 2, 128, 4, 1, 1>(p, st);
+        case 27: return launch_ws<T, 128, 1, 8, 4, 128, 4, 1, 1>(p, st);
+        // stride 2 from 256 channels (dark5 downsample 256 -> 512, PAFPN bu_conv1 256 -> 256)
+        case 28: return launch_ws<T, 256, 2, 8, 2, 32, 1, 4, 1>(p, st);
+        case 29: return launch_ws<T, 256, 2, 8, 2, 64, 2, 4, 1>(p, st);
+        case 30: return launch_ws<T, 256, 2, 16, 1, 32, 1, 4, 1>(p, st);
+        // fused Bottleneck (conv1 1x1 + conv2 3x3 + shortcut): ids 191-196
+        case 31: return launch_ws<T, 32, 1, 16, 8, 32, 1, 1, 4, 1, true>(p, st);
+        case 32: return launch_ws<T, 32, 1, 16, 16, 32, 1, 1, 8, 1, true>(p, st);
+        case 33: return launch_ws<T, 64, 1, 16, 4, 64, 2, 1, 2, 1, true>(p, st);
+        case 34: return launch_ws<T, 64, 1, 16, 8, 64, 2, 1, 2, 1, true>(p, st);
+        case 35: return launch_ws<T, 128, 1, 16, 4, 128, 4, 1, 1, 1, true>(p, st);
+        case 36: return launch_ws<T, 128, 1, 8, 4, 128, 4, 1, 1, 1, true>(p, st);
         default: set_error("conv_ws tile id %d", id); return YXH_EINVAL;
     }
 }

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -47,7 +47,7 @@ class ConvDesc(C.Structure):
                 ("dst_dtype", C.c_int32), ("res_bstride", C.c_int64), ("dst", C.c_void_p),
                 ("dst_cstride", C.c_int32), ("act", C.c_int32), ("dst_bstride", C.c_int64),
                 ("decode_stride", C.c_float), ("decode_coff", C.c_int32), ("tile", C.c_int32),
-                ("flags", C.c_int32)]
+                ("flags", C.c_int32), ("reserved0", C.c_int32), ("pre_weight", C.c_void_p), ("pre_bias", C.c_void_p)]
 
 
 CONV_ACCUMULATE = 1

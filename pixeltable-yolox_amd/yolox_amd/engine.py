@@ -104,7 +104,8 @@ class OpRec:
 
 
 class PlanCtx:
-    def __init__(self, batch: int, dtype: torch.dtype, device: torch.device, fuse_stem: bool = True):
+    def __init__(self, batch: int, dtype: torch.dtype, device: torch.device, fuse_stem: bool = True,
+                 fuse_bottleneck: bool = False):
         if dtype not in (torch.float32, torch.bfloat16, torch.float16):
             raise ValueError(f"compute dtype {dtype} not supported (float32, bfloat16, float16)")
         self.batch = batch
@@ -114,6 +115,9 @@ class PlanCtx:
         self.epc = 16 // self.esize
         self.device = device
         self.fuse_stem = fuse_stem
+        # Bottleneck conv1 (1x1) folded into conv2's 3x3 (conv_ws fused tiles): 16-bit only.
+        # Off by default: measured no faster than the two launches
+        self.fuse_bottleneck = fuse_bottleneck and dtype != torch.float32
         self.buffers: list[Buffer] = []
         self.weights: list[WeightSpec] = []
         self.ops: list[OpRec] = []
@@ -206,6 +210,34 @@ class PlanCtx:
         self.flops += 2.0 * self.batch * oh * ow * cout * kh * kw * (conv.in_channels // groups)
         return out
 
+    def bottleneck_fusable(self, b) -> bool:
+        c1, c2 = b.conv1, b.conv2
+        if not (self.fuse_bottleneck and hasattr(c1, "conv") and hasattr(c2, "conv")):
+            return False
+        k1, k3 = c1.conv, c2.conv
+        ch = k1.in_channels
+        return (ch in (32, 64, 128) and k1.out_channels == ch and k3.in_channels == ch and k3.out_channels == ch
+                and k1.kernel_size == (1, 1) and k1.groups == 1 and k3.kernel_size == (3, 3)
+                and k3.stride == (1, 1) and k3.padding == (1, 1) and k3.groups == 1
+                and getattr(c1, "act_name", "silu") == getattr(c2, "act_name", "silu") == "silu")
+
+    def bottleneck(self, b, x: View, out: View) -> View:
+        """Bottleneck (network_blocks.py:77-99) as ONE conv: conv1's 1x1 is computed per tile
+        on the 3x3's halo in LDS (yxh_conv_desc.pre_weight) -- the hidden map never reaches
+        HBM.  ``out`` must not alias ``x`` (neighbouring tiles read x's halo)."""
+        k1, k3 = b.conv1.conv, b.conv2.conv
+        ch = k1.in_channels
+        if out.buf is x.buf and out.coff < x.coff + x.ch and x.coff < out.coff + out.ch:
+            raise ValueError("fused Bottleneck output aliases its input")
+        spec = self._weights([(k3, b.conv2.bn)], ch)
+        pre = self._weights([(k1, b.conv1.bn)], ch)
+        self.ops.append(OpRec(N.OP_CONV, dict(
+            srcs=[x], out=out, residual=x if b.use_add else None, spec=spec, pre_spec=pre, cin=ch, cout=ch, k=3,
+            stride=1, pad=1, groups=1, in_h=x.lh, in_w=x.lw, out_h=x.lh, out_w=x.lw,
+            act=N.ACT_CODE["silu"], dst_f32=False)))
+        self.flops += 2.0 * self.batch * x.lh * x.lw * ch * ch * 10  # 1x1 + 3x3
+        return out
+
     def spp(self, cat: Buffer, hidden: int) -> None:
         self.ops.append(OpRec(N.OP_SPP, dict(buf=cat, c=hidden)))
 
@@ -248,7 +280,7 @@ class OutBuffer:
 # conv_pwr kernel, 97-104 the dense 1x1 conv_pwf kernel, 113-150 the 3x3 conv_r3 kernel
 # (yoloxhip.h yxh_conv_desc.tile)
 TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
-                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 185)]
+                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 197)]
 _TUNE_CACHE: dict = {}
 _TUNE_ALL = os.environ.get("YOLOX_AMD_TUNE_ALL", "0") == "1"  # print every variant's time
 
@@ -271,7 +303,7 @@ def load_tune_cache(path: str) -> int:
 def _tune_key(d) -> tuple:
     return (d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w, d.cin, d.cout, d.kh, d.stride, d.nsrc,
             d.src[0].channels, d.src[0].upsample, d.src[1].upsample if d.nsrc > 1 else 0,
-            bool(d.residual), d.dst_dtype, d.dst_cstride == d.cout, d.act >= N.ACT_DECODE)
+            bool(d.residual), d.dst_dtype, d.dst_cstride == d.cout, d.act >= N.ACT_DECODE, bool(d.pre_weight))
 
 
 def op_dependencies(ops) -> list:
@@ -321,7 +353,7 @@ class Plan:
 
     def __init__(self, model, batch: int, height: int, width: int, dtype: torch.dtype, device,
                  input_layout: int = N.NCHW, input_dtype: torch.dtype = torch.float32, train: bool = False,
-                 fuse_stem: bool = True, chunk: Optional[int] = None):
+                 fuse_stem: bool = True, chunk: Optional[int] = None, fuse_bottleneck: bool = False):
         if height % 32 or width % 32:
             raise ValueError("input size must be multiples of 32")
         chunk = chunk or batch
@@ -336,7 +368,7 @@ class Plan:
         self.dtype = dtype
         head = model.head
         self.num_classes = head.num_classes
-        ctx = PlanCtx(chunk, dtype, self.device, fuse_stem=fuse_stem)
+        ctx = PlanCtx(chunk, dtype, self.device, fuse_stem=fuse_stem, fuse_bottleneck=fuse_bottleneck)
         feats = model.backbone.plan(ctx, ctx.image(height, width))
         anchors = sum(f.lh * f.lw for f in feats)
         self.out_spec = OutBuffer(anchors, 5 + self.num_classes)
@@ -456,6 +488,10 @@ class Plan:
                 spec: WeightSpec = a["spec"]
                 d.weight = self.warena.data_ptr() + spec.w_off
                 d.bias = self.barena.data_ptr() + spec.b_off
+                pre = a.get("pre_spec")
+                if pre is not None:
+                    d.pre_weight = self.warena.data_ptr() + pre.w_off
+                    d.pre_bias = self.barena.data_ptr() + pre.b_off
                 res = a["residual"]
                 if res is not None:
                     d.residual = self._ptr(res)

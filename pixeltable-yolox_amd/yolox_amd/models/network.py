@@ -117,6 +117,18 @@ class CspLayer(_Planned):
         x1 = cat.slice(0, hidden)
         # conv1 | conv2 read the same input: one conv writes the whole [x_1 | x_2]
         ctx.conv_multi([self.conv1, self.conv2], srcs, out=cat.full())
+        if self.m and all(ctx.bottleneck_fusable(b) for b in self.m):
+            # fused Bottlenecks cannot run in place: ping-pong between x_1 and a side buffer;
+            # conv3 then reads [last | x_2] as two sources
+            side = ctx.buffer(srcs[0].lh, srcs[0].lw, hidden).full()
+            cur = x1
+            for b in self.m:
+                nxt = side if cur is x1 else x1
+                ctx.bottleneck(b, cur, nxt)
+                cur = nxt
+            if cur is not x1:
+                return self.conv3.plan(ctx, [cur, cat.slice(hidden, hidden)], out=out)
+            return self.conv3.plan(ctx, [cat.full()], out=out)
         for b in self.m:
             b.plan(ctx, x1, out=x1)
         return self.conv3.plan(ctx, [cat.full()], out=out)

@@ -131,6 +131,27 @@ def test_fused_stem_plan_matches_focus_plan(golden, dtype):
         assert dp.max().item() < 0.2 and dp.flatten().quantile(0.99).item() < 0.06
 
 
+def test_fused_bottleneck_plan_matches_split_plan(golden):
+    """Bottlenecks planned as ONE conv_ws launch (conv1 computed on the 3x3's halo,
+    ping-pong buffers, conv3 over two sources) give the split plan's output up to
+    summation order: both hold conv1's output rounded to bf16."""
+    from yolox_amd import _native as N
+    from yolox_amd.engine import Plan
+    d = golden("fwd_yolox_s_128.npz")
+    m = model("yolox_s", torch.bfloat16)
+    x = torch.from_numpy(d["input_u8"]).cuda()
+    fused = Plan(m, 2, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8, fuse_bottleneck=True)
+    split = Plan(m, 2, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8)
+    n_pre = sum(1 for o in fused.ctx.ops if o.args.get("pre_spec") is not None)
+    assert n_pre == 1 + 3 + 3 + 1 + 1 + 1  # dark2, dark3, dark4, C3_p4, C3_p3, C3_n3 (C = 32/64/128)
+    assert len(fused.ctx.ops) == len(split.ctx.ops) - n_pre
+    a, b = fused.run(x).clone(), split.run(x).clone()
+    dp = (a[..., 4:] - b[..., 4:]).abs()
+    assert dp.max().item() < 0.2 and dp.flatten().quantile(0.99).item() < 0.06
+    db = (a[..., :4] - b[..., :4]).abs() / b[..., :4].abs().clamp_min(1.0)
+    assert db.flatten().quantile(0.99).item() < 0.05
+
+
 def test_chunked_plan_matches_whole_batch():
     """Executing the op list per chunk of images (Infinity-Cache-sized passes) gives
     the whole-batch result bit for bit, eager and as a graph."""

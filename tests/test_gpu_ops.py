@@ -74,7 +74,8 @@ def ref_conv(x, conv, bn, act):
     return {"silu": F.silu, "relu": F.relu, "lrelu": lambda t: F.leaky_relu(t, 0.1), "none": lambda t: t}[act](y)
 
 
-def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_coff=0, out_c=None, tile=0, flags=0):
+def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_coff=0, out_c=None, tile=0, flags=0,
+             pre=None):
     """srcs: list of (nhwc tensor [B,h,w,C], coff, ch, upsample)."""
     n = N()
     B = srcs[0][0].shape[0]
@@ -107,6 +108,8 @@ def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_cof
     d.act = n.ACT_CODE[act]
     d.tile = tile
     d.flags = flags
+    if pre is not None:  # fused Bottleneck conv1 (packed weight, bias)
+        d.pre_weight, d.pre_bias = pre[0].data_ptr(), pre[1].data_ptr()
     n.check(n.lib().yxh_conv2d(ctypes.byref(d), n.stream_ptr()), "conv2d")
     torch.cuda.synchronize()
     return out
@@ -687,7 +690,7 @@ WS_GEOMS = [  # cin, cout, s, H, W (input), batch
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("geom", WS_GEOMS)
 def test_conv_ws_3x3(dtype, geom):
-    """conv_ws (ids 161-184): weight-stationary persistent 3x3 conv, every variant built for
+    """conv_ws (ids 161-190): weight-stationary persistent 3x3 conv, every variant built for
     this (cin, stride) vs the fp32 reference: partial spatial tiles, cout tails, several
     tiles per persistent block, K split over waves, a channel-slice source."""
     cin, cout, s, H, W, B = geom
@@ -697,7 +700,7 @@ def test_conv_ws_3x3(dtype, geom):
     wide = torch.zeros(B, H, W, cin + 32, dtype=dtype, device=DEV)
     wide[..., 16:16 + cin] = nhwc(x, dtype)
     ran = 0
-    for tid in range(161, 185):
+    for tid in range(161, 191):
         try:
             y = run_conv([(wide, 16, cin, 0)], conv, bn, dtype, tile=2 * tid)
         except NotImplementedError as e:
@@ -706,6 +709,36 @@ def test_conv_ws_3x3(dtype, geom):
         close(y.permute(0, 3, 1, 2), want, dtype)
         ran += 1
     assert ran >= 1
+
+
+@pytest.mark.parametrize("ch,H,W,B", [(32, 37, 45, 2), (64, 40, 24, 3), (128, 20, 22, 4), (64, 80, 80, 4)])
+@pytest.mark.parametrize("shortcut", [True, False])
+def test_conv_ws_fused_bottleneck(ch, H, W, B, shortcut):
+    """Fused Bottleneck (ids 191-196; network_blocks.py:77-99): conv1 1x1 + SiLU computed on
+    the 3x3's halo in LDS (zero outside the image), conv2 3x3 + SiLU, + x, vs torch fp32 on
+    the same rounded operands (t rounded to bf16 as the kernel holds it)."""
+    dtype = torch.bfloat16
+    c1, bn1 = make_conv(ch, ch, 1, 1, seed=ch + 1)
+    c3, bn3 = make_conv(ch, ch, 3, 1, seed=ch + 2)
+    x = torch.randn(B, ch, H, W, generator=torch.Generator().manual_seed(H * W))
+    xq = x.to(dtype).float()
+    w1, b1 = pack(c1, bn1, dtype, ch)
+    t = ref_conv(xq, c1, bn1, "silu").to(dtype).float()
+    want = ref_conv(t, c3, bn3, "silu") + (xq if shortcut else 0)
+    X = nhwc(x, dtype)
+    ran = 0
+    for tid in range(191, 197):
+        try:
+            y = run_conv([(X, 0, ch, 0)], c3, bn3, dtype, residual=(X, 0) if shortcut else None, tile=2 * tid,
+                         pre=(w1, b1))
+        except NotImplementedError as e:
+            assert "input channels" in str(e), e
+            continue
+        close(y.permute(0, 3, 1, 2), want, dtype)
+        ran += 1
+    assert ran >= 1
+    with pytest.raises(NotImplementedError):  # a plain tile refuses a fused descriptor
+        run_conv([(X, 0, ch, 0)], c3, bn3, dtype, tile=2 * 166, pre=(w1, b1))
 
 
 def test_conv_ws_residual_and_strided_dst():
