@@ -269,5 +269,8 @@ constexpr int kNumR3Tiles = 48;  // ids beyond the built ones report EINVAL
 // Weight-stationary persistent 3x3 conv (conv_ws.hip): tile ids 161..160+kNumWsTiles
 int conv_ws_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumWsTiles = 36;  // 31..36: fused Bottleneck (pre_weight)
+// Weight-stationary persistent 1x1 conv over dense sources (conv_ws1.hip): tile ids 201..200+kNumWs1Tiles
+int conv_ws1_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
+constexpr int kNumWs1Tiles = 10;
 
 }  // namespace yxh

@@ -1,0 +1,291 @@
+// conv_ws1: weight-stationary persistent 1x1 conv (16-bit) over dense sources -- the
+// 1x1 BaseConvs of CspLayer (network_blocks.py:160-183 conv1 | conv2 and conv3 over the
+// concat), SPPBottleneck (:107-116), the PAFPN lateral / reduce convs (yolo_pafpn.py:58-64)
+// and the head stems (yolo_head.py:52-56).
+//
+// The 1x1 form of conv_ws.hip: a block keeps its TN output channels x all of K in VGPRs
+// for its life and walks pixel tiles of TM consecutive pixels of the flattened batch; per
+// tile only the pixel rows land in LDS (LDS-DMA, two buffers), the next tile's rows fly
+// while this tile computes, and the epilogue of tile k-1 is spread over tile k's MFMAs.
+// Two sources (a channel concat) occupy two LDS regions of the same pixel stride, so every
+// 1 KiB DMA reads one source; a K step (32 channels) lies inside one source.
+#include "conv_common.hpp"
+#include "lds_dma.hpp"
+
+namespace yxh {
+
+template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC>
+__global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p, int ntiles, int ntn, int nwork,
+                                                                    int ps, int l0, int l1) {
+    static_assert(sizeof(T) == 2, "16-bit operands");
+    constexpr int NW = WN * WK * WM;
+    constexpr int NCB = CIN / 32, WCB = NCB / WK;
+    constexpr int WTN = TN / WN, FR = WTN / 16;
+    constexpr int WTM = TM / WM, FC = WTM / 16;
+    constexpr int C16 = CIN / 8;
+    // LDS image bound: two regions of TM pixels x ps 16-byte slots (ps padded up to 2 x odd,
+    // at most 3 slots per region), each rounded up to whole 1 KiB wave-loads
+    constexpr int LMAX = (TM * (C16 + 6) + 63) / 64 + 2, GB = (LMAX + NW - 1) / NW, HBYTES = LMAX * 1024;
+    constexpr int RBYTES = WK > 1 ? WN * WM * FR * FC * (WK - 1) * 1024 : 0;
+    constexpr int SMEM = 2 * HBYTES + RBYTES;
+    constexpr int FCO = (FC + WK - 1) / WK;
+    static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0, "tile");
+    static_assert(FR * WCB * 4 <= (NW == 4 && BPC == 1 ? 288 : 160), "weights must stay in VGPRs");
+    static_assert(SMEM <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave % WN, wk = (wave / WN) % WK, wm = wave / (WN * WK);
+    const int frow = lane & 15, fq = lane >> 4;
+    const int bid = dma::xcd_remap(blockIdx.x, gridDim.x);
+    const int nt = bid % ntn, worker = bid / ntn;
+    const int n0 = nt * TN;
+    const int tile = worker;
+    if (tile >= ntiles) return;  // block-uniform
+    const int M = p.M, cout = p.cout, dcs = p.dst_cs;
+    const int c0 = p.src0_ch, ncb0 = c0 / 32;
+    const int c1 = CIN - c0;
+
+    uint4 a[FR][WCB];
+    {
+        const T* w = (const T*)p.w;
+#pragma unroll
+        for (int i = 0; i < FR; ++i) {
+            const int n = min(n0 + wn * WTN + i * 16 + frow, cout - 1);
+#pragma unroll
+            for (int c = 0; c < WCB; ++c) a[i][c] = *(const uint4*)(w + (long long)n * CIN + (wk * WCB + c) * 32 + fq * 8);
+        }
+    }
+    float bias[FR][4];
+#pragma unroll
+    for (int i = 0; i < FR; ++i) {
+        const int n = n0 + wn * WTN + i * 16 + fq * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[i][r] = n + r < cout ? p.bias[n + r] : 0.0f;
+    }
+    uint32_t boff[FC];
+#pragma unroll
+    for (int j = 0; j < FC; ++j) boff[j] = (uint32_t)(((wm * FC + j) * 16 + frow) * ps * 16 + fq * 16);
+
+    // per-lane DMA slot geometry: pixel of the tile | 16-byte chunk << 16 (-1: pad slot)
+    int geo[GB];
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+        const int L = wave + NW * i;
+        const int r = L < l0 ? 0 : 1;
+        const int s = 64 * (L - r * l0) + lane;
+        const int hp = s / ps, ch = s - hp * ps;
+        const bool st = L < l0 + l1 && hp < TM && ch < (r ? c1 : c0) / 8;
+        geo[i] = st ? (hp | (ch << 16)) : -1;
+    }
+    const uint32_t lds0 = dma::lds_addr(smem);
+    const dma::u32x4 srd0 = dma::srd(p.sptr[0], (uint32_t)((long long)M * p.scs[0] * 2));
+    const dma::u32x4 srd1 = dma::srd(p.nsrc > 1 ? p.sptr[1] : p.sptr[0],
+                                     (uint32_t)((long long)M * (p.nsrc > 1 ? p.scs[1] : p.scs[0]) * 2));
+    const int scs0 = p.scs[0], scs1 = p.nsrc > 1 ? p.scs[1] : 0;
+
+    auto issue = [&](int t, int kb) {
+        const int m0 = t * TM;
+#pragma unroll
+        for (int i = 0; i < GB; ++i) {
+            const int L = wave + NW * i;
+            if (L < l0 + l1) {
+                const int g = geo[i];
+                const int m = m0 + (g & 0xffff);
+                const bool ok = g >= 0 && m < M;
+                const uint32_t ldsa = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(kb * HBYTES + L * 1024));
+                const bool r0 = L < l0;  // wave-uniform: the DMA reads one source
+                dma::u32x4 rs = r0 ? srd0 : srd1;
+                rs.x = __builtin_amdgcn_readfirstlane(rs.x);
+                rs.y = __builtin_amdgcn_readfirstlane(rs.y);
+                rs.z = __builtin_amdgcn_readfirstlane(rs.z);
+                rs.w = __builtin_amdgcn_readfirstlane(rs.w);
+                const uint32_t voff = ok ? (uint32_t)((m * (r0 ? scs0 : scs1) + (g >> 16) * 8) * 2) : dma::kOob;
+                dma::load16(rs, voff, 0u, ldsa);
+            }
+        }
+    };
+
+    const bool silu = p.act == YXH_ACT_SILU;
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const __amdgpu_buffer_rsrc_t dsrd =
+        __builtin_amdgcn_make_buffer_rsrc(p.dst, (short)0, (int)((long long)M * dcs * 2), 0x00020000);
+    auto epi_piece = [&](const int tprev, const f32x4 (&ap)[FR][FCO], const int o, const int i) {
+        const int j = wk + WK * o;
+        const int m = tprev * TM + (wm * FC + j) * 16 + frow;
+        const int n = n0 + wn * WTN + i * 16 + fq * 4;
+        const bool ok = j < FC && m < M && n < cout;
+        const int od = ok ? (m * dcs + n) * 2 : (int)dma::kOob;
+        T t[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float x = ap[i][o][q] + bias[i][q];
+            t[q] = from_f32<T>(silu ? yxh::silu<false>(x) : x);
+        }
+        u32x2 u;
+        __builtin_memcpy(&u, t, 8);
+        __builtin_amdgcn_raw_buffer_store_b64(u, dsrd, od, 0, 0);
+    };
+
+    f32x4 accp[FR][FCO];
+    constexpr int NP = FR * FCO;
+    auto tile_step = [&](const int t, const int k, const int tprev, auto epi) -> int {
+        constexpr bool EPI = decltype(epi)::value;
+        const int kb = k & 1;
+        const int next = t + nwork;
+        dma::wait_vm<0>();
+        dma::barrier();
+        if (next < ntiles) issue(next, kb ^ 1);
+
+        f32x4 acc[FR][FC];
+#pragma unroll
+        for (int i = 0; i < FR; ++i)
+#pragma unroll
+            for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* hb = smem + kb * HBYTES;
+        uint4 bf[2][FC];
+        auto load_b = [&](int s, uint4 (&d)[FC]) {
+            const int cg = wk * WCB + s;
+            const int so = cg < ncb0 ? cg * 64 : l0 * 1024 + (cg - ncb0) * 64;
+#pragma unroll
+            for (int j = 0; j < FC; ++j) d[j] = *(const uint4*)(hb + boff[j] + so);
+        };
+        load_b(0, bf[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);
+#pragma unroll
+        for (int s = 0; s < WCB; ++s) {
+            if (s + 1 < WCB) load_b(s + 1, bf[(s + 1) & 1]);
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], a[i][s], bf[s & 1][j]);
+            if constexpr (EPI)
+                if (s < NP) epi_piece(tprev, accp, s / FR, s % FR);
+            if (s + 1 < WCB) __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);
+#pragma unroll
+            for (int m = 0; m < FR * FC; ++m) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if constexpr (EPI) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+        }
+        if constexpr (EPI)
+#pragma unroll
+            for (int q = WCB; q < NP; ++q) epi_piece(tprev, accp, q / FR, q % FR);
+
+        if constexpr (WK > 1) {
+            char* red = smem + 2 * HBYTES;
+            const int grp = wm * WN + wn;
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j) {
+                    const int own = j % WK;
+                    if (own != wk) {
+                        const int slot = wk < own ? wk : wk - 1;
+                        *(f32x4*)(red + (((grp * FR + i) * FC + j) * (WK - 1) + slot) * 1024 + lane * 16) = acc[i][j];
+                    }
+                }
+            dma::barrier();
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j)
+                    if (j % WK == wk) {
+                        f32x4 v = acc[i][j];
+#pragma unroll
+                        for (int o = 0; o < WK - 1; ++o)
+                            v += *(const f32x4*)(red + (((grp * FR + i) * FC + j) * (WK - 1) + o) * 1024 + lane * 16);
+                        accp[i][j / WK] = v;
+                    }
+        } else {
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j) accp[i][j] = acc[i][j];
+        }
+        return next;
+    };
+
+    issue(tile, 0);
+    int cur = tile;
+    int next = tile_step(cur, 0, 0, std::false_type{});
+    int k = 1;
+    for (; next < ntiles; ++k) {
+        const int prev = cur;
+        cur = next;
+        next = tile_step(cur, k, prev, std::true_type{});
+    }
+#pragma unroll
+    for (int o = 0; o < FCO; ++o)
+#pragma unroll
+        for (int i = 0; i < FR; ++i) epi_piece(cur, accp, o, i);
+}
+
+template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC = 1>
+static int launch_ws1(const ConvParams& p, hipStream_t st) {
+    if (p.cin != CIN) {
+        set_error("conv_ws1 variant built for %d input channels", CIN);
+        return YXH_EUNSUPPORTED;
+    }
+    const int c0 = p.src0_ch, c1 = CIN - c0;
+    if (!p.src_dense || !p.dst_dense || p.dst_f32 || p.accum || p.res || p.pw1 ||
+        (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) || p.cout % 8 || c0 % 32 || c1 % 32 ||
+        (p.nsrc == 1) != (c1 == 0)) {
+        set_error("conv_ws1: dense 1x1 over 32-channel-aligned sources, 16-bit dst, SiLU/no activation, %d input channels",
+                  CIN);
+        return YXH_EUNSUPPORTED;
+    }
+    const long long M = p.M;
+    if (M * p.scs[0] * 2 >= (1LL << 31) || (p.nsrc > 1 && M * p.scs[1] * 2 >= (1LL << 31)) ||
+        M * p.dst_cs * 2 >= (1LL << 31)) {
+        set_error("conv_ws1: tensors exceed 31-bit byte offsets");
+        return YXH_EUNSUPPORTED;
+    }
+    // one pixel stride for both regions, 2 x odd 16-byte slots (conflict-free fragment reads)
+    int ps = std::max(c0, c1) / 8;
+    ps += (6 - ps % 4) % 4;
+    const int l0 = (TM * ps + 63) / 64, l1 = c1 ? (TM * ps + 63) / 64 : 0;
+    if (l0 + l1 > (TM * (CIN / 8 + 6) + 63) / 64 + 2) {
+        set_error("conv_ws1: source split %d + %d does not fit the LDS image", c0, c1);
+        return YXH_EUNSUPPORTED;
+    }
+    const long long ntiles = (M + TM - 1) / TM;
+    const int ntn = (p.cout + TN - 1) / TN;
+    const int nwork = (int)std::min<long long>(ntiles, std::max(1, 256 * BPC / ntn));
+    hipLaunchKernelGGL((conv_ws1<T, CIN, TM, TN, WN, WK, WM, BPC>), dim3((unsigned)(nwork * ntn)),
+                       dim3(64 * WN * WK * WM), 0, st, p, (int)ntiles, ntn, nwork, ps, l0, l1);
+    YXH_CHECK_LAUNCH("conv_ws1 launch");
+    return YXH_OK;
+}
+
+template <typename T>
+static int ws1_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
+    // id -> (CIN, TM, TN, WN, WK, WM[, blocks per CU])
+    switch (id) {
+        case 1: return launch_ws1<T, 64, 128, 64, 2, 1, 2, 2>(p, st);
+        case 2: return launch_ws1<T, 64, 256, 64, 2, 1, 4, 1>(p, st);
+        case 3: return launch_ws1<T, 128, 64, 128, 4, 1, 1, 2>(p, st);
+        case 4: return launch_ws1<T, 128, 128, 64, 2, 1, 2, 2>(p, st);
+        case 5: return launch_ws1<T, 256, 64, 128, 4, 1, 1, 2>(p, st);
+        case 6: return launch_ws1<T, 256, 64, 64, 2, 1, 2, 2>(p, st);
+        case 7: return launch_ws1<T, 512, 32, 128, 4, 1, 1, 1>(p, st);
+        case 8: return launch_ws1<T, 512, 64, 64, 2, 2, 2, 1>(p, st);
+        case 9: return launch_ws1<T, 1024, 32, 64, 2, 2, 2, 1>(p, st);
+        case 10: return launch_ws1<T, 256, 128, 128, 4, 1, 2, 1>(p, st);
+        default: set_error("conv_ws1 tile id %d", id); return YXH_EINVAL;
+    }
+}
+
+int conv_ws1_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st) {
+    if (p.taps != 1 || p.stride != 1 || p.pad != 0) {
+        set_error("conv_ws1 needs a 1x1 s1 conv");
+        return YXH_EUNSUPPORTED;
+    }
+    if (dtype == YXH_BF16) return ws1_dispatch_t<bf16>(id, p, st);
+    if (dtype == YXH_F16) return ws1_dispatch_t<f16>(id, p, st);
+    set_error("conv_ws1 is built for bf16/f16");
+    return YXH_EUNSUPPORTED;
+}
+
+}  // namespace yxh

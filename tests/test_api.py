@@ -118,7 +118,12 @@ def test_planner_topology_and_flops(name, hw, gflop, anchors):
     heads = kinds.count(4)
     if name in ("yolox_s", "yolox_l"):  # head widths 128 / 256 (yolox_x: 320, unfused)
         assert heads == 3
-    assert kinds.count(0) == n_bn_convs - n_csp - fused_head + 2 * (3 - heads) - 1
+    # ... and a 16-bit plan folds each fusable Bottleneck's conv1 into its 3x3 (one op)
+    n_fused_bneck = sum(1 for o in ctx.ops if o.args.get("pre_spec") is not None)
+    n_bneck = sum(1 for x in m.modules() if x.__class__.__name__ == "Bottleneck")
+    assert n_fused_bneck == sum(1 for x in m.modules() if x.__class__.__name__ == "Bottleneck"
+                                and ctx.bottleneck_fusable(x)) <= n_bneck
+    assert kinds.count(0) == n_bn_convs - n_csp - fused_head + 2 * (3 - heads) - 1 - n_fused_bneck
 
 
 def test_synthetic_weights_are_deterministic():

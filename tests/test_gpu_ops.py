@@ -713,11 +713,11 @@ def test_conv_ws_3x3(dtype, geom):
 
 @pytest.mark.parametrize("ch,H,W,B", [(32, 37, 45, 2), (64, 40, 24, 3), (128, 20, 22, 4), (64, 80, 80, 4)])
 @pytest.mark.parametrize("shortcut", [True, False])
-def test_conv_ws_fused_bottleneck(ch, H, W, B, shortcut):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_ws_fused_bottleneck(ch, H, W, B, shortcut, dtype):
     """Fused Bottleneck (ids 191-196; network_blocks.py:77-99): conv1 1x1 + SiLU computed on
     the 3x3's halo in LDS (zero outside the image), conv2 3x3 + SiLU, + x, vs torch fp32 on
-    the same rounded operands (t rounded to bf16 as the kernel holds it)."""
-    dtype = torch.bfloat16
+    the same rounded operands (t rounded to the compute dtype as the kernel holds it)."""
     c1, bn1 = make_conv(ch, ch, 1, 1, seed=ch + 1)
     c3, bn3 = make_conv(ch, ch, 3, 1, seed=ch + 2)
     x = torch.randn(B, ch, H, W, generator=torch.Generator().manual_seed(H * W))
@@ -739,6 +739,45 @@ def test_conv_ws_fused_bottleneck(ch, H, W, B, shortcut):
     assert ran >= 1
     with pytest.raises(NotImplementedError):  # a plain tile refuses a fused descriptor
         run_conv([(X, 0, ch, 0)], c3, bn3, dtype, tile=2 * 166, pre=(w1, b1))
+
+
+WS1_GEOMS = [  # sources (channels, buffer channels, channel offset), cout, H, W, batch
+    ([(64, 64, 0)], 64, 37, 45, 3), ([(32, 64, 0), (32, 32, 0)], 64, 40, 24, 2), ([(128, 160, 16)], 128, 20, 21, 4),
+    ([(128, 256, 0), (128, 128, 0)], 256, 20, 20, 2), ([(256, 256, 0)], 128, 23, 17, 3),
+    ([(256, 512, 256), (256, 256, 0)], 512, 11, 13, 4), ([(1024, 1024, 0)], 512, 10, 10, 4),
+    ([(256, 256, 0)], 256, 40, 40, 32)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("geom", WS1_GEOMS)
+def test_conv_ws1_1x1(dtype, geom):
+    """conv_ws1 (ids 201-210): weight-stationary persistent 1x1 conv over one or two dense
+    sources (channel slices of wider buffers), output into a channel slice, every variant
+    built for this cin vs torch fp32; partial last pixel tile, cout tails of the block."""
+    srcs, cout, H, W, B = geom
+    cin = sum(c for c, _, _ in srcs)
+    conv, bn = make_conv(cin, cout, 1, 1, seed=cin + cout)
+    g = torch.Generator().manual_seed(H * W + cin)
+    parts, bufs = [], []
+    for c, cb, off in srcs:
+        x = torch.randn(B, c, H, W, generator=g)
+        buf = torch.zeros(B, H, W, cb, dtype=dtype, device=DEV)
+        buf[..., off:off + c] = nhwc(x, dtype)
+        parts.append(x)
+        bufs.append((buf, off, c, 0))
+    want = ref_conv(torch.cat(parts, 1), conv, bn, "silu")
+    out = torch.zeros(B, H, W, cout + 16, dtype=dtype, device=DEV)
+    ran = 0
+    for tid in range(201, 211):
+        try:
+            y = run_conv(bufs, conv, bn, dtype, out=out, out_coff=8, tile=2 * tid)
+        except NotImplementedError as e:
+            assert "input channels" in str(e), e
+            continue
+        close(y[..., 8:8 + cout].permute(0, 3, 1, 2), want, dtype)
+        assert not y[..., :8].any() and not y[..., 8 + cout:].any()
+        ran += 1
+    assert ran >= 1
 
 
 def test_conv_ws_residual_and_strided_dst():
