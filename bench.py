@@ -494,7 +494,7 @@ def main():
             "chunk": plan.chunk,
         },
         "roofline": {
-            "kernel": "the forward conv stack (conv_r3h / conv_r3 / conv_pwf / stem_rows / head_pred: every launch of one forward; HIP events on the plan stream around each graph replay)",
+            "kernel": "the forward conv stack (conv_ws / conv_ws1 / conv_r3h / conv_pwf / stem_rows / head_pred: every launch of one forward; HIP events on the plan stream around each graph replay)",
             "bound": "mfma",
             "achieved": round(achieved, 2),
             "peak": PEAK_BF16_TFLOPS if args.dtype != "fp32" else PEAK_F32_TFLOPS,

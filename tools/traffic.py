@@ -13,7 +13,7 @@ import json
 import sys
 from collections import defaultdict
 
-FWD_KEYS = ("conv_igemm", "conv_glds", "conv_rows", "conv_pw", "conv_r3", "head_pred", "stem_conv", "stem_rows", "spp_maxpool",
+FWD_KEYS = ("conv_igemm", "conv_glds", "conv_rows", "conv_pw", "conv_r3", "conv_ws", "head_pred", "stem_conv", "stem_rows", "spp_maxpool",
             "focus_pack", "dwconv")
 
 
