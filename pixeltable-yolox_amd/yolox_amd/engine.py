@@ -103,8 +103,10 @@ class OpRec:
     lane: int = 0  # graph branch (yxh_graph_create_lanes); 0 = backbone / neck
 
 
-# YOLOX_AMD_FUSE_BOTTLENECK=0 plans every Bottleneck as its two convs (A/B measurement)
-_FUSE_BOTTLENECK = os.environ.get("YOLOX_AMD_FUSE_BOTTLENECK", "1") != "0"
+# Bottleneck fusion is opt-in (Plan(fuse_bottleneck=True) or YOLOX_AMD_FUSE_BOTTLENECK=1): in one
+# process on one box (tools/ab_fuse.py) the two-launch form is 1.8 % faster (2.001 vs 2.038 ms per
+# yolox_s bs32 forward) -- the fused kernel's 1x1-on-the-halo phase is not overlapped with MFMAs
+_FUSE_BOTTLENECK = os.environ.get("YOLOX_AMD_FUSE_BOTTLENECK", "0") == "1"
 
 
 class PlanCtx:
@@ -120,7 +122,6 @@ class PlanCtx:
         self.device = device
         self.fuse_stem = fuse_stem
         # Bottleneck conv1 (1x1) folded into conv2's 3x3 (conv_ws fused tiles): 16-bit only
-        # (yolox_s bs32: per-layer sum 2.294 -> 2.268 ms, 10 fewer launches)
         self.fuse_bottleneck = fuse_bottleneck and dtype != torch.float32
         self.buffers: list[Buffer] = []
         self.weights: list[WeightSpec] = []
