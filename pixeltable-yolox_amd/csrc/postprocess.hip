@@ -50,39 +50,67 @@ __device__ __forceinline__ unsigned int ordered(float f) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-__global__ __launch_bounds__(64) void pp_filter(float* pred, int A, int C, float conf, PPWork w) {
+// Filter (boxes.py:36-52): one block = 64 anchor rows staged in LDS; four lanes per row
+// each take the argmax over a quarter of the classes (first maximum wins, as a serial
+// strict '>' scan does), combined with two lane shuffles.
+__global__ __launch_bounds__(256) void pp_filter(float* pred, int A, int C, float conf, PPWork w) {
     extern __shared__ float tile[];  // [64][5+C]
     const int D = 5 + C;
-    const int b = blockIdx.y, a0 = blockIdx.x * 64, lane = threadIdx.x;
+    const int b = blockIdx.y, a0 = blockIdx.x * 64, tid = threadIdx.x;
     const int rows = min(64, A - a0);
     float* src = pred + ((long long)b * A + a0) * D;
-    for (int q = lane; q < rows * D; q += 64) tile[q] = src[q];
+    for (int q = tid; q < rows * D; q += 256) tile[q] = src[q];
     __syncthreads();
-    if (lane < rows) {
-        float* p = tile + lane * D;
+    const int r = tid >> 2, part = tid & 3;
+    const float* p = tile + min(r, rows - 1) * D;
+    // the serial scan starts from class 0 and replaces on a strict '>': quarter 0 does
+    // exactly that; later quarters start empty (bi == C) and so skip NaNs and never win
+    // a tie against a lower class; only quarter 0 can hold a NaN (class 0 itself)
+    const int per = (C + 3) / 4, c0 = part * per, c1 = min(C, c0 + per);
+    float best = part == 0 ? p[5] : -INFINITY;
+    int bi = part == 0 ? 0 : C;
+    for (int c = part == 0 ? 1 : c0; c < c1; ++c) {
+        const float v = p[5 + c];
+        if (v > best) { best = v; bi = c; }
+    }
+#pragma unroll
+    for (int off = 1; off < 4; off <<= 1) {
+        const float ob = __shfl_xor(best, off);
+        const int oi = __shfl_xor(bi, off);
+        bool take;
+        if (oi >= C) take = false;
+        else if (bi >= C) take = true;
+        else if (best != best) take = false;  // ours: class 0 is NaN, the serial answer
+        else if (ob != ob) take = true;       // theirs
+        else take = ob > best || (ob == best && oi < bi);
+        if (take) { best = ob; bi = oi; }
+    }
+    if (part == 0 && r < rows) {
         const float cx = p[0], cy = p[1], bw = p[2], bh = p[3];
         const float hw = bw / 2.0f, hh = bh / 2.0f;
         const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
-        float* g = src + lane * D;
+        float* g = src + r * D;
         g[0] = x1; g[1] = y1; g[2] = x2; g[3] = y2;
-        float best = p[5];
-        int bi = 0;
-        for (int c = 1; c < C; ++c) {
-            const float v = p[5 + c];
-            if (v > best) { best = v; bi = c; }
-        }
         const float obj = p[4];
         const float sc = obj * best;
         if (sc >= conf) {
-            const int a = a0 + lane;
+            const int a = a0 + r;
             const int slot = atomicAdd(&w.cnt[b], 1);
             w.slot_of[(long long)b * A + a] = slot;
             w.key[(long long)b * A + slot] =
                 ((unsigned long long)(~ordered(sc)) << 32) | (unsigned int)a;
-            float* r = w.cand + ((long long)b * A + slot) * kRow;
-            *(float4*)r = make_float4(x1, y1, x2, y2);
-            *(float4*)(r + 4) = make_float4(obj, best, (float)bi, sc);
+            float* o = w.cand + ((long long)b * A + slot) * kRow;
+            *(float4*)o = make_float4(x1, y1, x2, y2);
+            *(float4*)(o + 4) = make_float4(obj, best, (float)bi, sc);
         }
+    }
+}
+
+// counters of the filter (per image) and the caller's detection counts, zeroed in one launch
+__global__ __launch_bounds__(256) void pp_init(int B, int* cnt, int* counts) {
+    for (int q = threadIdx.x; q < B; q += 256) {
+        cnt[q] = 0;
+        counts[q] = 0;
     }
 }
 
@@ -348,12 +376,10 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     w.srt = (float*)take(sizeof(float) * kRow * (size_t)B * A);
     w.mask = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * w.cap * w.capw);
     unsigned long long* key2 = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * A);
-    int rc = check_hip(hipMemsetAsync(w.cnt, 0, sizeof(int) * B, st), "memset counters");
-    if (rc) return rc;
-    rc = check_hip(hipMemsetAsync(counts, 0, sizeof(int) * B, st), "memset counts");
-    if (rc) return rc;
+    hipLaunchKernelGGL(pp_init, dim3(1), dim3(256), 0, st, B, w.cnt, counts);
+    YXH_CHECK_LAUNCH("pp_init");
     if (A == 0) return YXH_OK;
-    hipLaunchKernelGGL(pp_filter, dim3((A + 63) / 64, B), dim3(64), lds, st, pred, A, C, conf, w);
+    hipLaunchKernelGGL(pp_filter, dim3((A + 63) / 64, B), dim3(256), lds, st, pred, A, C, conf, w);
     YXH_CHECK_LAUNCH("pp_filter");
     const int nch = (A + kSortCap - 1) / kSortCap;
     hipLaunchKernelGGL(pp_sort_chunk, dim3(nch, B), dim3(1024), 0, st, A, w);

@@ -80,6 +80,25 @@ def test_score_ties_are_resolved_by_anchor_order(oracle):
     run_both(oracle, pred, 4, 0.1, 0.3, vanilla=0)
 
 
+@pytest.mark.parametrize("C", [80, 7, 3, 1])
+def test_class_argmax_ties_across_quarters(oracle, C):
+    """The filter's class argmax runs as four partial scans + lane shuffles: equal maxima
+    in different quarters (and -inf / all-equal rows) must give the serial first maximum,
+    as the oracle's strict '>' scan (torch.max on the CPU tensor) does."""
+    pred = synthetic_pred(2, 640, C, 13, dense=True)
+    pred[..., 4] = 0.9
+    q = max(1, (C + 3) // 4)
+    for a in range(0, 640, 5):  # same maximum in the first class of every quarter
+        pred[:, a, 5:] = 0.1
+        for k in range(0, C, q):
+            pred[:, a, 5 + k] = 0.7
+    pred[:, 1::7, 5:] = 0.25  # all classes equal
+    pred[:, 3::11, 5:] = -np.inf  # scores below conf: filtered
+    pred[:, 2::13, 5 + C - 1] = 0.95  # the last class wins outright
+    run_both(oracle, pred, C, 0.05, 0.5)
+    run_both(oracle, pred, C, 0.05, 0.5, agnostic=True)
+
+
 def test_single_class_many_overlaps(oracle):
     pred = synthetic_pred(2, 1024, 1, 5, dense=True)
     run_both(oracle, pred, 1, 0.0, 0.5)
