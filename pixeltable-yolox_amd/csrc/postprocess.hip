@@ -244,10 +244,14 @@ __device__ __forceinline__ int image_mode(int n, int agnostic, long long vanilla
     return (4LL * n > vanilla_numel) ? 2 : 1;
 }
 
-__global__ __launch_bounds__(64) void pp_mask(int A, double thr, int agnostic, long long vanilla_numel,
-                                              PPWork w) {
+// Suppression bitmask, one 64 x 64 (row block, column block) pair per work item: the four
+// waves of a block each test 16 of the 64 columns for every row and the partial words meet
+// in LDS (the tests of one row are independent, so the bits are those of a serial scan).
+__global__ __launch_bounds__(256) void pp_mask(int A, double thr, int agnostic, long long vanilla_numel,
+                                               PPWork w) {
     __shared__ Box cols[64];
-    const int b = blockIdx.y, lane = threadIdx.x;
+    __shared__ unsigned long long part[4][64];
+    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = w.cnt[b];
     if (n <= 0) return;
     const int mode = image_mode(n, agnostic, vanilla_numel);
@@ -265,23 +269,26 @@ __global__ __launch_bounds__(64) void pp_mask(int A, double thr, int agnostic, l
         while (rb > 0 && S(rb) > pi) --rb;
         while (rb + 1 < nb && S(rb + 1) <= pi) ++rb;
         const int cb = rb + (int)(pi - S(rb));
-        const int j = cb * 64 + lane;
         __syncthreads();
-        if (j < n) cols[lane] = load_box(srt + (long long)j * kRow, mode, step);
+        if (tid < 64 && cb * 64 + tid < n) cols[tid] = load_box(srt + (long long)(cb * 64 + tid) * kRow, mode, step);
         __syncthreads();
         const int i = rb * 64 + lane;
-        if (i >= n) continue;
-        const Box bi = load_box(srt + (long long)i * kRow, mode, step);
         unsigned long long bits = 0;
-        const int jn = min(64, n - cb * 64);
-        for (int t = 0; t < jn; ++t) {
-            const int jj = cb * 64 + t;
-            if (jj <= i) continue;
-            const Box& bj = cols[t];
-            if (mode == 2 && bj.cls != bi.cls) continue;
-            if (suppresses(bi, bj, thr)) bits |= 1ull << t;
+        if (i < n) {
+            const Box bi = load_box(srt + (long long)i * kRow, mode, step);
+            const int jn = min(64, n - cb * 64);
+            for (int t = wv * 16; t < min(jn, wv * 16 + 16); ++t) {
+                const int jj = cb * 64 + t;
+                if (jj <= i) continue;
+                const Box& bj = cols[t];
+                if (mode == 2 && bj.cls != bi.cls) continue;
+                if (suppresses(bi, bj, thr)) bits |= 1ull << t;
+            }
         }
-        w.mask[((long long)b * w.cap + i) * w.capw + cb] = bits;
+        part[wv][lane] = bits;
+        __syncthreads();
+        if (tid < 64 && i < n)
+            w.mask[((long long)b * w.cap + i) * w.capw + cb] = part[0][lane] | part[1][lane] | part[2][lane] | part[3][lane];
     }
 }
 
@@ -301,10 +308,13 @@ __global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int
     const unsigned long long* mrow = w.mask + (long long)b * w.cap * w.capw;
     float* out = det + (long long)b * A * 7;
     int nk = 0;
+    // the diagonal word of block blk + 1 is loaded while block blk is scanned
+    unsigned long long diag_next = lane < n ? mrow[(long long)lane * w.capw] : 0ull;
     for (int blk = 0; blk < nw; ++blk) {
         const int row = blk * 64 + lane;
         const int cnt = min(64, n - blk * 64);
-        const unsigned long long diag = row < n ? mrow[(long long)row * w.capw + blk] : 0ull;
+        const unsigned long long diag = diag_next;
+        diag_next = (blk + 1 < nw && row + 64 < n) ? mrow[(long long)(row + 64) * w.capw + blk + 1] : 0ull;
         unsigned long long cur = removed[blk];
         unsigned long long kept = 0;
         for (int t = 0; t < cnt; ++t) {
@@ -395,7 +405,7 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     }
     hipLaunchKernelGGL(pp_gather, dim3(B), dim3(1024), 0, st, A, w, (const unsigned long long*)cur);
     YXH_CHECK_LAUNCH("pp_gather");
-    hipLaunchKernelGGL(pp_mask, dim3(128, B), dim3(64), 0, st, A, nms, agnostic, vanilla_numel, w);
+    hipLaunchKernelGGL(pp_mask, dim3(128, B), dim3(256), 0, st, A, nms, agnostic, vanilla_numel, w);
     YXH_CHECK_LAUNCH("pp_mask");
     hipLaunchKernelGGL(pp_reduce, dim3(B), dim3(64), (size_t)w.capw * 8, st, A, w, det, counts);
     YXH_CHECK_LAUNCH("pp_reduce");
