@@ -22,55 +22,11 @@
 // TN = 64 (4 waves along pixels) or 128 (2 x 2); CH 16-byte chunks (8 channels each
 // for 16-bit types) per stage.
 #include "conv_common.hpp"
+#include "lds_dma.hpp"
 
 namespace yxh {
 
 namespace {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-template <int N>
-__device__ __forceinline__ void r3_wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ void r3_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
-
-// raw buffer descriptor (stride 0, byte-range checked): out-of-range loads return 0
-__device__ __forceinline__ u32x4 r3_srd(const void* base, uint32_t bytes) {
-    const uint64_t a = (uint64_t)base;
-    u32x4 r;
-    r.x = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    r.y = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu);
-    r.z = __builtin_amdgcn_readfirstlane(bytes);
-    r.w = 0x00020000u;
-    return r;
-}
-
-__device__ __forceinline__ void r3_dma(u32x4 srd, uint32_t voff, uint32_t soff, uint32_t lds) {
-    uint32_t saved;  // M0 is reserved to the compiler: save and restore it around the DMA
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(saved)
-        : "v"(voff), "s"(srd), "s"(soff), "s"(lds)
-        : "memory");
-}
-
-__device__ __forceinline__ uint32_t r3_lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-__device__ __forceinline__ int r3_xcd_remap(int id, int nblk) {
-    const int q = nblk / 8, r = nblk % 8, xcd = id % 8;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
-}
-
-constexpr uint32_t kR3Oob = 0x80000000u;  // beyond any descriptor range: reads 0
 
 // Probe builds only (tools/r3_split.sh): 1 = no MFMA / LDS reads, 2 = no DMA
 #ifndef YXH_R3_PROBE
@@ -115,7 +71,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nblk = tiles_x * tiles_y * (p.M / p.ohw) * ntn;
-    const int bid = r3_xcd_remap(blockIdx.x, nblk);
+    const int bid = dma::xcd_remap(blockIdx.x, nblk);
     const int nt = bid % ntn;
     int t = bid / ntn;
     const int tx_i = t % tiles_x;
@@ -126,8 +82,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
     const int wr = wave / WM, wc = wave % WM;
     const int cin = p.cin, scs = p.scs[0], in_w = p.in_w, in_h = p.in_h;
 
-    const u32x4 wsrd = r3_srd(p.w, (uint32_t)((long long)p.cout * 9 * cin * ES));
-    const u32x4 xsrd = r3_srd((const T*)p.sptr[0] + (long long)b * p.sbs[0],
+    const dma::u32x4 wsrd = dma::srd(p.w, (uint32_t)((long long)p.cout * 9 * cin * ES));
+    const dma::u32x4 xsrd = dma::srd((const T*)p.sptr[0] + (long long)b * p.sbs[0],
                               (uint32_t)((long long)in_h * in_w * scs * ES));
 
     // per-lane DMA offsets, fixed for the block's life
@@ -138,7 +94,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
         const int kx = s / (CH * TN), rem = s - kx * (CH * TN);
         const int c = rem / TN, rp = rem - c * TN;
         const int n = min(n0 + (rp ^ (2 * (c & 3) + (c >> 2))), p.cout - 1);
-        aoff[i] = s < A_SLOTS ? (uint32_t)(((n * 9 + kx) * cin + c * EPC) * ES) : kR3Oob;
+        aoff[i] = s < A_SLOTS ? (uint32_t)(((n * 9 + kx) * cin + c * EPC) * ES) : dma::kOob;
     }
     uint32_t boff[GB][3];  // per kernel row ky
 #pragma unroll
@@ -152,10 +108,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
         for (int ky = 0; ky < 3; ++ky) {
             const int iy = iy0 + ky;
             const bool ok = sb < B_SLOTS && iy >= 0 && iy < in_h && ix >= 0 && ix < in_w;
-            boff[i][ky] = ok ? (uint32_t)(((iy * in_w + ix) * scs + c * EPC) * ES) : kR3Oob;
+            boff[i][ky] = ok ? (uint32_t)(((iy * in_w + ix) * scs + c * EPC) * ES) : dma::kOob;
         }
     }
-    const uint32_t lds0 = r3_lds_addr(smem) + (uint32_t)wave * 1024;
+    const uint32_t lds0 = dma::lds_addr(smem) + (uint32_t)wave * 1024;
 
     auto issue_to = [&](int cb, auto kyc, uint32_t slot) {
         constexpr int ky = decltype(kyc)::value;
@@ -165,11 +121,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
 #pragma unroll
         for (int i = 0; i < GA; ++i)
             if (A_PART == 0 || i + 1 < GA || wave < A_PART)
-                r3_dma(wsrd, aoff[i], soa, base + i * NW * 1024);
+                dma::load16(wsrd, aoff[i], soa, base + i * NW * 1024);
 #pragma unroll
         for (int i = 0; i < GB; ++i)
             if (B_PART == 0 || i + 1 < GB || wave < B_PART)
-                r3_dma(xsrd, boff[i][ky], sob, base + A_BYTES + i * NW * 1024);
+                dma::load16(xsrd, boff[i][ky], sob, base + A_BYTES + i * NW * 1024);
     };
     auto issue = [&](int cb, auto kyc) { issue_to(cb, kyc, (uint32_t)decltype(kyc)::value); };
 
@@ -225,9 +181,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
     // this wave's DMA instructions per stage, and "wait until one younger stage remains"
     const int cnt = G - (A_PART && wave >= A_PART ? 1 : 0) - (B_PART && wave >= B_PART ? 1 : 0);
     auto wait_younger = [&]() {
-        if (cnt == G) r3_wait_vm<G>();
-        else if (cnt == G - 1) r3_wait_vm<G - 1>();
-        else r3_wait_vm<G - 2>();
+        if (cnt == G) dma::wait_vm<G>();
+        else if (cnt == G - 1) dma::wait_vm<G - 1>();
+        else dma::wait_vm<G - 2>();
     };
     if constexpr (NBUF == 3) {
         issue(0, K0{});
@@ -237,16 +193,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
         for (int cb = 0; cb < ncb; ++cb) {
             const bool more = cb + 1 < ncb;
             wait_younger();
-            r3_barrier();
+            dma::barrier();
             issue(cb, K2{});
             compute(0);
             wait_younger();
-            r3_barrier();
+            dma::barrier();
             if (more) issue(cb + 1, K0{});
             compute(1);
             if (more) wait_younger();
-            else r3_wait_vm<0>();
-            r3_barrier();
+            else dma::wait_vm<0>();
+            dma::barrier();
             if (more) issue(cb + 1, K1{});
             compute(2);
         }
@@ -256,22 +212,22 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
         issue_to(0, K0{}, 0u);
         for (int cb = 0; cb < ncb; ++cb) {
             const uint32_t s0 = (uint32_t)(3 * cb) & 1u;
-            r3_wait_vm<0>();
-            r3_barrier();
+            dma::wait_vm<0>();
+            dma::barrier();
             issue_to(cb, K1{}, s0 ^ 1u);
             compute((int)s0);
-            r3_wait_vm<0>();
-            r3_barrier();
+            dma::wait_vm<0>();
+            dma::barrier();
             issue_to(cb, K2{}, s0);
             compute((int)(s0 ^ 1u));
-            r3_wait_vm<0>();
-            r3_barrier();
+            dma::wait_vm<0>();
+            dma::barrier();
             if (cb + 1 < ncb) issue_to(cb + 1, K0{}, s0 ^ 1u);
             compute((int)s0);
         }
     }
-    r3_wait_vm<0>();
-    r3_barrier();
+    dma::wait_vm<0>();
+    dma::barrier();
     const int OH = p.out_h, OW = p.out_w, mb = b * p.ohw;
     conv_epilogue_map<T, TN, TM, WN, WM, NBUF * BUF>(
         p, acc, smem,
@@ -296,11 +252,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3(ConvParams p, int tiles
 __device__ __forceinline__ void r3_wait_dyn(int n) {
     switch (n) {
 #define YXH_W(k) \
-    case k: r3_wait_vm<k>(); break;
+    case k: dma::wait_vm<k>(); break;
         YXH_W(1) YXH_W(2) YXH_W(3) YXH_W(4) YXH_W(5) YXH_W(6) YXH_W(7) YXH_W(8) YXH_W(9) YXH_W(10)
         YXH_W(11) YXH_W(12) YXH_W(13) YXH_W(14) YXH_W(15)
 #undef YXH_W
-        default: r3_wait_vm<0>(); break;
+        default: dma::wait_vm<0>(); break;
     }
 }
 
@@ -327,7 +283,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3h(ConvParams p, int tile
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nblk = tiles_x * tiles_y * (p.M / p.ohw) * ntn;
-    const int bid = r3_xcd_remap(blockIdx.x, nblk);
+    const int bid = dma::xcd_remap(blockIdx.x, nblk);
     const int nt = bid % ntn;
     int t = bid / ntn;
     const int tx_i = t % tiles_x;
@@ -338,8 +294,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3h(ConvParams p, int tile
     const int wr = wave / WM, wc = wave % WM;
     const int cin = p.cin, scs = p.scs[0], in_w = p.in_w, in_h = p.in_h;
 
-    const u32x4 wsrd = r3_srd(p.w, (uint32_t)((long long)p.cout * 9 * cin * ES));
-    const u32x4 xsrd = r3_srd((const T*)p.sptr[0] + (long long)b * p.sbs[0],
+    const dma::u32x4 wsrd = dma::srd(p.w, (uint32_t)((long long)p.cout * 9 * cin * ES));
+    const dma::u32x4 xsrd = dma::srd((const T*)p.sptr[0] + (long long)b * p.sbs[0],
                               (uint32_t)((long long)in_h * in_w * scs * ES));
     uint32_t aoff[GA];
 #pragma unroll
@@ -348,7 +304,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3h(ConvParams p, int tile
         const int kx = s / (CH * TN), rem = s - kx * (CH * TN);
         const int c = rem / TN, rp = rem - c * TN;
         const int n = min(n0 + (rp ^ (2 * c)), p.cout - 1);
-        aoff[i] = s < A_SLOTS ? (uint32_t)(((n * 9 + kx) * cin + c * EPC) * ES) : kR3Oob;
+        aoff[i] = s < A_SLOTS ? (uint32_t)(((n * 9 + kx) * cin + c * EPC) * ES) : dma::kOob;
     }
     uint32_t boff[GB];
 #pragma unroll
@@ -359,9 +315,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3h(ConvParams p, int tile
         const int hy = hp / HX, hx = hp - hy * HX;
         const int iy = oy0 * S - 1 + hy, ix = ox0 * S - 1 + hx;
         const bool ok = sb < B_SLOTS && iy >= 0 && iy < in_h && ix >= 0 && ix < in_w;
-        boff[i] = ok ? (uint32_t)(((iy * in_w + ix) * scs + c * EPC) * ES) : kR3Oob;
+        boff[i] = ok ? (uint32_t)(((iy * in_w + ix) * scs + c * EPC) * ES) : dma::kOob;
     }
-    const uint32_t lds0 = r3_lds_addr(smem) + (uint32_t)wave * 1024;
+    const uint32_t lds0 = dma::lds_addr(smem) + (uint32_t)wave * 1024;
     // this wave's share of a stage's wave-loads
     const int cnt_a = GA - (A_PART && wave >= A_PART ? 1 : 0);
     const int cnt_b = GB - (B_PART && wave >= B_PART ? 1 : 0);
@@ -372,7 +328,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3h(ConvParams p, int tile
         const uint32_t soa = (uint32_t)((ky * 3 * cin + cb * KST) * ES);
 #pragma unroll
         for (int i = 0; i < GA; ++i)
-            if (A_PART == 0 || i + 1 < GA || wave < A_PART) r3_dma(wsrd, aoff[i], soa, base + i * NW * 1024);
+            if (A_PART == 0 || i + 1 < GA || wave < A_PART) dma::load16(wsrd, aoff[i], soa, base + i * NW * 1024);
     };
     auto issue_b = [&](int cb) {
         if constexpr (YXH_R3_PROBE == 2) return;
@@ -380,7 +336,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3h(ConvParams p, int tile
         const uint32_t sob = (uint32_t)(cb * KST * ES);
 #pragma unroll
         for (int i = 0; i < GB; ++i)
-            if (B_PART == 0 || i + 1 < GB || wave < B_PART) r3_dma(xsrd, boff[i], sob, base + i * NW * 1024);
+            if (B_PART == 0 || i + 1 < GB || wave < B_PART) dma::load16(xsrd, boff[i], sob, base + i * NW * 1024);
     };
 
     f32x4 acc[FR][FC];
@@ -435,23 +391,23 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3h(ConvParams p, int tile
     for (int cb = 0; cb < ncb; ++cb) {
         const bool more = cb + 1 < ncb;
         r3_wait_dyn(cnt_a);  // stage (cb, 0) landed; (cb, 1) may fly
-        r3_barrier();
+        dma::barrier();
         issue_a(cb, 2);
         compute(cb, K0{});
         r3_wait_dyn(cnt_a);  // (cb, 1) landed; (cb, 2) may fly
-        r3_barrier();
+        dma::barrier();
         if (more) {
             issue_a(cb + 1, 0);
             issue_b(cb + 1);
         }
         compute(cb, K1{});
         r3_wait_dyn(more ? cnt_a + cnt_b : 0);  // (cb, 2) landed; (cb + 1, 0) may fly
-        r3_barrier();
+        dma::barrier();
         if (more) issue_a(cb + 1, 1);
         compute(cb, K2{});
     }
-    r3_wait_vm<0>();
-    r3_barrier();
+    dma::wait_vm<0>();
+    dma::barrier();
     const int OH = p.out_h, OW = p.out_w, mb = b * p.ohw;
     conv_epilogue_map<T, TN, TM, WN, WM, SMEM>(
         p, acc, smem,
