@@ -126,6 +126,34 @@ def test_planner_topology_and_flops(name, hw, gflop, anchors):
     assert kinds.count(0) == n_bn_convs - n_csp - fused_head + 2 * (3 - heads) - 1 - n_fused_bneck
 
 
+def test_planner_fused_bottleneck_ping_pong():
+    """Plan(fuse_bottleneck=True): every fusable Bottleneck (C 32/64/128, 3x3 s1 conv2) is one
+    conv op carrying conv1 as pre_spec; no fused op writes the buffer it reads (neighbouring
+    tiles read its halo), and after an odd chain CspLayer.conv3 reads [last | x_2] as two
+    sources."""
+    from yolox_amd.config import named_config
+    from yolox_amd.engine import OutBuffer, PlanCtx
+    m = named_config("yolox_s").get_model()
+    ctx = PlanCtx(1, torch.bfloat16, torch.device("cpu"), fuse_bottleneck=True)
+    feats = m.backbone.plan(ctx, ctx.image(640, 640))
+    m.head.plan(ctx, feats, OutBuffer(sum(f.lh * f.lw for f in feats), 85))
+    fused = [o for o in ctx.ops if o.args.get("pre_spec") is not None]
+    assert len(fused) == 10 and {o.args["cin"] for o in fused} == {32, 64, 128}
+    for o in fused:
+        src, out = o.args["srcs"][0], o.args["out"]
+        assert o.args["k"] == 3 and o.args["stride"] == 1 and len(o.args["srcs"]) == 1
+        assert not (out.buf is src.buf and out.coff < src.coff + src.ch and src.coff < out.coff + out.ch)
+        if o.args["residual"] is not None:
+            assert o.args["residual"] is src
+    two_src_1x1 = [o for o in ctx.ops if o.kind == 0 and o.args["k"] == 1 and len(o.args["srcs"]) == 2
+                   and not any(s.up for s in o.args["srcs"])]
+    assert len(two_src_1x1) == 6  # dark2/3/4, C3_p4, C3_p3, C3_n3: n = 1 or 3, odd
+    assert round(ctx.flops / 1e9, 2) == 26.69  # same algorithmic work as the split plan
+    fp32 = PlanCtx(1, torch.float32, torch.device("cpu"), fuse_bottleneck=True)
+    feats = m.backbone.plan(fp32, fp32.image(640, 640))
+    assert not any(o.args.get("pre_spec") is not None for o in fp32.ops)  # 16-bit only
+
+
 def test_synthetic_weights_are_deterministic():
     from yolox_amd.weights import synthetic_state_dict
     shapes = {"a.conv.weight": (4, 3, 3, 3), "a.bn.weight": (4,), "head.cls_preds.0.bias": (80,)}
