@@ -5,7 +5,9 @@ configs[1]: batch 32 per GPU, synthetic uniform [0,255] images, seeded weights).
 One step = one batch through the hot path: the captured hipGraph of the whole
 forward (Focus -> CSPDarknet -> PAFPN -> decoupled head with fused decode, 82
 kernels) followed by device post-processing (filter, sort, bitmask NMS) at the
-processor defaults (conf 0.5, nms 0.65).  Inputs are resident in HBM (bf16 NHWC)
+processor defaults (conf 0.5, nms 0.65); a batch's NMS runs on a side stream beside the
+next batch's forward, which waits only for the NMS filter pass (the one reader of the
+forward's output) -- --serial-nms runs them back to back on one stream.  Inputs are resident in HBM (bf16 NHWC)
 before the timed region.  With --gpus N (torchrun, one process per GPU) each rank
 runs an independent replica -- inference has no exchange step, so there is no
 collective in the data path -- and value = all images / max
@@ -82,6 +84,8 @@ def parse():
     ap.add_argument("--nms", type=float, default=0.65)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--serial-nms", action="store_true",
+                    help="NMS behind each forward on one stream (default: beside the next batch's forward)")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise only the process topology (spawn, rendezvous, barrier, max over ranks) "
                          "with gloo on the CPU; prints one JSON line from rank 0")
@@ -429,17 +433,39 @@ def main():
         engine.save_tune_cache(args.tune_file)
     plan.capture()
     A = plan.anchors
-    det = torch.empty(B, A, 7, dtype=torch.float32, device=dev)
-    counts = torch.empty(B, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    # Serving pipeline: the NMS of batch k runs on a side stream beside the forward of batch
+    # k+1. Only NMS's filter pass reads the forward's output, so the next replay waits for
+    # that pass alone (event recorded by yxh_postprocess_ev); detections are double-buffered.
+    # --serial-nms puts the NMS back behind each forward on one stream.
+    side = torch.cuda.Stream(dev) if not args.serial_nms else stream
+    dets = [torch.empty(B, A, 7, dtype=torch.float32, device=dev) for _ in range(2)]
+    cnts = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(2)]
+    filt = [torch.cuda.Event() for _ in range(2)]
+    fwd_done = torch.cuda.Event()
+    state = {"k": 0}
+    det, counts = dets[0], cnts[0]
 
     def step(ev0=None, ev1=None):
+        nonlocal det, counts
+        k = state["k"]
+        if k > 0 and not args.serial_nms:
+            stream.wait_event(filt[(k - 1) % 2])  # the previous batch's filter has read the output
         if ev0 is not None:
             ev0.record(stream)
         out = plan.replay()
         if ev1 is not None:
             ev1.record(stream)
-        postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts)
+        det, counts = dets[k % 2], cnts[k % 2]
+        if args.serial_nms:
+            postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts)
+        else:
+            fwd_done.record(stream)
+            side.wait_event(fwd_done)
+            with torch.cuda.stream(side):
+                postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts,
+                                   filter_done=filt[k % 2])
+        state["k"] = k + 1
 
     for _ in range(args.warmup):
         step()

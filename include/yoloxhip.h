@@ -211,6 +211,14 @@ int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_cla
                     float conf_thre, double nms_thre, int32_t class_agnostic,
                     int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,
                     size_t workspace_bytes, void* stream);
+/* The same, recording `filter_done` (a hipEvent_t, may be NULL) on `stream` as soon as the
+ * filter pass has read `pred` and written its xyxy columns: every later pass reads only the
+ * workspace, so a producer may overwrite `pred` once that event has fired (a serving loop
+ * runs the next batch's forward beside this batch's NMS). */
+int yxh_postprocess_ev(float* pred, int32_t batch, int32_t anchors, int32_t num_classes,
+                       float conf_thre, double nms_thre, int32_t class_agnostic,
+                       int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,
+                       size_t workspace_bytes, void* filter_done, void* stream);
 
 /*
  * yxh_yolox_loss: YoloxHead.get_losses (yolo_head.py:253-411) with SimOTA assignment

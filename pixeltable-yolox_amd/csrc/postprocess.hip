@@ -361,7 +361,7 @@ size_t pp_workspace(int B, int A) {
 }
 
 int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
-                float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st) {
+                float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t filter_done) {
     YXH_CHECK_ARG(pred && det && counts, "null pointer");
     YXH_CHECK_ARG(B > 0 && A >= 0 && C > 0, "postprocess shape B=%d A=%d C=%d", B, A, C);
     YXH_CHECK_ARG(ws && ws_bytes >= pp_workspace(B, A), "workspace too small (%zu < %zu)", ws_bytes,
@@ -388,9 +388,14 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     unsigned long long* key2 = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * A);
     hipLaunchKernelGGL(pp_init, dim3(1), dim3(256), 0, st, B, w.cnt, counts);
     YXH_CHECK_LAUNCH("pp_init");
-    if (A == 0) return YXH_OK;
+    int rc = YXH_OK;
+    if (A == 0) return filter_done ? check_hip(hipEventRecord(filter_done, st), "record filter_done") : YXH_OK;
     hipLaunchKernelGGL(pp_filter, dim3((A + 63) / 64, B), dim3(256), lds, st, pred, A, C, conf, w);
     YXH_CHECK_LAUNCH("pp_filter");
+    if (filter_done) {  // pred is read and rewritten only by the filter
+        rc = check_hip(hipEventRecord(filter_done, st), "record filter_done");
+        if (rc) return rc;
+    }
     const int nch = (A + kSortCap - 1) / kSortCap;
     hipLaunchKernelGGL(pp_sort_chunk, dim3(nch, B), dim3(1024), 0, st, A, w);
     YXH_CHECK_LAUNCH("pp_sort_chunk");

@@ -63,7 +63,7 @@ int yolox_loss_bwd(const float* preds, const float* raw, const float* labels, in
                    const float* piou, const int* num_fg, const float* gtot, int use_l1, int dt, void* g_ro,
                    void* g_cls, hipStream_t st);
 int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
-                float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st);
+                float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t filter_done);
 int head_pred_launch(const yxh_head_desc* d, hipStream_t st);
 
 static int run_op(const yxh_op& op, hipStream_t st) {
@@ -140,7 +140,14 @@ int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_cla
                     double nms_thre, int32_t class_agnostic, int64_t vanilla_numel, float* det, int32_t* counts,
                     void* workspace, size_t workspace_bytes, void* stream) {
     return postprocess(pred, batch, anchors, num_classes, conf_thre, nms_thre, class_agnostic, vanilla_numel, det,
-                       counts, workspace, workspace_bytes, (hipStream_t)stream);
+                       counts, workspace, workspace_bytes, (hipStream_t)stream, nullptr);
+}
+
+int yxh_postprocess_ev(float* pred, int32_t batch, int32_t anchors, int32_t num_classes, float conf_thre,
+                       double nms_thre, int32_t class_agnostic, int64_t vanilla_numel, float* det, int32_t* counts,
+                       void* workspace, size_t workspace_bytes, void* filter_done, void* stream) {
+    return postprocess(pred, batch, anchors, num_classes, conf_thre, nms_thre, class_agnostic, vanilla_numel, det,
+                       counts, workspace, workspace_bytes, (hipStream_t)stream, (hipEvent_t)filter_done);
 }
 
 size_t yxh_yolox_loss_workspace_bytes(int32_t batch, int32_t anchors, int32_t max_labels) {

@@ -38,9 +38,12 @@ def _workspace(device, B: int, A: int) -> torch.Tensor:
 def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: float = 0.7,
                        nms_thre: float = 0.45, class_agnostic: bool = False,
                        vanilla_numel: int = VANILLA_NUMEL_CPU, det: Optional[torch.Tensor] = None,
-                       counts: Optional[torch.Tensor] = None):
+                       counts: Optional[torch.Tensor] = None, filter_done: Optional[torch.cuda.Event] = None):
     """Asynchronous form: returns (det [B, A, 7], counts [B] int32) on the device,
-    nothing synchronised.  ``prediction`` (fp32, on device) becomes xyxy in place."""
+    nothing synchronised, on the current stream.  ``prediction`` (fp32, on device) becomes xyxy
+    in place.  ``filter_done`` is recorded once ``prediction`` is no longer read (after the
+    filter pass): a producer that waits on it may overwrite ``prediction`` while the rest of
+    the NMS runs."""
     N.require_device(prediction, "prediction")
     if prediction.dtype != torch.float32 or not prediction.is_contiguous():
         raise ValueError("prediction must be a contiguous float32 [B, A, 5+C] tensor")
@@ -53,10 +56,18 @@ def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: fl
     if counts is None:
         counts = torch.empty(B, dtype=torch.int32, device=dev)
     ws = _workspace(dev, B, A)
-    N.check(N.lib().yxh_postprocess(
-        prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre), int(bool(class_agnostic)),
-        int(vanilla_numel), det.data_ptr(), counts.data_ptr(), ws.data_ptr(), ws.numel(),
-        N.stream_ptr(dev)), "postprocess")
+    if filter_done is not None and not filter_done.cuda_event:
+        filter_done.record()  # torch creates the event lazily, on its first record
+    if filter_done is None:
+        N.check(N.lib().yxh_postprocess(
+            prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre), int(bool(class_agnostic)),
+            int(vanilla_numel), det.data_ptr(), counts.data_ptr(), ws.data_ptr(), ws.numel(),
+            N.stream_ptr(dev)), "postprocess")
+    else:
+        N.check(N.lib().yxh_postprocess_ev(
+            prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre), int(bool(class_agnostic)),
+            int(vanilla_numel), det.data_ptr(), counts.data_ptr(), ws.data_ptr(), ws.numel(),
+            filter_done.cuda_event, N.stream_ptr(dev)), "postprocess")
     return det, counts
 
 

@@ -99,6 +99,30 @@ def test_class_argmax_ties_across_quarters(oracle, C):
     run_both(oracle, pred, C, 0.05, 0.5, agnostic=True)
 
 
+def test_filter_done_event_lets_the_producer_overwrite_pred(oracle):
+    """yxh_postprocess_ev: once `filter_done` has fired, nothing reads `pred` any more -- a
+    forward may overwrite it while the rest of the NMS runs (bench.py's pipelined step)."""
+    from yolox_amd.utils.boxes import postprocess_device
+    pred = synthetic_pred(3, 2000, 80, 21, dense=True)
+    p = torch.from_numpy(pred.copy()).cuda()
+    ev, side = torch.cuda.Event(), torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        det, counts = postprocess_device(p, 80, 0.3, 0.65, filter_done=ev)
+    torch.cuda.current_stream().wait_event(ev)
+    want_xyxy = p[..., :4].clone()  # ordered after the filter's in-place write
+    p.fill_(-7.0)  # the next batch's forward
+    torch.cuda.synchronize()
+    ref = pred.copy()
+    want = oracle.postprocess(ref, 80, 0.3, 0.65)
+    np.testing.assert_array_equal(want_xyxy.cpu().numpy(), ref[..., :4])
+    n = counts.cpu().tolist()
+    for b, w in enumerate(want):
+        assert n[b] == (0 if w is None else len(w))
+        if w is not None:
+            np.testing.assert_array_equal(det[b, :n[b]].cpu().numpy(), w)
+
+
 def test_single_class_many_overlaps(oracle):
     pred = synthetic_pred(2, 1024, 1, 5, dense=True)
     run_both(oracle, pred, 1, 0.0, 0.5)
