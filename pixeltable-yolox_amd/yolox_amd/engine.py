@@ -674,7 +674,7 @@ class Plan:
                 pass
 
     # -------------------------------------------------------------- autotune
-    def autotune(self, reps: int = 3, verbose: bool = False) -> dict:
+    def autotune(self, reps: int = 5, verbose: bool = False) -> dict:
         """Pick each conv's tile (TN x TM, K slabs) by timing every variant on the
         device with HIP events, on this plan's own buffers (after one real forward so
         they hold realistic values).  Results are cached per layer shape for the
