@@ -118,6 +118,11 @@ typedef struct {
 } yxh_conv_desc;
 
 #define YXH_CONV_ACCUMULATE 1
+/* Two groups over one source of 2*cin channels: output channels [0, cout/2) read source channels
+ * [0, cin), [cout/2, cout) read [cin, 2*cin) -- a head level's cls_convs[k][1] | reg_convs[k][1]
+ * over its stacked [cls | reg] features (yolo_head.py:160-161) as ONE launch; conv_ws tiles,
+ * 16-bit, 3x3 s1 only. */
+#define YXH_CONV_GROUPS2 2
 
 int yxh_conv2d(const yxh_conv_desc* d, void* stream);
 

@@ -441,7 +441,12 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         dilated |= q.upsample == 2;
         chs += q.channels;
     }
-    YXH_CHECK_ARG(chs == d->cin, "source channels %d != cin %d", chs, d->cin);
+    const bool grp2 = (d->flags & YXH_CONV_GROUPS2) != 0;
+    YXH_CHECK_ARG(chs == (grp2 ? 2 * d->cin : d->cin), "source channels %d != cin %d%s", chs, d->cin,
+                  grp2 ? " x 2 groups" : "");
+    YXH_CHECK_ARG(!grp2 || (d->nsrc == 1 && d->groups == 1 && d->cout % 2 == 0 && !d->pre_weight && !d->residual &&
+                            dt != YXH_F32),
+                  "YXH_CONV_GROUPS2: 16-bit, one source, even cout, no residual / fused conv1");
     YXH_CHECK_ARG((d->in_h + 2 * d->pad - d->kh) / d->stride + 1 == d->out_h &&
                       (d->in_w + 2 * d->pad - d->kw) / d->stride + 1 == d->out_w,
                   "output size mismatch");
@@ -493,6 +498,12 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     p.res_dense = d->residual && d->res_bstride == (long long)p.ohw * d->res_cstride;
     p.pw1 = d->pre_weight;
     p.pb1 = d->pre_bias;
+    p.grp2 = grp2 ? 1 : 0;
+    if (grp2 && d->tile == 0) return conv_ws_dispatch(dt, d->cin == 256 ? 176 - 160 : 185 - 160, p, st);
+    if (grp2 && !((d->tile >> 1) > 160 && (d->tile >> 1) <= 190)) {
+        set_error("YXH_CONV_GROUPS2 runs on the plain conv_ws tiles (ids 161-190) only");
+        return YXH_EUNSUPPORTED;
+    }
     YXH_CHECK_ARG(!d->pre_weight || (d->pre_bias && aligned16(d->pre_weight) && d->kh == 3 && d->stride == 1 &&
                                      d->pad == 1 && d->groups == 1 && d->nsrc == 1 && dt != YXH_F32),
                   "fused Bottleneck: 16-bit 3x3 s1 conv over one source with a pre_bias");

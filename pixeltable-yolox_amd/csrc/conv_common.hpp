@@ -29,6 +29,7 @@ struct ConvParams {
     float dstride;
     const void* pw1;  // fused Bottleneck conv1 (1x1, cin -> cin) ahead of the 3x3: conv_ws only
     const float* pb1;
+    int grp2;  // YXH_CONV_GROUPS2: output half g reads source channels [g*cin, (g+1)*cin)
 };
 
 // ---------------------------------------------------------------- MFMA step

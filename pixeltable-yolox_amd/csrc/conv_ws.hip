@@ -140,6 +140,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 
     const uint32_t lds0 = dma::lds_addr(smem);
     const uint32_t bytes = (uint32_t)((long long)in_h * in_w * scs * 2);
+    const int gsrc = p.grp2 && n0 >= cout / 2 ? CIN : 0;  // YXH_CONV_GROUPS2: this half's source channels
 
     // per-lane halo slot geometry, fixed for the block's life: the slot's pixel (hy, hx)
     // in the halo and its source byte offset relative to the halo's top-left pixel
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     auto issue_halo = [&](const TileC& c, int kb) {
         const int iy0 = c.oy0 * S - 1, ix0 = c.ox0 * S - 1;
         const int base = (iy0 * in_w + ix0) * scs * 2;
-        const dma::u32x4 rsrc = dma::srd((const T*)p.sptr[0] + (long long)c.b * p.sbs[0], bytes);
+        const dma::u32x4 rsrc = dma::srd((const T*)p.sptr[0] + (long long)c.b * p.sbs[0] + gsrc, bytes);
 #pragma unroll
         for (int i = 0; i < GB; ++i) {
             const int L = wave + NW * i;
@@ -413,6 +414,10 @@ template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, in
 static int launch_ws(const ConvParams& p, hipStream_t st) {
     if (p.stride != S || p.cin != CIN) {
         set_error("conv_ws variant built for stride %d, %d input channels", S, CIN);
+        return YXH_EUNSUPPORTED;
+    }
+    if (p.grp2 && (F1 || (p.cout / 2) % TN)) {
+        set_error("conv_ws variant (%d input channels) cannot split its channel tiles over two groups", CIN);
         return YXH_EUNSUPPORTED;
     }
     if ((p.pw1 != nullptr) != F1) {

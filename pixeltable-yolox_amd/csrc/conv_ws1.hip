@@ -229,7 +229,7 @@ static int launch_ws1(const ConvParams& p, hipStream_t st) {
         return YXH_EUNSUPPORTED;
     }
     const int c0 = p.src0_ch, c1 = CIN - c0;
-    if (!p.src_dense || !p.dst_dense || p.dst_f32 || p.accum || p.res || p.pw1 ||
+    if (!p.src_dense || !p.dst_dense || p.dst_f32 || p.accum || p.res || p.pw1 || p.grp2 ||
         (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) || p.cout % 8 || c0 % 32 || c1 % 32 ||
         (p.nsrc == 1) != (c1 == 0)) {
         set_error("conv_ws1: dense 1x1 over 32-channel-aligned sources, 16-bit dst, SiLU/no activation, %d input channels",

@@ -51,6 +51,7 @@ class ConvDesc(C.Structure):
 
 
 CONV_ACCUMULATE = 1
+CONV_GROUPS2 = 2
 
 
 class OptSeg(C.Structure):

@@ -243,6 +243,31 @@ class PlanCtx:
         self.flops += 2.0 * self.batch * x.lh * x.lw * ch * ch * 10  # 1x1 + 3x3
         return out
 
+    def grouped2_fusable(self, a, b, src: View) -> bool:
+        if self.dtype == torch.float32 or not (hasattr(a, "conv") and hasattr(b, "conv")):
+            return False
+        ka, kb = a.conv, b.conv
+        same = all(getattr(ka, f) == getattr(kb, f) for f in ("in_channels", "out_channels", "kernel_size",
+                                                              "stride", "padding", "groups"))
+        return (same and ka.kernel_size == (3, 3) and ka.stride == (1, 1) and ka.groups == 1
+                and ka.in_channels in (128, 256) and src.ch == 2 * ka.in_channels and ka.out_channels % 64 == 0
+                and getattr(a, "act_name", "silu") == getattr(b, "act_name", "silu") == "silu")
+
+    def conv_grouped2(self, ms, src: View) -> View:
+        """Two same-shaped 3x3 BaseConvs over the two halves of one source (a head level's
+        cls_convs[k][1] | reg_convs[k][1] over [cls | reg], yolo_head.py:160-161) as ONE launch
+        (YXH_CONV_GROUPS2); the output buffer is [a | b]."""
+        ka, kb = ms[0].conv, ms[1].conv
+        cin, half = ka.in_channels, ka.out_channels
+        out = self.buffer(src.lh, src.lw, 2 * half).full()
+        spec = self._weights([(ka, ms[0].bn), (kb, ms[1].bn)], cin)
+        self.ops.append(OpRec(N.OP_CONV, dict(
+            srcs=[src], out=out, residual=None, spec=spec, cin=cin, cout=2 * half, k=3, stride=1, pad=1, groups=1,
+            in_h=src.lh, in_w=src.lw, out_h=src.lh, out_w=src.lw, act=N.ACT_CODE["silu"], dst_f32=False,
+            grouped2=True)))
+        self.flops += 2.0 * self.batch * src.lh * src.lw * 2 * half * 9 * cin
+        return out
+
     def spp(self, cat: Buffer, hidden: int) -> None:
         self.ops.append(OpRec(N.OP_SPP, dict(buf=cat, c=hidden)))
 
@@ -308,7 +333,8 @@ def load_tune_cache(path: str) -> int:
 def _tune_key(d) -> tuple:
     return (d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w, d.cin, d.cout, d.kh, d.stride, d.nsrc,
             d.src[0].channels, d.src[0].upsample, d.src[1].upsample if d.nsrc > 1 else 0,
-            bool(d.residual), d.dst_dtype, d.dst_cstride == d.cout, d.act >= N.ACT_DECODE, bool(d.pre_weight))
+            bool(d.residual), d.dst_dtype, d.dst_cstride == d.cout, d.act >= N.ACT_DECODE, bool(d.pre_weight),
+            d.flags)
 
 
 def op_dependencies(ops) -> list:
@@ -493,6 +519,7 @@ class Plan:
                 spec: WeightSpec = a["spec"]
                 d.weight = self.warena.data_ptr() + spec.w_off
                 d.bias = self.barena.data_ptr() + spec.b_off
+                d.flags = N.CONV_GROUPS2 if a.get("grouped2") else 0
                 pre = a.get("pre_spec")
                 if pre is not None:
                     d.pre_weight = self.warena.data_ptr() + pre.w_off

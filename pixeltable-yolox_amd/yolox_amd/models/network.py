@@ -270,8 +270,16 @@ class YoloxHead(_Planned):
                 c, r = cr.buf.slice(0, hw_), cr.buf.slice(hw_, hw_)
             else:
                 c, r = c0.plan(ctx, [s]), r0.plan(ctx, [s])
-            c = self.cls_convs[k][1].plan(ctx, [c])
-            r = self.reg_convs[k][1].plan(ctx, [r])
+            c1, r1 = self.cls_convs[k][1], self.reg_convs[k][1]
+            if (c.buf is r.buf and c.coff == 0 and r.coff == c.ch and c.buf.c == 2 * c.ch
+                    and ctx.grouped2_fusable(c1, r1, c.buf.full())):
+                # cls_convs[k][1] | reg_convs[k][1] over [cls | reg]: one two-group launch
+                cr2 = ctx.conv_grouped2([c1, r1], c.buf.full())
+                half = c1.conv.out_channels
+                c, r = cr2.buf.slice(0, half), cr2.buf.slice(half, half)
+            else:
+                c = c1.plan(ctx, [c])
+                r = r1.plan(ctx, [r])
             ctx.head_preds(k, self, c, r, out, a_off, self.strides[k], train)
             for rec in ctx.ops[n0:]:  # levels are independent: one graph branch each
                 rec.lane = 1 + k

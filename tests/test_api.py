@@ -123,7 +123,10 @@ def test_planner_topology_and_flops(name, hw, gflop, anchors):
     n_bneck = sum(1 for x in m.modules() if x.__class__.__name__ == "Bottleneck")
     assert n_fused_bneck == sum(1 for x in m.modules() if x.__class__.__name__ == "Bottleneck"
                                 and ctx.bottleneck_fusable(x)) <= n_bneck
-    assert kinds.count(0) == n_bn_convs - n_csp - fused_head + 2 * (3 - heads) - 1 - n_fused_bneck
+    # ... and a 16-bit plan runs cls_convs[k][1] | reg_convs[k][1] as one two-group launch
+    n_grouped = sum(1 for o in ctx.ops if o.args.get("grouped2"))
+    assert n_grouped == (3 if name in ("yolox_s", "yolox_l") else n_grouped)
+    assert kinds.count(0) == n_bn_convs - n_csp - fused_head + 2 * (3 - heads) - 1 - n_fused_bneck - n_grouped
 
 
 def test_planner_fused_bottleneck_ping_pong():

@@ -75,7 +75,7 @@ def ref_conv(x, conv, bn, act):
 
 
 def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_coff=0, out_c=None, tile=0, flags=0,
-             pre=None):
+             pre=None, groups2=False):
     """srcs: list of (nhwc tensor [B,h,w,C], coff, ch, upsample)."""
     n = N()
     B = srcs[0][0].shape[0]
@@ -84,7 +84,7 @@ def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_cof
     k, s, pd = conv.kernel_size[0], conv.stride[0], conv.padding[0]
     oh, ow = (in_h + 2 * pd - k) // s + 1, (in_w + 2 * pd - k) // s + 1
     cin = sum(c for _, _, c, _ in srcs)
-    w, b = pack(conv, bn, dtype, cin if conv.groups == 1 else None)
+    w, b = pack(conv, bn, dtype, (cin // 2 if groups2 else cin) if conv.groups == 1 else None)
     cout = conv.out_channels
     if out is None:
         out = torch.zeros(B, oh, ow, out_c or cout, dtype=dtype, device=DEV)
@@ -110,6 +110,9 @@ def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_cof
     d.flags = flags
     if pre is not None:  # fused Bottleneck conv1 (packed weight, bias)
         d.pre_weight, d.pre_bias = pre[0].data_ptr(), pre[1].data_ptr()
+    if groups2:  # output half g reads source channels [g*cin, (g+1)*cin)
+        d.cin = cin // 2
+        d.flags = flags | n.CONV_GROUPS2
     n.check(n.lib().yxh_conv2d(ctypes.byref(d), n.stream_ptr()), "conv2d")
     torch.cuda.synchronize()
     return out
@@ -778,6 +781,35 @@ def test_conv_ws1_1x1(dtype, geom):
         assert not y[..., :8].any() and not y[..., 8 + cout:].any()
         ran += 1
     assert ran >= 1
+
+
+@pytest.mark.parametrize("cin,H,W,B", [(128, 20, 22, 3), (128, 80, 80, 4), (256, 20, 20, 2)])
+def test_conv_ws_two_groups(cin, H, W, B):
+    """YXH_CONV_GROUPS2 (a head level's cls_convs[k][1] | reg_convs[k][1] over [cls | reg] as one
+    launch): output half g = conv of source half g with weight rows of half g, vs torch fp32."""
+    dtype = torch.bfloat16
+    conv, bn = make_conv(cin, 2 * cin, 3, 1, seed=cin + H)  # weights [2 cin][cin][3][3]: the two stacked
+    x = torch.randn(B, 2 * cin, H, W, generator=torch.Generator().manual_seed(H * W))
+    want = ref_conv_groups2(x, conv, bn, cin)
+    X = nhwc(x, dtype)
+    ran = 0
+    for tid in range(161, 191):
+        try:
+            y = run_conv([(X, 0, 2 * cin, 0)], conv, bn, dtype, tile=2 * tid, groups2=True)
+        except NotImplementedError as e:
+            assert "input channels" in str(e), e
+            continue
+        close(y.permute(0, 3, 1, 2), want, dtype)
+        ran += 1
+    assert ran >= 1
+    with pytest.raises(NotImplementedError):  # the other kernel families refuse the two-group form
+        run_conv([(X, 0, 2 * cin, 0)], conv, bn, dtype, tile=2 * 141, groups2=True)
+
+
+def ref_conv_groups2(x, conv, bn, cin):
+    y = F.conv2d(x, conv.weight, None, 1, 1, groups=2)
+    y = F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
+    return F.silu(y)
 
 
 def test_conv_ws_residual_and_strided_dst():
