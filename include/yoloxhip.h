@@ -208,10 +208,15 @@ int yxh_letterbox_batch(const uint8_t* pool, const yxh_lb_image* images, int32_t
  *   det       [B, A, 7] fp32 out: rows [x1,y1,x2,y2,obj,cls_conf,cls_idx] in keep order
  *   counts    [B] int32 out: detections per image (0 == the reference's None)
  *   workspace >= yxh_postprocess_workspace_bytes(B, A)
- * Any candidate count (anchors <= 2^19 per image); the workspace holds a
- * [B][A][ceil(A/64)] u64 suppression matrix.
+ * Any candidate count (anchors <= 2^19 per image).  The u64 suppression matrix is built
+ * and consumed in passes of R sorted rows x ceil(A/64) words per image, R chosen so one
+ * pass holds at most the mask budget (256 MiB over the batch), so the workspace grows
+ * linearly in A for large inputs instead of quadratically.
  */
 size_t yxh_postprocess_workspace_bytes(int32_t batch, int32_t anchors);
+/* Process-wide mask budget in bytes (0 = the 256 MiB default).  Changes the workspace size
+ * and the pass count of later calls; tests use a tiny budget to force many passes. */
+void yxh_set_nms_mask_budget(size_t bytes);
 int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_classes,
                     float conf_thre, double nms_thre, int32_t class_agnostic,
                     int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,

@@ -20,11 +20,19 @@
 //   pp_reduce : one wave per image walks the sorted boxes, keeps the unsuppressed
 //               ones and ORs their mask rows (greedy NMS), writing detections in keep
 //               order.
+//   The matrix is built and consumed in passes of R sorted rows (R from a fixed byte
+//   budget, pp_rows_per_pass): pass p holds rows [p*R, (p+1)*R) against every column, its
+//   reduce continues the removed set and keep count of pass p-1 (kept in the workspace).
+//   Greedy NMS only ever reads the rows of boxes it has reached, so the result is that
+//   of the whole matrix; the workspace no longer grows with the square of the anchor
+//   count, and passes past an image's candidate count exit at once.
 //
 // Bit-exactness: IoU is evaluated with exactly torchvision's CPU fp32 operation
 // sequence (areas=(x2-x1)*(y2-y1); inter=w*h; inter/((a_i+a_j)-inter) > (double)thr),
 // so FP contraction is disabled for this file (and -ffp-contract=off at build).
 #pragma clang fp contract(off)
+
+#include <algorithm>
 
 #include "yxh_common.hpp"
 
@@ -33,6 +41,8 @@ namespace yxh {
 constexpr int kSortCap = 16384;      // keys sorted per block in LDS (128 KiB)
 constexpr int kMaxAnchors = 1 << 19;  // pp_reduce keeps one removed-bit per candidate in LDS
 constexpr int kRow = 8;  // x1 y1 x2 y2 obj conf cls score
+constexpr size_t kMaskBudget = 256ull << 20;  // bytes of suppression words per pass (all images)
+size_t g_mask_budget = kMaskBudget;  // yxh_set_nms_mask_budget (tests: force many passes)
 
 struct PPWork {
     int* cnt;         // [B]
@@ -41,7 +51,8 @@ struct PPWork {
     unsigned long long* key;  // [B][A]
     float* cand;      // [B][A][8]
     float* srt;       // [B][A][8] sorted
-    unsigned long long* mask;  // [B][cap][capw]
+    unsigned long long* mask;     // [B][rows per pass][capw]
+    unsigned long long* removed;  // [B][capw] greedy state carried across passes
     int cap, capw;
 };
 
@@ -247,28 +258,31 @@ __device__ __forceinline__ int image_mode(int n, int agnostic, long long vanilla
 // Suppression bitmask, one 64 x 64 (row block, column block) pair per work item: the four
 // waves of a block each test 16 of the 64 columns for every row and the partial words meet
 // in LDS (the tests of one row are independent, so the bits are those of a serial scan).
+// This pass covers row blocks [rb0, rb1) (sorted rows [64*rb0, 64*rb1)) x column blocks >= rb.
 __global__ __launch_bounds__(256) void pp_mask(int A, double thr, int agnostic, long long vanilla_numel,
-                                               PPWork w) {
+                                               PPWork w, int rb0, int rb1) {
     __shared__ Box cols[64];
     __shared__ unsigned long long part[4][64];
     const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = w.cnt[b];
-    if (n <= 0) return;
+    const int nb = (n + 63) / 64;
+    rb1 = min(rb1, nb);
+    if (rb0 >= rb1) return;
     const int mode = image_mode(n, agnostic, vanilla_numel);
     const float step = w.maxc[b] + 1.0f;
-    const int nb = (n + 63) / 64;
-    const long long pairs = (long long)nb * (nb + 1) / 2;
+    const int nr = nb - rb0;  // column blocks of the pass's first row block
+    // row block rb0 + k holds nr - k pairs; S(k) = pairs of the first k row blocks
+    auto S = [nr](long long k) { return k * nr - k * (k - 1) / 2; };
+    const long long pairs = S(rb1 - rb0);
     const float* srt = w.srt + (long long)b * A * kRow;
     for (long long pi = blockIdx.x; pi < pairs; pi += gridDim.x) {
-        // triangular index -> (rb, cb), cb >= rb
-        // rows r < rb hold S(rb) = rb*nb - rb*(rb-1)/2 pairs; largest rb with S(rb) <= pi
-        const double q = 2.0 * nb + 1.0;
-        int rb = (int)((q - sqrt(q * q - 8.0 * (double)pi)) * 0.5);
-        rb = max(0, min(rb, nb - 1));
-        auto S = [nb](long long r) { return r * nb - r * (r - 1) / 2; };
-        while (rb > 0 && S(rb) > pi) --rb;
-        while (rb + 1 < nb && S(rb + 1) <= pi) ++rb;
-        const int cb = rb + (int)(pi - S(rb));
+        const double q = 2.0 * nr + 1.0;
+        int k = (int)((q - sqrt(q * q - 8.0 * (double)pi)) * 0.5);
+        k = max(0, min(k, rb1 - rb0 - 1));
+        while (k > 0 && S(k) > pi) --k;
+        while (k + 1 < rb1 - rb0 && S(k + 1) <= pi) ++k;
+        const int rb = rb0 + k;
+        const int cb = rb + (int)(pi - S(k));
         __syncthreads();
         if (tid < 64 && cb * 64 + tid < n) cols[tid] = load_box(srt + (long long)(cb * 64 + tid) * kRow, mode, step);
         __syncthreads();
@@ -288,7 +302,8 @@ __global__ __launch_bounds__(256) void pp_mask(int A, double thr, int agnostic, 
         part[wv][lane] = bits;
         __syncthreads();
         if (tid < 64 && i < n)
-            w.mask[((long long)b * w.cap + i) * w.capw + cb] = part[0][lane] | part[1][lane] | part[2][lane] | part[3][lane];
+            w.mask[((long long)b * w.cap + (i - rb0 * 64)) * w.capw + cb] =
+                part[0][lane] | part[1][lane] | part[2][lane] | part[3][lane];
     }
 }
 
@@ -296,25 +311,32 @@ __global__ __launch_bounds__(256) void pp_mask(int A, double thr, int agnostic, 
 // removed-set words live in LDS; within a 64-box block the keep decisions are a
 // register-only scan over the block's diagonal mask words (one coalesced load),
 // then every kept lane ORs its own mask row into the later words (independent
-// loads across lanes) -- no dependent global load per kept box.
-__global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int* counts) {
+// loads across lanes) -- no dependent global load per kept box.  One launch per pass
+// (row blocks [rb0, rb1)): the removed set and the keep count continue from the
+// previous pass through the workspace / ``counts``.
+__global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int* counts, int rb0, int rb1) {
     extern __shared__ unsigned long long removed[];  // [capw]
     const int b = blockIdx.x, lane = threadIdx.x;
     const int n = w.cnt[b];
     const int nw = (n + 63) / 64;
-    for (int q = lane; q < nw; q += 64) removed[q] = 0;
+    rb1 = min(rb1, nw);
+    if (rb0 >= rb1) return;
+    unsigned long long* gremoved = w.removed + (long long)b * w.capw;
+    for (int q = lane; q < nw; q += 64) removed[q] = rb0 == 0 ? 0ull : gremoved[q];
     __syncthreads();
     const float* srt = w.srt + (long long)b * A * kRow;
-    const unsigned long long* mrow = w.mask + (long long)b * w.cap * w.capw;
+    // pass-local mask rows: sorted row i is row i - 64*rb0 of this pass
+    const unsigned long long* pass = w.mask + (long long)b * w.cap * w.capw;
+    auto mword = [&](int row, int col) { return pass[(long long)(row - rb0 * 64) * w.capw + col]; };
     float* out = det + (long long)b * A * 7;
-    int nk = 0;
+    int nk = rb0 == 0 ? 0 : counts[b];
     // the diagonal word of block blk + 1 is loaded while block blk is scanned
-    unsigned long long diag_next = lane < n ? mrow[(long long)lane * w.capw] : 0ull;
-    for (int blk = 0; blk < nw; ++blk) {
+    unsigned long long diag_next = rb0 * 64 + lane < n ? mword(rb0 * 64 + lane, rb0) : 0ull;
+    for (int blk = rb0; blk < rb1; ++blk) {
         const int row = blk * 64 + lane;
         const int cnt = min(64, n - blk * 64);
         const unsigned long long diag = diag_next;
-        diag_next = (blk + 1 < nw && row + 64 < n) ? mrow[(long long)(row + 64) * w.capw + blk + 1] : 0ull;
+        diag_next = (blk + 1 < rb1 && row + 64 < n) ? mword(row + 64, blk + 1) : 0ull;
         unsigned long long cur = removed[blk];
         unsigned long long kept = 0;
         for (int t = 0; t < cnt; ++t) {
@@ -332,21 +354,33 @@ __global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int
             float* o = out + (long long)pos * 7;
 #pragma unroll
             for (int c = 0; c < 7; ++c) o[c] = s[c];
-            const unsigned long long* mr = mrow + (long long)row * w.capw;
             for (int q = blk + 1; q < nw; ++q) {
-                const unsigned long long v = mr[q];
+                const unsigned long long v = mword(row, q);
                 if (v) atomicOr(&removed[q], v);
             }
         }
         nk += __popcll(kept);
         __syncthreads();
     }
+    if (rb1 < nw)  // a later pass continues from here
+        for (int q = lane; q < nw; q += 64) gremoved[q] = removed[q];
     if (lane == 0) counts[b] = nk;
 }
 
+// Sorted rows per mask pass: a multiple of 64, all rows at once when the budget allows.
+int pp_rows_per_pass(int B, int A) {
+    const size_t capw = ((size_t)A + 63) / 64;
+    const size_t all = capw * 64;
+    size_t r = g_mask_budget / ((size_t)B * capw * 8) / 64 * 64;
+    if (r < 64) r = 64;
+    return (int)(r < all ? r : all);
+}
+
+void pp_set_mask_budget(size_t bytes) { g_mask_budget = bytes ? bytes : kMaskBudget; }
+
 size_t pp_workspace(int B, int A) {
-    const size_t cap = (size_t)A;
-    const size_t capw = (cap + 63) / 64;
+    const size_t cap = (size_t)pp_rows_per_pass(B, A);
+    const size_t capw = ((size_t)A + 63) / 64;
     size_t s = 0;
     auto add = [&](size_t bytes) { s += (bytes + 255) & ~(size_t)255; };
     add(sizeof(int) * B);
@@ -357,6 +391,7 @@ size_t pp_workspace(int B, int A) {
     add(sizeof(float) * kRow * (size_t)B * A);
     add(sizeof(unsigned long long) * (size_t)B * cap * capw);
     add(sizeof(unsigned long long) * (size_t)B * A);  // merge ping-pong keys
+    add(sizeof(unsigned long long) * (size_t)B * capw);  // removed set between passes
     return s;
 }
 
@@ -376,8 +411,8 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
         return r;
     };
     YXH_CHECK_ARG(A <= kMaxAnchors, "postprocess supports at most %d anchors per image (got %d)", kMaxAnchors, A);
-    w.cap = A;
-    w.capw = (w.cap + 63) / 64;
+    w.cap = pp_rows_per_pass(B, A);
+    w.capw = (A + 63) / 64;
     w.cnt = (int*)take(sizeof(int) * B);
     w.maxc = (float*)take(sizeof(float) * B);
     w.slot_of = (int*)take(sizeof(int) * (size_t)B * A);
@@ -386,6 +421,7 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     w.srt = (float*)take(sizeof(float) * kRow * (size_t)B * A);
     w.mask = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * w.cap * w.capw);
     unsigned long long* key2 = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * A);
+    w.removed = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * w.capw);
     hipLaunchKernelGGL(pp_init, dim3(1), dim3(256), 0, st, B, w.cnt, counts);
     YXH_CHECK_LAUNCH("pp_init");
     int rc = YXH_OK;
@@ -410,10 +446,17 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     }
     hipLaunchKernelGGL(pp_gather, dim3(B), dim3(1024), 0, st, A, w, (const unsigned long long*)cur);
     YXH_CHECK_LAUNCH("pp_gather");
-    hipLaunchKernelGGL(pp_mask, dim3(128, B), dim3(256), 0, st, A, nms, agnostic, vanilla_numel, w);
-    YXH_CHECK_LAUNCH("pp_mask");
-    hipLaunchKernelGGL(pp_reduce, dim3(B), dim3(64), (size_t)w.capw * 8, st, A, w, det, counts);
-    YXH_CHECK_LAUNCH("pp_reduce");
+    const int rbp = w.cap / 64;  // row blocks per pass
+    for (int rb0 = 0; rb0 < w.capw; rb0 += rbp) {
+        // worst-case pairs of this pass (n = A): rbp row blocks x up to capw - rb0 column blocks
+        const long long worst = (long long)rbp * (w.capw - rb0);
+        const int gx = (int)std::min<long long>(worst, std::max(128, 8192 / B));
+        hipLaunchKernelGGL(pp_mask, dim3(gx, B), dim3(256), 0, st, A, nms, agnostic, vanilla_numel, w, rb0,
+                           rb0 + rbp);
+        YXH_CHECK_LAUNCH("pp_mask");
+        hipLaunchKernelGGL(pp_reduce, dim3(B), dim3(64), (size_t)w.capw * 8, st, A, w, det, counts, rb0, rb0 + rbp);
+        YXH_CHECK_LAUNCH("pp_reduce");
+    }
     return YXH_OK;
 }
 

@@ -37,6 +37,7 @@ int stem_launch(const yxh_stem_desc* d, hipStream_t st);
 int stem_pack_launch(const float* w, const float* g, const float* beta, const float* mean, const float* var,
                      float eps, int cout, int dt, void* wo, float* bo, hipStream_t st);
 size_t pp_workspace(int B, int A);
+void pp_set_mask_budget(size_t bytes);
 size_t sim_workspace(int B, int A, int L);
 int yolox_loss(const float* preds, const float* origin, const float* labels, int B, int A, int C, int L,
                const int* lhw, const int* strides, int nlev, uint8_t* fg, int* matched, float* piou, int* num_fg,
@@ -135,6 +136,8 @@ int yxh_letterbox_batch(const uint8_t* pool, const yxh_lb_image* images, int32_t
 }
 
 size_t yxh_postprocess_workspace_bytes(int32_t batch, int32_t anchors) { return pp_workspace(batch, anchors); }
+
+void yxh_set_nms_mask_budget(size_t bytes) { pp_set_mask_budget(bytes); }
 
 int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_classes, float conf_thre,
                     double nms_thre, int32_t class_agnostic, int64_t vanilla_numel, float* det, int32_t* counts,

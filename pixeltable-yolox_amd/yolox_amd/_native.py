@@ -155,6 +155,7 @@ def lib():
                                  C.c_int),
             "yxh_letterbox_batch": ([vp, vp, i32, i32, i32, i32, vp, vp], C.c_int),
             "yxh_postprocess_workspace_bytes": ([i32, i32], sz),
+            "yxh_set_nms_mask_budget": ([sz], None),
             "yxh_postprocess": ([vp, i32, i32, i32, f32, f64, i32, i64, vp, vp, vp, sz, vp], C.c_int),
             "yxh_postprocess_ev": ([vp, i32, i32, i32, f32, f64, i32, i64, vp, vp, vp, sz, vp, vp], C.c_int),
             "yxh_yolox_loss_workspace_bytes": ([i32, i32, i32], sz),
@@ -199,7 +200,7 @@ def lib():
 
 
 EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d", "yxh_head_pred",
-            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_postprocess_workspace_bytes",
+            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_postprocess_workspace_bytes", "yxh_set_nms_mask_budget",
             "yxh_postprocess", "yxh_postprocess_ev", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
             "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_spp_bwd",

@@ -23,15 +23,35 @@ VANILLA_NUMEL_CUDA = 20000
 _workspaces: dict = {}
 
 
-def _workspace(device, B: int, A: int) -> torch.Tensor:
-    """Scratch for one yxh_postprocess call, cached per (device, stream): calls in flight
-    on different streams never share it, calls on one stream are ordered by it."""
+class _Workspace:
+    """One yxh_postprocess scratch buffer per device, shared by every stream: each call
+    waits for the previous call's completion event (on whatever stream that ran) and
+    records its own, so calls on different streams never overlap on it, and a caller that
+    makes a new stream per request reuses the same buffer instead of leaking one each."""
+
+    def __init__(self):
+        self.buf: Optional[torch.Tensor] = None
+        self.done: Optional[torch.cuda.Event] = None
+
+    def acquire(self, device, need: int) -> torch.Tensor:
+        stream = torch.cuda.current_stream(device)
+        if self.done is not None:
+            stream.wait_event(self.done)
+        if self.buf is None or self.buf.numel() < need:
+            self.buf = torch.empty(need, dtype=torch.uint8, device=device)
+        self.buf.record_stream(stream)  # the allocator may recycle it only after this stream's use
+        return self.buf
+
+    def release(self, device) -> None:
+        if self.done is None:
+            self.done = torch.cuda.Event()
+        self.done.record(torch.cuda.current_stream(device))
+
+
+def _workspace(device, B: int, A: int) -> "_Workspace":
     need = int(N.lib().yxh_postprocess_workspace_bytes(B, A))
-    key = (device, N.stream_ptr(device))
-    ws = _workspaces.get(key)
-    if ws is None or ws.numel() < need:
-        ws = torch.empty(need, dtype=torch.uint8, device=device)
-        _workspaces[key] = ws
+    ws = _workspaces.setdefault(torch.device(device), _Workspace())
+    ws.acquire(device, need)
     return ws
 
 
@@ -55,19 +75,23 @@ def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: fl
         det = torch.empty(B, max(A, 1), 7, dtype=torch.float32, device=dev)
     if counts is None:
         counts = torch.empty(B, dtype=torch.int32, device=dev)
-    ws = _workspace(dev, B, A)
     if filter_done is not None and not filter_done.cuda_event:
         filter_done.record()  # torch creates the event lazily, on its first record
-    if filter_done is None:
-        N.check(N.lib().yxh_postprocess(
-            prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre), int(bool(class_agnostic)),
-            int(vanilla_numel), det.data_ptr(), counts.data_ptr(), ws.data_ptr(), ws.numel(),
-            N.stream_ptr(dev)), "postprocess")
-    else:
-        N.check(N.lib().yxh_postprocess_ev(
-            prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre), int(bool(class_agnostic)),
-            int(vanilla_numel), det.data_ptr(), counts.data_ptr(), ws.data_ptr(), ws.numel(),
-            filter_done.cuda_event, N.stream_ptr(dev)), "postprocess")
+    ws = _workspace(dev, B, A)
+    buf = ws.buf
+    try:
+        if filter_done is None:
+            N.check(N.lib().yxh_postprocess(
+                prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre),
+                int(bool(class_agnostic)), int(vanilla_numel), det.data_ptr(), counts.data_ptr(), buf.data_ptr(),
+                buf.numel(), N.stream_ptr(dev)), "postprocess")
+        else:
+            N.check(N.lib().yxh_postprocess_ev(
+                prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre),
+                int(bool(class_agnostic)), int(vanilla_numel), det.data_ptr(), counts.data_ptr(), buf.data_ptr(),
+                buf.numel(), filter_done.cuda_event, N.stream_ptr(dev)), "postprocess")
+    finally:
+        ws.release(dev)
     return det, counts
 
 

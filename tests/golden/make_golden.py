@@ -436,6 +436,40 @@ def gen_processor(ref) -> None:
     save("processor_yolox_s_640.npz", **arrays)
 
 
+def tiny_416_image():
+    """BASELINE configs[0] input: one 416x416 RGB image (r == 1 at yolox_tiny's 416 test size, so
+    the cv2 stub's identity resize is exact) -- the top-left 416x416 crop of the reference's first
+    test image."""
+    from PIL import Image
+    return Image.open(IMAGE_FILES[0]).convert("RGB").crop((0, 0, 416, 416))
+
+
+def gen_processor_tiny(ref) -> None:
+    """configs[0]: yolox_tiny single-image inference through the reference's own Yolox.__call__
+    (yolox.py:41-52 -> YoloxProcessor (416) -> YoloxModule -> postprocess), seeded weights."""
+    import hashlib
+
+    global NMS_MODE
+    NMS_MODE = "oracle"
+    model = build(ref, "yolox_tiny")
+    proc = ref.processor.YoloxProcessor("yolox_tiny")
+    yolox = ref.yolox.Yolox(model, proc)
+    im = tiny_416_image()
+    arrays = {"img.sha256": np.array(hashlib.sha256(np.asarray(im).tobytes()).hexdigest())}
+    with torch.no_grad():
+        tensor = proc([im])
+        arrays["tensor.sha256"] = np.array(hashlib.sha256(tensor.numpy().tobytes()).hexdigest())
+        arrays["tensor.shape"] = np.array(tensor.shape, np.int64)
+        for thr in (0.5, 0.3):
+            (d,) = yolox([im], threshold=thr)
+            arrays[f"t{thr}.bboxes"] = np.array(d["bboxes"], np.float64).reshape(-1, 4)
+            arrays[f"t{thr}.scores"] = np.array(d["scores"], np.float64)
+            arrays[f"t{thr}.labels"] = np.array(d["labels"], np.int64)
+            print(f"tiny 416 threshold {thr}: {len(d['labels'])} detections")
+    NMS_MODE = "record"
+    save("processor_yolox_tiny_416.npz", **arrays)
+
+
 def main() -> None:
     if not os.path.isdir(REF):
         sys.exit("reference not present: fixtures can only be generated in the build container")

@@ -7,15 +7,27 @@ configs[1]  yolox_s 640 bf16 batch 32: the autotuned, graph-captured plan bench.
 configs[2]  yolox_s 640 train step batch 8 in fp32 (the reference's default precision):
             the six loss values and every parameter gradient within 1e-3 of the
             oracle's autograd (north_star tolerance).
-configs[3]  yolox_l 640 fp16 batch 16: images 0 and 15 vs the oracle (fp16 bounds).
+configs[0]  yolox_tiny 416 single image through Yolox.from_pretrained (a local checkpoint of
+            the seeded weights) and Yolox.__call__: Detections vs the reference-run fixture
+            (processor_yolox_tiny_416.npz; the reference test's bars) and == the oracle NMS +
+            formatting on the same device output.
+configs[3]  yolox_l 640 fp16 batch 16 (bench plan): all 16 images vs the oracle's fp32 forward
+            (fp16 bounds) and device NMS on the whole batch bit-exact vs the oracle's NMS on the
+            same output.
 configs[4]  yolox_x 1280 --fp16 train: on-device SimOTA at A = 33600 anchors with up to
             120 GTs exact vs the oracle (fg mask, matched GT, num_fg; IoUs to fp32
-            rounding) plus the loss values; and an fp16-autocast train step of yolox_x at
-            1280 (batch 2) with finite losses and gradients.
+            rounding) plus the loss values; a yolox_x 1280 batch-1 train step in fp32 whose six
+            losses (rel 1e-3) and named parameter gradients (1e-3 of the tensor's max) match
+            the oracle's autograd; and the same step under fp16 autocast against the same
+            oracle with the fp16 bound stated in the test.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
+
+from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
@@ -135,11 +147,25 @@ def test_configs2_yolox_s_640_train_fp32_batch8(oracle, monkeypatch):
 
 
 def test_configs3_yolox_l_640_fp16_batch16(oracle):
+    from yolox_amd.utils.boxes import postprocess_device
     model, plan, imgs = bench_plan("yolox_l", 16, 640, torch.float16)
-    host = plan.replay().cpu().numpy()
-    ref = oracle_forward(oracle, "yolox_l", imgs[[0, 15]])
-    for got, want in zip(host[[0, 15]], ref):
+    out = plan.replay()
+    torch.cuda.synchronize()
+    host = out.cpu().numpy()
+    torch.set_num_threads(16)
+    ref = oracle_forward(oracle, "yolox_l", imgs)
+    for got, want in zip(host, ref):
         probs_close(got, want, 0.05, 0.01, 0.5)
+    # device NMS (processor defaults conf 0.5, nms 0.65) on the replayed fp16-plan output
+    pred = out.clone()
+    det, counts = postprocess_device(pred, 80, 0.5, 0.65)
+    n = counts.cpu().numpy()
+    want = oracle.postprocess(host.copy(), 80, 0.5, 0.65)
+    np.testing.assert_array_equal(pred.cpu().numpy(), oracle_xyxy(host))
+    dets = det.cpu().numpy()
+    assert (n > 0).all()
+    for b in range(16):
+        np.testing.assert_array_equal(dets[b, :n[b]], want[b])
 
 
 @pytest.mark.parametrize("seed", [0, 1])
@@ -174,16 +200,112 @@ def test_configs4_simota_1280_max_labels(oracle, seed):
         assert float(losses[k]) == pytest.approx(float(ref[k]), rel=1e-4, abs=1e-6), k
 
 
-def test_configs4_yolox_x_1280_fp16_train_step():
+def _oracle_train_step(oracle, monkeypatch, m, name, x, labels, spp_in):
+    """The oracle's fp32 autograd train step on the module's own weights, with SPP's pooling
+    ROUTING taken from the device forward (see configs[2]); returns (losses, sd)."""
+    import torch.nn.functional as F
+    sd = {k: v.detach().cpu().float().clone() for k, v in m.state_dict().items()}
+    max_pool2d = F.max_pool2d
+
+    def pool_routed_like_device(t, k, stride=None, padding=0, **kw):
+        _, idx = max_pool2d(spp_in, k, 1, k // 2, return_indices=True)
+        return t.flatten(2).gather(2, idx.flatten(2)).view_as(idx)
+
+    monkeypatch.setattr(F, "max_pool2d", pool_routed_like_device)
+    sdo = {k: v.requires_grad_("running" not in k and "num_batches" not in k) for k, v in sd.items()}
+    torch.set_num_threads(16)
+    ref = oracle.forward_train(sdo, oracle.ARCHS[name], x, labels)
+    ref["total_loss"].backward()
+    monkeypatch.setattr(F, "max_pool2d", max_pool2d)
+    return ref, sdo
+
+
+def _device_train_step(monkeypatch, m, x, labels, amp_dtype=None):
+    import yolox_amd.train as T
+    spp_conv1, seen = m.backbone.backbone.dark5[1].conv1, {}
+    base_conv = T.TrainGraph.base_conv
+
+    def recording(self, mod, inputs, out=None, residual=None, cin_store=None):
+        r = base_conv(self, mod, inputs, out, residual, cin_store)
+        if mod is spp_conv1:
+            seen["act"] = r
+        return r
+
+    monkeypatch.setattr(T.TrainGraph, "base_conv", recording)
+    m.zero_grad(set_to_none=True)
+    if amp_dtype is None:
+        out = m(x.cuda(), labels.cuda())
+    else:
+        with torch.autocast("cuda", dtype=amp_dtype):
+            out = m(x.cuda().to(amp_dtype), labels.cuda())
+    out["total_loss"].backward()
+    torch.cuda.synchronize()
+    monkeypatch.setattr(T.TrainGraph, "base_conv", base_conv)
+    a = seen["act"]
+    spp_in = a.t[..., a.coff:a.coff + a.ch].permute(0, 3, 1, 2).cpu().float()
+    return out, spp_in
+
+
+GRAD_NAMES = ("backbone.backbone.stem.conv.conv.weight", "backbone.backbone.dark2.0.conv.weight",
+              "backbone.backbone.dark5.1.conv2.conv.weight", "backbone.C3_n4.conv3.conv.weight",
+              "head.stems.0.conv.weight", "head.cls_convs.0.1.conv.weight", "head.cls_preds.0.weight",
+              "head.reg_preds.1.weight", "head.obj_preds.2.bias", "head.stems.2.bn.weight")
+
+
+def test_configs4_yolox_x_1280_train_step_vs_oracle(oracle, monkeypatch):
+    """configs[4]'s model and image size (yolox_x, 1280x1280, up to 120 labels), batch 1:
+    fp32 losses within 1e-3 of the oracle (north_star tolerance) and named gradients within
+    1e-3 of each tensor's max; then the --fp16 (autocast) step against the same oracle:
+    losses within 2e-2 relative, gradients within 5e-2 of each tensor's max (fp16 operands
+    with fp32 accumulation through ~100 layers; bound measured, not derived)."""
     from yolox_amd.models import YoloxModule
     from yolox_amd.weights import synthetic_images, synthetic_labels
     m = YoloxModule.synthetic("yolox_x", seed=0, device="cuda").train()
-    x = torch.from_numpy(synthetic_images(2, 1280, 1280, seed=5)).cuda().permute(0, 3, 1, 2).half()
-    labels = torch.from_numpy(synthetic_labels(2, 1280, 1280, max_gt=120, seed=6)).cuda()
-    with torch.autocast("cuda", dtype=torch.float16):
-        out = m(x, labels)
-    out["total_loss"].backward()
-    torch.cuda.synchronize()
-    assert all(np.isfinite(float(out[k])) for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss"))
+    x = torch.from_numpy(synthetic_images(1, 1280, 1280, seed=5)).permute(0, 3, 1, 2).float()
+    labels = torch.from_numpy(synthetic_labels(1, 1280, 1280, max_gt=120, seed=6))
+    out, spp_in = _device_train_step(monkeypatch, m, x, labels)
+    grads = {n: p.grad.cpu().clone() for n, p in m.named_parameters() if n in GRAD_NAMES}
+    ref, sdo = _oracle_train_step(oracle, monkeypatch, m, "yolox_x", x, labels, spp_in)
+    for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss", "num_fg"):
+        assert float(out[k]) == pytest.approx(float(ref[k]), rel=1e-3, abs=1e-6), k
     assert float(out["num_fg"]) > 0
-    assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+    for name in GRAD_NAMES:
+        g, gr = grads[name], sdo[name].grad
+        e = float((g - gr).abs().max() / (gr.abs().max() + 1e-12))
+        assert e < 1e-3, (name, e)
+    # --fp16: same module, autocast selects fp16 compute (trainer.py:100-104)
+    out16, _ = _device_train_step(monkeypatch, m, x, labels, torch.float16)
+    for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss"):
+        v = float(out16[k])
+        assert np.isfinite(v) and v == pytest.approx(float(ref[k]), rel=2e-2), k
+    for name, p in m.named_parameters():
+        assert torch.isfinite(p.grad).all(), name
+        if name in GRAD_NAMES:
+            gr = sdo[name].grad
+            e = float((p.grad.cpu().float() - gr).abs().max() / (gr.abs().max() + 1e-12))
+            assert e < 5e-2, (name, e)
+
+
+def test_configs0_yolox_tiny_416_single_image(golden, oracle, tmp_path):
+    """BASELINE configs[0]: Yolox.from_pretrained(<local checkpoint>, config) + Yolox.__call__
+    on one 416x416 image (r == 1), against the reference's own run (fixture) and the oracle."""
+    from PIL import Image
+
+    from yolox_amd.config import YoloxConfig
+    from yolox_amd.models import Yolox, YoloxModule
+    d = golden("processor_yolox_tiny_416.npz")
+    ckpt = tmp_path / "yolox_tiny.pth"
+    syn = YoloxModule.synthetic("yolox_tiny", seed=0, device="cuda")
+    torch.save({"model": {k: v.cpu() for k, v in syn.state_dict().items()}}, ckpt)
+    yolox = Yolox.from_pretrained(str(ckpt), config=YoloxConfig.get_named_config("yolox_tiny"), device="cuda")
+    im = Image.open(os.path.join(GOLDEN, "images", "000000000001.jpg")).convert("RGB").crop((0, 0, 416, 416))
+    for thr in (0.5, 0.3):
+        (det,) = yolox([im], threshold=thr)
+        assert det["labels"] == d[f"t{thr}.labels"].tolist()
+        np.testing.assert_allclose(np.array(det["bboxes"]).reshape(-1, 4), d[f"t{thr}.bboxes"], atol=1e-2, rtol=0)
+        np.testing.assert_allclose(det["scores"], d[f"t{thr}.scores"], atol=1e-4, rtol=0)
+    # the same device output through the oracle's NMS + the reference formatting: identical
+    out = yolox.module(yolox.processor([im]))
+    (rows,) = oracle.postprocess(out.cpu().numpy().copy(), 80, 0.5, 0.65)
+    assert yolox.processor.postprocess([im], out, threshold=0.5) == [
+        oracle.detections(rows, (416, 416), (416, 416))]

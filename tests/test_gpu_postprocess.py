@@ -144,3 +144,21 @@ def test_candidate_counts_past_one_sort_chunk(oracle, A):
     """Candidate counts just past one LDS chunk and past two merge levels, few classes."""
     pred = synthetic_pred(1, A, 3, 13)
     run_both(oracle, pred, 3, 0.0, 0.5)
+
+
+@pytest.mark.parametrize("budget", [1 << 16, 1 << 20])
+def test_mask_passes_match_one_pass(oracle, budget):
+    """The suppression matrix in many row passes (tiny mask budget: 64-row passes for the
+    first case) gives the oracle's keep lists bit for bit, both batched_nms branches."""
+    from yolox_amd import _native as N
+    lib = N.lib()
+    lib.yxh_set_nms_mask_budget(budget)
+    try:
+        pred = synthetic_pred(2, 6000, 80, 17)
+        pred[..., 4] = np.maximum(pred[..., 4], 0.5)
+        run_both(oracle, pred, 80, 0.05, 0.65)
+        run_both(oracle, pred, 80, 0.05, 0.65, agnostic=True)
+        pred = synthetic_pred(1, 3000, 2, 19, dense=True)
+        run_both(oracle, pred, 2, 0.0, 0.5)
+    finally:
+        lib.yxh_set_nms_mask_budget(0)

@@ -12,7 +12,7 @@ from conftest import REPO
 
 def header_symbols():
     text = open(os.path.join(REPO, "include", "yoloxhip.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(yxh_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|void|const char\*)\s+(yxh_\w+)\s*\(", text, re.M)))
 
 
 def test_library_exports_every_header_symbol():
@@ -55,6 +55,16 @@ def test_postprocess_workspace_is_monotone():
     b = lib.yxh_postprocess_workspace_bytes(32, 8400)
     c = lib.yxh_postprocess_workspace_bytes(32, 33600)
     assert 0 < a < b < c
+    # the suppression matrix is built in budgeted row passes: linear in A past the budget
+    # (was B * A * ceil(A/64) * 8 = 9.0 GB at 32 x 33600)
+    assert c < 700 << 20
+    assert lib.yxh_postprocess_workspace_bytes(1, 1 << 19) < 600 << 20
+    lib.yxh_set_nms_mask_budget(1 << 16)
+    try:
+        assert lib.yxh_postprocess_workspace_bytes(32, 8400) < b
+    finally:
+        lib.yxh_set_nms_mask_budget(0)
+    assert lib.yxh_postprocess_workspace_bytes(32, 8400) == b
 
 
 def test_library_targets_gfx950_only():

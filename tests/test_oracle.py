@@ -205,3 +205,25 @@ def test_oracle_letterbox_resize_paths(oracle):
     out = oracle.letterbox(c, (640, 640))
     np.testing.assert_array_equal(out[:, :480], c.transpose(2, 0, 1).astype(np.float32))
     assert (out[:, 480:] == 114).all()
+
+
+def test_processor_tiny_416_matches_reference(oracle, golden):
+    """BASELINE configs[0] (yolox_tiny 416, one image) pinned: the reference's Yolox.__call__ on
+    a 416x416 crop of its first test image (tests/golden/make_golden.py gen_processor_tiny) vs
+    the oracle chain (letterbox r == 1, fp32 forward, C NMS, processor formatting)."""
+    import hashlib
+
+    from PIL import Image
+    d = golden("processor_yolox_tiny_416.npz")
+    a = np.asarray(Image.open(os.path.join(GOLDEN, "images", "000000000001.jpg")).convert("RGB")
+                   .crop((0, 0, 416, 416)))
+    assert hashlib.sha256(a.tobytes()).hexdigest() == str(d["img.sha256"])
+    x = oracle.letterbox(a, (416, 416))[None]
+    assert hashlib.sha256(x.tobytes()).hexdigest() == str(d["tensor.sha256"])
+    out = oracle.forward_eval(weights("yolox_tiny"), oracle.ARCHS["yolox_tiny"], torch.from_numpy(x)).numpy()
+    for thr in (0.5, 0.3):
+        (rows,) = oracle.postprocess(out.copy(), 80, thr, 0.65)
+        det = oracle.detections(rows, a.shape[:2], (416, 416))
+        assert det["labels"] == d[f"t{thr}.labels"].tolist()
+        np.testing.assert_allclose(np.array(det["bboxes"]).reshape(-1, 4), d[f"t{thr}.bboxes"], atol=1e-2, rtol=0)
+        np.testing.assert_allclose(det["scores"], d[f"t{thr}.scores"], atol=1e-4, rtol=0)
