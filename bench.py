@@ -13,8 +13,8 @@ runs an independent replica -- inference has no exchange step, so there is no
 collective in the data path -- and value = all images / max
 rank time.
 
-roofline: the dominant kernel family is conv_igemm (every conv of the network);
-one "launch" = one forward's conv stack, timed with HIP events on the plan's stream
+roofline: the forward's conv stack (conv_ws / conv_ws1 / conv_pwf / conv_r3h /
+stem_rows / head_pred; every launch of one forward); one "launch" = one forward's conv stack, timed with HIP events on the plan's stream
 around every replay inside the timed region; achieved = algorithmic conv FLOPs per
 forward / mean forward duration, against the dense bf16 MFMA peak (2.5 PF).
 traffic: HBM bytes per forward from a rocprofv3 --pmc pass (profiles/traffic_*.json,
@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--model", default="yolox_s")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--chunk", type=int, default=0, help="images per pass of the op list (0 = whole batch)")
+    ap.add_argument("--par-chunks", action="store_true",
+                    help="with --chunk: chunks on arenas of their own, side by side in the captured graph")
     ap.add_argument("--size", type=int, default=640)
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32"],
                     help="compute dtype (default: bf16 for infer = configs[1]; fp32 for train = configs[2], "
@@ -420,7 +422,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     model = YoloxModule.synthetic(args.model, seed=0, device=dev, dtype=dtype)
     B, S = args.batch, args.size
-    plan = model.plan_for(B, S, S, N.NHWC, dtype, chunk=args.chunk or None)
+    plan = model.plan_for(B, S, S, N.NHWC, dtype, chunk=args.chunk or None, parallel_chunks=args.par_chunks)
     imgs = torch.from_numpy(synthetic_images(B, S, S, seed=1000 + rank)).to(dev)
     plan.static_input().copy_(imgs.to(dtype))
     from yolox_amd import engine
@@ -518,6 +520,8 @@ def main():
             "parallelism": f"replicas x{world} (no data-path collective)",
             "input": f"{args.dtype} NHWC resident in HBM",
             "chunk": plan.chunk,
+            "parallel_chunks": plan.parallel_chunks,
+            "graph": plan.graph_mode,
         },
         "roofline": {
             "kernel": "the forward conv stack (conv_ws / conv_ws1 / conv_r3h / conv_pwf / stem_rows / head_pred: every launch of one forward; HIP events on the plan stream around each graph replay)",

@@ -406,9 +406,16 @@ int yxh_graph_create(const yxh_op* ops, int32_t n, void* stream, void** graph_ex
  * deps[dep_off[i] .. dep_off[i+1]) (indices < i); cross-lane dependencies become graph
  * edges, same-lane order is stream order.  Lane 0 forks the others at the start and
  * joins them at the end.  Used to overlap the three head levels with each other and
- * with the PAFPN bottom-up path (yolo_head.py:140-211 runs the levels independently). */
+ * with the PAFPN bottom-up path (yolo_head.py:140-211 runs the levels independently).
+ * At most 4 lanes (EINVAL above: more capture streams segfaulted in the join). */
 int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, const int32_t* dep_off,
                            const int32_t* deps, int32_t nlanes, void* stream, void** graph_exec);
+/* yxh_graph_create_dag: the op list as its dataflow DAG -- op i is one graph node (the
+ * op captured alone) whose predecessors are the ops deps[dep_off[i] .. dep_off[i+1])
+ * (indices < i).  No lanes: every independent pair of ops may run concurrently (head
+ * levels, batch chunks planned on arenas of their own). */
+int yxh_graph_create_dag(const yxh_op* ops, int32_t n, const int32_t* dep_off, const int32_t* deps,
+                         void* stream, void** graph_exec);
 int yxh_graph_launch(void* graph_exec, void* stream);
 int yxh_graph_destroy(void* graph_exec);
 

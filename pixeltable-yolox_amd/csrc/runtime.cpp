@@ -265,9 +265,73 @@ int yxh_graph_create(const yxh_op* ops, int32_t n, void* stream, void** graph_ex
     return YXH_OK;
 }
 
+// One graph node per op, wired by the op list's own dependency edges: each op is captured
+// ALONE on one stream into a small graph (a conv is one kernel, post-processing several)
+// and added to the parent as a child-graph node whose predecessors are the nodes of the ops
+// it depends on.  No multi-stream capture is involved (yxh_graph_create_lanes with more
+// than four capture streams ended in a segfault inside the lane join / hipStreamEndCapture
+// after every op had been captured), and the parent holds exactly the dataflow DAG: every
+// pair of independent ops -- the head levels, or batch chunks with arenas of their own --
+// may run concurrently, with no lane assignment by the caller.
+int yxh_graph_create_dag(const yxh_op* ops, int32_t n, const int32_t* dep_off, const int32_t* deps, void* stream,
+                         void** graph_exec) {
+    YXH_CHECK_ARG(graph_exec && (ops || n == 0) && dep_off, "null argument");
+    YXH_CHECK_ARG(dep_off[0] == 0, "dep_off[0] must be 0");
+    for (int i = 0; i < n; ++i) {
+        YXH_CHECK_ARG(dep_off[i + 1] >= dep_off[i], "dep_off not monotone at %d", i);
+        for (int k = dep_off[i]; k < dep_off[i + 1]; ++k)
+            YXH_CHECK_ARG(deps && deps[k] >= 0 && deps[k] < i, "op %d dependency %d", i, deps ? deps[k] : -1);
+    }
+    (void)stream;
+    hipStream_t cap = nullptr;
+    hipGraph_t parent = nullptr;
+    int rc = check_hip(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking), "capture stream");
+    if (!rc) rc = check_hip(hipGraphCreate(&parent, 0), "graph create");
+    std::vector<hipGraphNode_t> node(n, nullptr);
+    std::vector<hipGraphNode_t> pred;
+    int orc = YXH_OK;
+    for (int i = 0; i < n && !rc && !orc; ++i) {
+        rc = check_hip(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal), "begin capture");
+        if (rc) break;
+        orc = run_op(ops[i], cap);
+        hipGraph_t g = nullptr;
+        const int erc = check_hip(hipStreamEndCapture(cap, &g), "end capture");
+        if (orc) {
+            char tmp[512];
+            snprintf(tmp, sizeof(tmp), "op %d: %s", i, g_err);
+            set_error("%s", tmp);
+        } else {
+            rc = erc;
+        }
+        if (!rc && !orc) {
+            pred.clear();
+            for (int k = dep_off[i]; k < dep_off[i + 1]; ++k) {
+                hipGraphNode_t d = node[deps[k]];
+                bool dup = false;
+                for (auto q : pred) dup |= q == d;
+                if (!dup) pred.push_back(d);
+            }
+            rc = check_hip(hipGraphAddChildGraphNode(&node[i], parent, pred.empty() ? nullptr : pred.data(),
+                                                     pred.size(), g),
+                           "add op node");
+        }
+        if (g) (void)hipGraphDestroy(g);
+    }
+    hipGraphExec_t ge = nullptr;
+    if (!rc && !orc) rc = check_hip(hipGraphInstantiate(&ge, parent, nullptr, nullptr, 0), "instantiate");
+    if (parent) (void)hipGraphDestroy(parent);
+    if (cap) (void)hipStreamDestroy(cap);
+    if (orc) return orc;
+    if (rc) return rc;
+    *graph_exec = (void*)ge;
+    return YXH_OK;
+}
+
 int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, const int32_t* dep_off,
                            const int32_t* deps, int32_t nlanes, void* stream, void** graph_exec) {
-    constexpr int kMaxLanes = 8;
+    // proven limit: 4 capture streams (7 segfaulted in the join / end of capture, DESIGN.md
+    // §11); more concurrency goes through yxh_graph_create_dag
+    constexpr int kMaxLanes = 4;
     YXH_CHECK_ARG(graph_exec && (ops || n == 0) && lanes && dep_off, "null argument");
     YXH_CHECK_ARG(nlanes >= 1 && nlanes <= kMaxLanes, "nlanes %d", nlanes);
     YXH_CHECK_ARG(dep_off[0] == 0, "dep_off[0] must be 0");

@@ -184,6 +184,8 @@ def lib():
             "yxh_graph_create": ([C.POINTER(Op), i32, vp, C.POINTER(vp)], C.c_int),
             "yxh_graph_create_lanes": ([C.POINTER(Op), i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32,
                                         vp, C.POINTER(vp)], C.c_int),
+            "yxh_graph_create_dag": ([C.POINTER(Op), i32, C.POINTER(i32), C.POINTER(i32), vp, C.POINTER(vp)],
+                                     C.c_int),
             "yxh_graph_launch": ([vp, vp], C.c_int),
             "yxh_graph_destroy": ([vp], C.c_int),
         }
@@ -201,7 +203,7 @@ def lib():
 
 EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d", "yxh_head_pred",
             "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_postprocess_workspace_bytes", "yxh_set_nms_mask_budget",
-            "yxh_postprocess", "yxh_postprocess_ev", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes",
+            "yxh_postprocess", "yxh_postprocess_ev", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes", "yxh_graph_create_dag",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
             "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_spp_bwd",
             "yxh_upsample_bwd", "yxh_head_decode_train", "yxh_yolox_loss_bwd", "yxh_opt_chunk_elems",

@@ -337,54 +337,72 @@ def _tune_key(d) -> tuple:
             d.flags)
 
 
-def op_dependencies(ops) -> list:
-    """Per op, the earlier ops it must wait for, from the buffers it reads and writes
-    (read-after-write, write-after-write, write-after-read).  Arena buffers never alias
-    (bump allocation); the input image and the [B, A, 5+C] output rows (disjoint anchor
-    ranges per level, written once) are not tracked."""
+def op_buffers(r: OpRec) -> tuple:
+    """(buffers read, buffers written) by one op; the input image and the [B, A, 5+C]
+    output rows (disjoint anchor ranges per level, written once) are not tracked."""
+    a = r.args
+    if r.kind == N.OP_SPP:
+        return [a["buf"]], [a["buf"]]
+    if r.kind in (N.OP_FOCUS, N.OP_STEM):
+        return [], [a["dst"].buf]
+    if r.kind == N.OP_HEAD:
+        return [a["reg"].buf, a["cls"].buf], []
+    reads = [v.buf for v in a["srcs"]]
+    if a.get("residual") is not None:
+        reads.append(a["residual"].buf)
+    return reads, ([a["out"].buf] if a.get("out") is not None else [])
+
+
+def dependencies_rw(rw: list) -> list:
+    """Per op, the earlier ops it must wait for, from (read keys, write keys) per op:
+    read-after-write, write-after-write and write-after-read edges."""
     last_w: dict = {}
     readers: dict = {}
     deps = []
-    for i, r in enumerate(ops):
-        a = r.args
-        if r.kind == N.OP_SPP:
-            reads, writes = [a["buf"]], [a["buf"]]
-        elif r.kind in (N.OP_FOCUS, N.OP_STEM):
-            reads, writes = [], [a["dst"].buf]
-        elif r.kind == N.OP_HEAD:
-            reads, writes = [a["reg"].buf, a["cls"].buf], []
-        else:
-            reads = [v.buf for v in a["srcs"]]
-            if a.get("residual") is not None:
-                reads.append(a["residual"].buf)
-            writes = [a["out"].buf] if a.get("out") is not None else []
+    for i, (reads, writes) in enumerate(rw):
         d = set()
-        for b in reads + writes:
-            if id(b) in last_w:
-                d.add(last_w[id(b)])
+        for b in list(reads) + list(writes):
+            if b in last_w:
+                d.add(last_w[b])
         for b in writes:
-            d.update(readers.get(id(b), ()))
+            d.update(readers.get(b, ()))
         d.discard(i)
         for b in reads:
-            readers.setdefault(id(b), []).append(i)
+            readers.setdefault(b, []).append(i)
         for b in writes:
-            last_w[id(b)] = i
-            readers[id(b)] = []
+            last_w[b] = i
+            readers[b] = []
         deps.append(sorted(d))
     return deps
+
+
+def op_dependencies(ops) -> list:
+    """Per op, the earlier ops it must wait for, from the buffers it reads and writes
+    (read-after-write, write-after-write, write-after-read).  Arena buffers never alias
+    (bump allocation)."""
+    rw = []
+    for r in ops:
+        reads, writes = op_buffers(r)
+        rw.append(([id(b) for b in reads], [id(b) for b in writes]))
+    return dependencies_rw(rw)
 
 
 class Plan:
     """A finalised op list with its arenas.  ``run(x)`` executes one forward pass.
 
     ``chunk``: the op list is planned for ``chunk`` images and executed batch/chunk
-    times back to back on the same activation arena (input and output pointers
-    advance per chunk), so each layer's output is still in the MI355X Infinity Cache
-    when the next layer reads it.  The result is identical to an unchunked plan."""
+    times (input and output pointers advance per chunk).  By default the chunks share
+    one activation arena and run back to back (each layer's output is still in the
+    MI355X Infinity Cache when the next layer reads it); with ``parallel_chunks`` every
+    chunk gets an arena of its own, so in the captured dataflow graph the chunks are
+    independent chains that the device runs side by side (one chunk's small layers and
+    kernel boundaries overlap the other's work).  The result is identical to an
+    unchunked plan either way."""
 
     def __init__(self, model, batch: int, height: int, width: int, dtype: torch.dtype, device,
                  input_layout: int = N.NCHW, input_dtype: torch.dtype = torch.float32, train: bool = False,
-                 fuse_stem: bool = True, chunk: Optional[int] = None, fuse_bottleneck: bool = _FUSE_BOTTLENECK):
+                 fuse_stem: bool = True, chunk: Optional[int] = None, fuse_bottleneck: bool = _FUSE_BOTTLENECK,
+                 parallel_chunks: bool = False):
         if height % 32 or width % 32:
             raise ValueError("input size must be multiples of 32")
         chunk = chunk or batch
@@ -392,6 +410,7 @@ class Plan:
             raise ValueError(f"chunk {chunk} must divide batch {batch}")
         self.lib = N.lib()
         self.chunk, self.nchunks = chunk, batch // chunk
+        self.parallel_chunks = bool(parallel_chunks) and self.nchunks > 1
         self.batch, self.height, self.width = batch, height, width
         self.device = torch.device(device)
         self.input_layout = input_layout
@@ -410,14 +429,18 @@ class Plan:
         self.nlanes = 1 + max((r.lane for r in ctx.ops), default=0)
         self._deps = op_dependencies(ctx.ops)
         self.use_lanes = os.environ.get("YOLOX_AMD_LANES", "1") != "0"
+        # captured graph form: "dag" (one node per op, dataflow edges; default), "lanes"
+        # (multi-stream capture, head levels on lanes), "linear" (one stream)
+        self.graph_mode = os.environ.get("YOLOX_AMD_GRAPH", "dag")
         self.flops = ctx.flops * self.nchunks
         # ------------------------------------------------ arenas
         off = 0
         for b in ctx.buffers:
             b.offset = off
             off += _align(chunk * b.nelem_image * b.esize)
-        self.act_bytes = off
-        self.arena = torch.empty(max(off, 1), dtype=torch.uint8, device=self.device)
+        self.act_bytes = off  # one chunk's activations
+        narenas = self.nchunks if self.parallel_chunks else 1
+        self.arena = torch.empty(max(off * narenas, 1), dtype=torch.uint8, device=self.device)
         woff = boff = 0
         for s in ctx.weights:
             s.w_off = woff
@@ -443,8 +466,12 @@ class Plan:
         self._encode_ops()
 
     # -------------------------------------------------------------- encoding
-    def _ptr(self, v: View) -> int:
-        return self.arena.data_ptr() + v.buf.offset + v.coff * v.buf.esize
+    def _ptr(self, v: View, c: int = 0) -> int:
+        return self._arena_base(c) + v.buf.offset + v.coff * v.buf.esize
+
+    def _arena_base(self, c: int) -> int:
+        """Activation arena of chunk c (all chunks share one unless parallel_chunks)."""
+        return self.arena.data_ptr() + (c * self.act_bytes if self.parallel_chunks else 0)
 
     def _encode_ops(self) -> None:
         for c in range(self.nchunks):
@@ -466,7 +493,7 @@ class Plan:
                 f.img_dtype = N.DTYPE_CODE[self.input_dtype]
                 f.batch, f.h, f.w = B, a["h"], a["w"]
                 f.dst_dtype = ctx.dcode
-                f.dst = self._ptr(a["dst"])
+                f.dst = self._ptr(a["dst"], c)
                 f.img = None
                 self._input_index = i
             elif rec.kind == N.OP_STEM:
@@ -478,7 +505,7 @@ class Plan:
                 t.weight = self.warena.data_ptr() + a["spec"].w_off
                 t.bias = self.barena.data_ptr() + a["spec"].b_off
                 v = a["dst"]
-                t.dst = self._ptr(v)
+                t.dst = self._ptr(v, c)
                 t.dst_cstride, t.dst_bstride = v.buf.c, v.buf.nelem_image
                 t.img = None
                 self._input_index = i
@@ -487,7 +514,7 @@ class Plan:
                 hd.dtype, hd.batch, hd.h, hd.w = ctx.dcode, B, a["h"], a["w"]
                 hd.cin, hd.num_classes = a["cin"], a["num_classes"]
                 for dst, v in ((hd.reg, a["reg"]), (hd.cls, a["cls"])):
-                    dst.ptr = self._ptr(v)
+                    dst.ptr = self._ptr(v, c)
                     dst.channels, dst.cstride, dst.bstride = v.ch, v.buf.c, v.buf.nelem_image
                     dst.h, dst.w, dst.upsample = v.buf.h, v.buf.w, 0
                 hd.w_reg = self.warena.data_ptr() + a["spec_ro"].w_off
@@ -501,7 +528,7 @@ class Plan:
             elif rec.kind == N.OP_SPP:
                 s = op.u.spp
                 buf: Buffer = a["buf"]
-                s.buf = self.arena.data_ptr() + buf.offset
+                s.buf = self._arena_base(c) + buf.offset
                 s.dtype, s.batch, s.h, s.w, s.c = ctx.dcode, B, buf.h, buf.w, a["c"]
                 s.cstride, s.bstride = buf.c, buf.nelem_image
             else:
@@ -513,7 +540,7 @@ class Plan:
                 d.nsrc = len(a["srcs"])
                 for j, v in enumerate(a["srcs"]):
                     s = d.src[j]
-                    s.ptr = self._ptr(v)
+                    s.ptr = self._ptr(v, c)
                     s.channels, s.cstride, s.bstride = v.ch, v.buf.c, v.buf.nelem_image
                     s.h, s.w, s.upsample = v.buf.h, v.buf.w, v.up
                 spec: WeightSpec = a["spec"]
@@ -526,7 +553,7 @@ class Plan:
                     d.pre_bias = self.barena.data_ptr() + pre.b_off
                 res = a["residual"]
                 if res is not None:
-                    d.residual = self._ptr(res)
+                    d.residual = self._ptr(res, c)
                     d.res_cstride, d.res_bstride = res.buf.c, res.buf.nelem_image
                 d.act = a["act"]
                 if a["dst_f32"]:
@@ -538,7 +565,7 @@ class Plan:
                     d.decode_stride, d.decode_coff = a["decode_stride"], a["decode_coff"]
                 else:
                     v = a["out"]
-                    d.dst = self._ptr(v)
+                    d.dst = self._ptr(v, c)
                     d.dst_dtype = ctx.dcode
                     d.dst_cstride, d.dst_bstride = v.buf.c, v.buf.nelem_image
 
@@ -653,7 +680,11 @@ class Plan:
             self._graph = None
         g = C.c_void_p()
         torch.cuda.synchronize(self.device)
-        if self.use_lanes and self.nlanes > 1:
+        if self.graph_mode == "dag":
+            off, deps = self._dag_arrays()
+            N.check(self.lib.yxh_graph_create_dag(self._ops, len(self._ops), off, deps, N.stream_ptr(self.device),
+                                                  C.byref(g)), "graph capture (dag)")
+        elif self.graph_mode == "lanes" and self.use_lanes and self.nlanes > 1 and not self.parallel_chunks:
             lanes, off, deps = self._lane_arrays()
             N.check(self.lib.yxh_graph_create_lanes(self._ops, len(self._ops), lanes, off, deps, self.nlanes,
                                                     N.stream_ptr(self.device), C.byref(g)), "graph capture (lanes)")
@@ -661,6 +692,25 @@ class Plan:
             N.check(self.lib.yxh_graph_create(self._ops, len(self._ops), N.stream_ptr(self.device), C.byref(g)),
                     "graph capture")
         self._graph = g
+
+    def _dag_arrays(self):
+        """(dep_off, deps) of the dataflow DAG over all chunks: buffers are keyed by arena
+        (per chunk with parallel_chunks, else shared), so chunks that share an arena are
+        ordered by their write-after-read / write-after-write edges and independent
+        chunks are not ordered at all."""
+        rw = []
+        for c in range(self.nchunks):
+            arena = c if self.parallel_chunks else 0
+            for r in self.ctx.ops:
+                reads, writes = op_buffers(r)
+                rw.append(([(arena, id(b)) for b in reads], [(arena, id(b)) for b in writes]))
+        deps_all = dependencies_rw(rw)
+        off, deps = [0], []
+        for d in deps_all:
+            deps.extend(d)
+            off.append(len(deps))
+        arr = lambda v: (C.c_int32 * max(1, len(v)))(*v)  # noqa: E731
+        return arr(off), arr(deps)
 
     def _lane_arrays(self):
         """(lanes, dep_off, deps) over all chunks.  Chunk c reuses chunk c-1's arena: its

@@ -48,18 +48,20 @@ class YoloxModule(nn.Module):
 
     def plan_for(self, batch: int, height: int, width: int, input_layout: int = N.NCHW,
                  input_dtype: torch.dtype = torch.float32, dtype: Optional[torch.dtype] = None,
-                 chunk: Optional[int] = None):
+                 chunk: Optional[int] = None, parallel_chunks: bool = False):
         """The (cached) HIP execution plan for this input geometry (``chunk``: images
-        per pass of the op list, see engine.Plan)."""
+        per pass of the op list; ``parallel_chunks``: chunks on arenas of their own, run
+        side by side in the captured graph -- see engine.Plan)."""
         from ..engine import Plan
 
         dtype = dtype or self.compute_dtype
-        key = (batch, height, width, input_layout, input_dtype, dtype, str(self.device), chunk)
+        key = (batch, height, width, input_layout, input_dtype, dtype, str(self.device), chunk, parallel_chunks)
         plan = self._plans.get(key)
         if plan is None:
             if self.device.type != "cuda":
                 raise RuntimeError("YoloxModule runs on a ROCm device only; call .to('cuda') first")
-            plan = Plan(self, batch, height, width, dtype, self.device, input_layout, input_dtype, chunk=chunk)
+            plan = Plan(self, batch, height, width, dtype, self.device, input_layout, input_dtype, chunk=chunk,
+                        parallel_chunks=parallel_chunks)
             self._plans[key] = plan
         return plan
 

@@ -38,3 +38,41 @@ def test_head_levels_plan_on_their_own_lanes():
     for k in (1, 2, 3):  # a level's first op waits only for the neck op producing its input
         first = lanes.index(k)
         assert [lanes[j] for j in deps[first]] == [0]
+
+
+def test_dag_dependencies_per_chunk_arena():
+    """The DAG of a chunked plan: with a shared arena chunk 1's writers wait for chunk 0's
+    readers of the same buffers; with arenas of their own the chunks are not ordered."""
+    from yolox_amd.engine import dependencies_rw, op_buffers
+    m = named_config("yolox_s").get_model()
+    ctx = PlanCtx(2, torch.bfloat16, torch.device("cpu"))
+    feats = m.backbone.plan(ctx, ctx.image(128, 128))
+    m.head.plan(ctx, feats, OutBuffer(sum(f.lh * f.lw for f in feats), 85))
+    n = len(ctx.ops)
+    for shared in (True, False):
+        rw = []
+        for c in range(2):
+            key = 0 if shared else c
+            for r in ctx.ops:
+                reads, writes = op_buffers(r)
+                rw.append(([(key, id(b)) for b in reads], [(key, id(b)) for b in writes]))
+        deps = dependencies_rw(rw)
+        cross = [(j, i) for i in range(n, 2 * n) for j in deps[i] if j < n]
+        assert bool(cross) == shared
+        assert deps[n:] == [[j + n for j in d] for d in deps[:n]] or shared
+
+
+def test_lane_and_dag_capture_argument_checks():
+    """yxh_graph_create_lanes refuses more than 4 capture streams (7 segfaulted in the join,
+    DESIGN.md §11); both graph builders reject forward/self dependencies -- all before any
+    HIP call, so this runs without a device."""
+    import ctypes as C
+    lib = N.lib()
+    ops = (N.Op * 2)()
+    g = C.c_void_p()
+    i32 = lambda v: (C.c_int32 * len(v))(*v)  # noqa: E731
+    assert lib.yxh_graph_create_lanes(ops, 2, i32([0, 4]), i32([0, 0, 1]), i32([0]), 5, None, C.byref(g)) == N.EINVAL
+    assert b"nlanes" in lib.yxh_last_error()
+    assert lib.yxh_graph_create_dag(ops, 2, i32([0, 1, 1]), i32([0]), None, C.byref(g)) == N.EINVAL
+    assert b"dependency" in lib.yxh_last_error()
+    assert lib.yxh_graph_create_dag(ops, 2, i32([1, 1, 1]), i32([0]), None, C.byref(g)) == N.EINVAL

@@ -172,22 +172,26 @@ def test_chunked_plan_matches_whole_batch():
         Plan(m, 4, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8, chunk=3)
 
 
-def test_lane_graph_matches_single_stream_graph():
-    """The head levels run as separate hipGraph branches (lanes) beside the PAFPN
-    bottom-up path; the result equals the single-stream graph bit for bit (chunked
-    plan: chunk c+1 waits for every lane of chunk c)."""
+def test_graph_forms_match_single_stream_graph():
+    """The captured forms of one plan -- the dataflow DAG (one node per op; head levels
+    concurrent), lanes (head levels on capture streams) and one stream -- give the same
+    output bit for bit, chunked with a shared arena and with parallel chunks (arenas of
+    their own, the chunks side by side), replayed twice each."""
     from yolox_amd import _native as N
     from yolox_amd.engine import Plan
     from yolox_amd.weights import synthetic_images
     m = model("yolox_s", torch.bfloat16)
     x = torch.from_numpy(synthetic_images(4, 160, 160, seed=4)).cuda()
     outs = []
-    for lanes in (True, False):
-        p = Plan(m, 4, 160, 160, torch.bfloat16, "cuda", N.NHWC, torch.uint8, chunk=2)
-        assert p.nlanes == 4
-        p.use_lanes = lanes
-        p.static_input().copy_(x)
-        outs.append(p.replay().clone())
-        outs.append(p.replay().clone())
+    for par in (False, True):
+        for mode in ("dag", "lanes", "linear"):
+            p = Plan(m, 4, 160, 160, torch.bfloat16, "cuda", N.NHWC, torch.uint8, chunk=2, parallel_chunks=par)
+            assert p.nlanes == 4 and p.parallel_chunks == par
+            p.graph_mode = mode
+            p.static_input().copy_(x)
+            outs.append(p.replay().clone())
+            outs.append(p.replay().clone())
+            if par:
+                assert torch.equal(p.run(x).clone(), outs[0])  # eager: chunks in order, one stream
     torch.cuda.synchronize()
-    assert all(torch.equal(o, outs[2]) for o in outs)
+    assert all(torch.equal(o, outs[0]) for o in outs)
