@@ -462,6 +462,7 @@ class Plan:
         self._graph = None
         self._graph_ptrs = None
         self._param_sig = None
+        self._packed_epoch = -1
         self._model = model
         self._encode_ops()
 
@@ -575,9 +576,13 @@ class Plan:
         m = self._model
         return tuple((t.data_ptr(), t._version) for t in list(m.parameters()) + list(m.buffers()))
 
+    def _epoch(self) -> int:
+        return getattr(self._model, "_weights_epoch", 0)
+
     def pack_weights(self, force: bool = False) -> None:
         sig = self._signature()
         if not force and sig == self._param_sig:
+            self._packed_epoch = self._epoch()
             return
         stream = N.stream_ptr(self.device)
         dt = self.ctx.dcode
@@ -614,6 +619,7 @@ class Plan:
         torch.cuda.current_stream(self.device).synchronize()  # `keep` tensors die after this
         del keep
         self._param_sig = sig
+        self._packed_epoch = self._epoch()
 
     # -------------------------------------------------------------- execution
     def _bind_input(self, x: torch.Tensor) -> torch.Tensor:
@@ -733,10 +739,14 @@ class Plan:
         return arr(lanes), arr(off), arr(deps)
 
     def replay(self) -> torch.Tensor:
-        """Launch the captured forward; parameters changed since the capture (optimizer or
-        EMA step, load_state_dict) are re-folded into the same weight arena first, which
-        the graph reads in place."""
-        self.pack_weights()
+        """Launch the captured forward.  Parameters changed since the last packing are
+        re-folded into the same weight arena first (the graph reads it in place); on this
+        serving path the check is the module's weights epoch (one integer compare), which
+        load_state_dict, FusedStep.step and YoloxModule.weights_changed() advance --
+        in-place edits made any other way need weights_changed() before the next replay.
+        ``run()`` (the eager API path) compares every parameter's version instead."""
+        if self._packed_epoch != self._epoch():
+            self.pack_weights()
         if self._graph is None:
             self.capture()
         N.check(self.lib.yxh_graph_launch(self._graph, N.stream_ptr(self.device)), "graph replay")

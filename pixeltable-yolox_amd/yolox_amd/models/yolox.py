@@ -36,6 +36,17 @@ class YoloxModule(nn.Module):
         self.backbone = backbone if backbone is not None else YoloPafpn()
         self.head = head if head is not None else YoloxHead(80)
         self._plans: dict = {}
+        self._weights_epoch = 0  # advanced on every weight change the captured plans must see
+
+    def weights_changed(self) -> None:
+        """Tell captured plans (engine.Plan.replay) that parameters or BN statistics were
+        edited in place; load_state_dict and FusedStep.step call this themselves."""
+        self._weights_epoch += 1
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        r = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self.weights_changed()
+        return r
 
     # ---------------------------------------------------------------- execution
     @property

@@ -78,6 +78,7 @@ class FusedStep:
                 else:
                     self.ema_only.append((e, s))
         self._key = None
+        self.model = model.module if hasattr(model, "module") else model
         self.chunk = int(self.lib.yxh_opt_chunk_elems())
         self.found_inf = torch.zeros(1, dtype=torch.float32, device=self.device)
 
@@ -148,8 +149,12 @@ class FusedStep:
             for p in self.params:
                 self.opt.state[p]["momentum_buffer"] = self.bufs[id(p)]
             self.first = False
-        # in-place writes behind torch's back: bump versions so the eval plans repack
+        # in-place writes behind torch's back: bump versions (eager plans) and the modules'
+        # weights epochs (captured plans) so eval plans repack
         torch.autograd.graph.increment_version(self.params)
+        for m in (self.model, getattr(self.ema, "ema", None)):
+            if hasattr(m, "weights_changed"):
+                m.weights_changed()
         if self.ema is not None:
             torch.autograd.graph.increment_version(list(self.ema.ema.parameters()))
 

@@ -596,6 +596,8 @@ def train_forward(model, images: torch.Tensor, targets: torch.Tensor, dtype: Opt
         g = TrainGraph(model, dtype)
         model._train_graph = g
     out = g.forward(images, targets)
+    if hasattr(model, "weights_changed"):  # BN running statistics were updated in place
+        model.weights_changed()
     anchor = torch.zeros((), device=model.device, requires_grad=True)
     out["total_loss"] = _LossFn.apply(anchor, out["total_loss"], g)
     return out

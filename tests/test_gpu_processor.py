@@ -173,3 +173,22 @@ def test_box_map_parity_vs_reference_detections(golden, api):
     prec = ev["precision"][:, :, :, 0, 2]
     ap = prec[prec > -1].mean()
     assert ap == pytest.approx(1.0) and ev["stats"][1] == pytest.approx(1.0), (ap, ev["stats"])
+
+
+def test_replay_sees_in_place_edit_after_weights_changed():
+    """Plan.replay checks the module's weights epoch (no per-replay parameter walk):
+    an in-place edit announced by weights_changed() is folded before the next replay."""
+    from yolox_amd import _native as N
+    from yolox_amd.models import YoloxModule
+    m = YoloxModule.synthetic("yolox_s", seed=0, device="cuda")
+    x = torch.from_numpy(np.random.default_rng(1).integers(0, 256, (2, 128, 128, 3), dtype=np.uint8)).cuda()
+    plan = m.plan_for(2, 128, 128, N.NHWC, torch.uint8)
+    plan.static_input().copy_(x)
+    plan.capture()
+    first = plan.replay().clone()
+    with torch.no_grad():
+        m.head.cls_preds[0].bias.add_(0.5)
+    m.weights_changed()
+    again = plan.replay().clone()
+    assert not torch.equal(first, again)
+    assert torch.equal(again, m.forward_nhwc(x))
