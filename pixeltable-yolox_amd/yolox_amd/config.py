@@ -4,12 +4,17 @@ Mirrors the reference's ``yolox.config.YoloxConfig`` API (config.py:17-157,
 412-469): the same field names and defaults, ``get_named_config`` accepting ``-``
 or ``_``, ``update`` with type coercion, ``validate`` and ``get_model``.  Named
 configs are module-level singletons, as in the reference (quirk: they cache the
-model they build, config.py:168-172, 466-469).  Data-loader / evaluator factories
-(CPU data pipeline, COCO files) are out of scope.
+model they build, config.py:168-172, 466-469).  The training-side factories the
+trainer calls are here too: ``get_optimizer`` (:307-333), ``get_lr_scheduler``
+(:335-348), ``random_resize`` (:275-294, rank-0 draw broadcast to every rank),
+``preprocess`` (:296-305, bilinear multiscale) and ``get_data_loader`` -- the latter
+over a synthetic COCO-shaped dataset (no datasets offline; COCO files and the
+Mosaic/MixUp CPU pipeline are out of scope).
 """
 from __future__ import annotations
 
 import ast
+import random
 from dataclasses import dataclass, field
 from typing import Any, Literal, Optional
 
@@ -114,6 +119,75 @@ class YoloxConfig:
         self.model.head.initialize_biases(1e-2)
         self.model.train()
         return self.model
+
+    # ------------------------------------------------------------ training factories
+    def get_optimizer(self, batch_size: int):
+        """config.py:307-333: SGD nesterov, BN weights without decay, conv weights with
+        ``weight_decay``, biases; lr = warmup_lr while warming up (the scheduler sets it
+        from the first iteration on)."""
+        if getattr(self, "optimizer", None) is None:
+            from .trainer import get_optimizer
+            lr = self.warmup_lr if self.warmup_epochs > 0 else self.basic_lr_per_img * batch_size
+            self.optimizer = get_optimizer(self.model, lr, self.momentum, self.weight_decay)
+        return self.optimizer
+
+    def get_lr_scheduler(self, lr: float, iters_per_epoch: int):
+        """config.py:335-348."""
+        from .trainer import LRScheduler
+        return LRScheduler(self.scheduler, lr, iters_per_epoch, self.max_epoch, warmup_epochs=self.warmup_epochs,
+                           warmup_lr_start=self.warmup_lr, no_aug_epochs=self.no_aug_epochs,
+                           min_lr_ratio=self.min_lr_ratio)
+
+    def get_data_loader(self, batch_size: int, is_distributed: bool, no_aug: bool = False, cache_img=None,
+                        dataset_size: int = 118287):
+        """config.py:214-273 with the synthetic dataset: the per-rank batch is
+        batch_size // world (:249-250) and every rank reads its rank-strided slice of one
+        seeded shuffled index stream (InfiniteSampler, samplers.py:28-82)."""
+        from .trainer import InfiniteSampler, SyntheticBatches, SyntheticCocoDataset
+        from .launch import get_world_size
+        if is_distributed:
+            batch_size = batch_size // get_world_size()
+        ds = SyntheticCocoDataset(dataset_size, self.input_size, seed=self.seed if self.seed else 0)
+        sampler = InfiniteSampler(len(ds), seed=self.seed if self.seed else 0)
+        return SyntheticBatches(ds, sampler, batch_size)
+
+    def random_resize(self, data_loader, epoch: int, rank: int, is_distributed: bool):
+        """config.py:275-294: rank 0 draws the next multiscale input size (multiples of 32
+        around input_size) and broadcasts it; every rank returns the same (h, w)."""
+        import torch
+        import torch.distributed as dist
+        dev = "cuda" if is_distributed and dist.get_backend() == "nccl" else "cpu"
+        tensor = torch.zeros(2, dtype=torch.int64, device=dev)
+        if rank == 0:
+            size_factor = self.input_size[1] * 1.0 / self.input_size[0]
+            if self.random_size is None:
+                min_size = int(self.input_size[0] / 32) - self.multiscale_range
+                max_size = int(self.input_size[0] / 32) + self.multiscale_range
+                self.random_size = (min_size, max_size)
+            size = random.randint(*self.random_size)
+            size = (int(32 * size), 32 * int(size * size_factor))
+            tensor[0] = size[0]
+            tensor[1] = size[1]
+        if is_distributed:
+            dist.barrier()
+            dist.broadcast(tensor, 0)
+        return (int(tensor[0].item()), int(tensor[1].item()))
+
+    def preprocess(self, inputs, targets, tsize):
+        """config.py:296-305: bilinear resize of the batch to ``tsize`` (align_corners
+        False) with the box columns scaled to match."""
+        import torch.nn.functional as F
+        scale_y = tsize[0] / self.input_size[0]
+        scale_x = tsize[1] / self.input_size[1]
+        if scale_x != 1 or scale_y != 1:
+            inputs = F.interpolate(inputs, size=tsize, mode="bilinear", align_corners=False)
+            targets[..., 1::2] = targets[..., 1::2] * scale_x
+            targets[..., 2::2] = targets[..., 2::2] * scale_y
+        return inputs, targets
+
+    def get_trainer(self, args):
+        from .trainer import Trainer
+        return Trainer(self, args)
 
 
 _PRESETS: dict[str, dict[str, Any]] = {

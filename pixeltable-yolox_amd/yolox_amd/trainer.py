@@ -94,3 +94,234 @@ def train_one_iter(model: nn.Module, optimizer, images: torch.Tensor, targets: t
     if ema is not None:
         ema.update(model)
     return outputs
+
+
+# ------------------------------------------------------------------ LR schedule
+def yolox_warm_cos_lr(lr, min_lr_ratio, total_iters, warmup_total_iters, warmup_lr_start, no_aug_iter, iters):
+    """utils/lr_scheduler.py:119-146 (quadratic warm-up, cosine, flat min_lr for the
+    no-aug epochs)."""
+    min_lr = lr * min_lr_ratio
+    if iters <= warmup_total_iters:
+        return (lr - warmup_lr_start) * pow(iters / float(warmup_total_iters), 2) + warmup_lr_start
+    if iters >= total_iters - no_aug_iter:
+        return min_lr
+    return min_lr + 0.5 * (lr - min_lr) * (1.0 + math.cos(
+        math.pi * (iters - warmup_total_iters) / (total_iters - warmup_total_iters - no_aug_iter)))
+
+
+def cos_lr(lr, total_iters, iters):
+    return lr * 0.5 * (1.0 + math.cos(math.pi * iters / total_iters))
+
+
+def warm_cos_lr(lr, total_iters, warmup_total_iters, warmup_lr_start, iters):
+    if iters <= warmup_total_iters:
+        return (lr - warmup_lr_start) * iters / float(warmup_total_iters) + warmup_lr_start
+    return 0.5 * lr * (1.0 + math.cos(math.pi * (iters - warmup_total_iters) / (total_iters - warmup_total_iters)))
+
+
+class LRScheduler:
+    """utils/lr_scheduler.py:7-117 for the schedules a YoloxConfig names (cos, warmcos,
+    yoloxwarmcos)."""
+
+    def __init__(self, name: str, lr: float, iters_per_epoch: int, total_epochs: int, **kwargs):
+        self.lr = lr
+        self.iters_per_epoch = iters_per_epoch
+        self.total_epochs = total_epochs
+        self.total_iters = iters_per_epoch * total_epochs
+        self.__dict__.update(kwargs)
+        from functools import partial
+        if name == "cos":
+            self.lr_func = partial(cos_lr, self.lr, self.total_iters)
+        elif name == "warmcos":
+            self.lr_func = partial(warm_cos_lr, self.lr, self.total_iters, self.iters_per_epoch * self.warmup_epochs,
+                                   getattr(self, "warmup_lr_start", 1e-6))
+        elif name == "yoloxwarmcos":
+            self.lr_func = partial(yolox_warm_cos_lr, self.lr, getattr(self, "min_lr_ratio", 0.2), self.total_iters,
+                                   self.iters_per_epoch * self.warmup_epochs, getattr(self, "warmup_lr_start", 0),
+                                   self.iters_per_epoch * self.no_aug_epochs)
+        else:
+            raise ValueError(f"Scheduler version {name} not supported.")
+
+    def update_lr(self, iters: int) -> float:
+        return self.lr_func(iters)
+
+
+# ------------------------------------------------------------------ data
+class InfiniteSampler:
+    """data/samplers.py:28-82: an infinite stream of seeded shuffles of range(size); rank r
+    of w reads elements r, r + w, r + 2w, ... (every rank sees a disjoint slice)."""
+
+    def __init__(self, size: int, shuffle: bool = True, seed: int = 0, rank: Optional[int] = None,
+                 world_size: Optional[int] = None):
+        from .launch import get_rank, get_world_size
+        assert size > 0
+        self._size, self._shuffle, self._seed = size, shuffle, int(seed)
+        self._rank = get_rank() if rank is None else rank
+        self._world_size = get_world_size() if world_size is None else world_size
+
+    def _infinite_indices(self):
+        g = torch.Generator()
+        g.manual_seed(self._seed)
+        while True:
+            if self._shuffle:
+                yield from torch.randperm(self._size, generator=g).tolist()
+            else:
+                yield from range(self._size)
+
+    def __iter__(self):
+        import itertools
+        yield from itertools.islice(self._infinite_indices(), self._rank, None, self._world_size)
+
+    def __len__(self) -> int:
+        return self._size // self._world_size
+
+
+class SyntheticCocoDataset:
+    """COCO-shaped training samples (no datasets offline): item i is a seeded uint8 image
+    as float32 CHW in [0, 255] and ``[120, 5]`` padded targets (cls, cx, cy, w, h) in
+    pixels, the layout TrainTransform hands the trainer (data_augment.py:159-232)."""
+
+    def __init__(self, size: int, input_size, seed: int = 0, max_labels: int = 120):
+        self.size, self.input_size, self.seed, self.max_labels = size, tuple(input_size), seed, max_labels
+
+    def __len__(self) -> int:
+        return self.size
+
+    def __getitem__(self, i: int):
+        import numpy as np
+
+        from .weights import synthetic_labels
+        h, w = self.input_size
+        rng = np.random.default_rng((self.seed, int(i)))
+        img = rng.integers(0, 256, size=(3, h, w), dtype=np.uint8).astype(np.float32)
+        lab = synthetic_labels(1, h, w, max_labels=self.max_labels, seed=int(rng.integers(1 << 31)))[0]
+        return torch.from_numpy(img), torch.from_numpy(lab)
+
+
+class SyntheticBatches:
+    """Batches of ``batch_size`` samples in sampler order (YoloBatchSampler over an
+    InfiniteSampler, drop_last False: len = ceil(len(sampler) / batch_size))."""
+
+    def __init__(self, dataset: SyntheticCocoDataset, sampler: InfiniteSampler, batch_size: int):
+        self.dataset, self.sampler, self.batch_size = dataset, sampler, batch_size
+        self._it = iter(sampler)
+
+    def __len__(self) -> int:
+        return (len(self.sampler) + self.batch_size - 1) // self.batch_size
+
+    def next_indices(self) -> list:
+        return [next(self._it) for _ in range(self.batch_size)]
+
+    def next(self):
+        items = [self.dataset[i] for i in self.next_indices()]
+        return torch.stack([a for a, _ in items]), torch.stack([b for _, b in items])
+
+    def close_mosaic(self) -> None:  # no mosaic in the synthetic pipeline
+        pass
+
+
+# ------------------------------------------------------------------ trainer
+class Trainer:
+    """core/trainer.py:34-330 on the HIP path: before_train builds the model, the reference
+    optimizer groups, the data loader (per-rank batch), the yoloxwarmcos schedule, DDP
+    (yolox_amd.dp) and EMA; ``train_one_iter`` is trainer.py:96-129 -- dtype cast,
+    ``config.preprocess`` to the current multiscale size, autocast forward, scaled backward,
+    fused SGD + EMA (+ GradScaler) step, LR update; ``after_iter`` redraws the input size
+    every 10 iterations on rank 0 and broadcasts it (:301-306).  Logging is a print every
+    ``print_interval`` iterations on rank 0; evaluation / checkpoint files are out of scope
+    (DESIGN.md).  ``args.max_iter`` (not in the reference) stops after that many iterations."""
+
+    def __init__(self, config, args):
+        from .launch import get_local_rank, get_rank, get_world_size
+        self.exp = config
+        self.args = args
+        self.max_epoch = config.max_epoch
+        self.amp_training = bool(args.fp16)
+        self.scaler = torch.amp.GradScaler("cuda", enabled=self.amp_training)
+        self.is_distributed = get_world_size() > 1
+        self.rank = get_rank()
+        self.local_rank = get_local_rank()
+        self.device = f"cuda:{self.local_rank}"
+        self.use_model_ema = config.ema
+        self.data_type = torch.float16 if args.fp16 else torch.float32
+        self.input_size = tuple(config.input_size)
+        self.start_epoch = 0
+        self.history: list = []  # (progress, input_size, loss) per iteration
+
+    def train(self) -> None:
+        self.before_train()
+        self.train_in_epoch()
+
+    def train_in_epoch(self) -> None:
+        for self.epoch in range(self.start_epoch, self.max_epoch):
+            self.before_epoch()
+            if not self.train_in_iter():
+                return
+
+    def train_in_iter(self) -> bool:
+        limit = getattr(self.args, "max_iter", None)
+        for self.iter in range(self.max_iter):
+            if limit is not None and self.progress_in_iter >= limit:
+                return False
+            self.train_one_iter()
+            self.after_iter()
+        return True
+
+    @property
+    def progress_in_iter(self) -> int:
+        return self.epoch * self.max_iter + self.iter
+
+    def before_train(self) -> None:
+        from .dp import DistributedDataParallel
+        from .optim import FusedStep
+        torch.cuda.set_device(self.local_rank)
+        model = self.exp.get_model()
+        model.to(self.device)
+        self.optimizer = self.exp.get_optimizer(self.args.batch_size)
+        self.no_aug = self.start_epoch >= self.max_epoch - self.exp.no_aug_epochs
+        self.train_loader = self.exp.get_data_loader(batch_size=self.args.batch_size,
+                                                     is_distributed=self.is_distributed, no_aug=self.no_aug,
+                                                     dataset_size=getattr(self.args, "dataset_size", 118287))
+        self.max_iter = len(self.train_loader)
+        self.lr_scheduler = self.exp.get_lr_scheduler(self.exp.basic_lr_per_img * self.args.batch_size,
+                                                      self.max_iter)
+        if self.is_distributed:
+            model = DistributedDataParallel(model, device_ids=[self.local_rank], broadcast_buffers=False)
+        self.ema_model = None
+        if self.use_model_ema:
+            self.ema_model = ModelEMA(model, 0.9998)
+            self.ema_model.updates = self.max_iter * self.start_epoch
+        self.model = model
+        self.fused = FusedStep(model, self.optimizer, self.ema_model)
+
+    def before_epoch(self) -> None:
+        if self.epoch + 1 == self.max_epoch - self.exp.no_aug_epochs or self.no_aug:
+            self.train_loader.close_mosaic()
+            m = self.model.module if self.is_distributed else self.model
+            m.head.use_l1 = True
+
+    def train_one_iter(self) -> None:
+        inps, targets = self.train_loader.next()
+        inps = inps.to(self.device, non_blocking=True).to(self.data_type)
+        targets = targets.to(self.device, non_blocking=True).to(self.data_type)
+        targets.requires_grad = False
+        inps, targets = self.exp.preprocess(inps, targets, self.input_size)
+        with torch.autocast("cuda", dtype=torch.float16, enabled=self.amp_training):
+            outputs = self.model(inps, targets)
+        loss = outputs["total_loss"]
+        self.optimizer.zero_grad(set_to_none=True)
+        self.scaler.scale(loss).backward()
+        self.fused.step(self.scaler if self.amp_training else None)  # SGD + EMA (+ scaler.step/update)
+        lr = self.lr_scheduler.update_lr(self.progress_in_iter + 1)
+        for param_group in self.optimizer.param_groups:
+            param_group["lr"] = lr
+        self.history.append((self.progress_in_iter, self.input_size, loss))
+
+    def after_iter(self) -> None:
+        if self.rank == 0 and (self.iter + 1) % self.exp.print_interval == 0:
+            _, size, loss = self.history[-1]
+            print(f"epoch: {self.epoch + 1}/{self.max_epoch}, iter: {self.iter + 1}/{self.max_iter}, "
+                  f"total_loss: {float(loss):.3f}, lr: {self.optimizer.param_groups[0]['lr']:.3e}, size: {size[0]}",
+                  flush=True)
+        if not self.exp.deterministic and (self.progress_in_iter + 1) % 10 == 0:
+            self.input_size = self.exp.random_resize(self.train_loader, self.epoch, self.rank, self.is_distributed)
