@@ -7,8 +7,8 @@ forward (Focus -> CSPDarknet -> PAFPN -> decoupled head with fused decode, 82
 kernels) followed by device post-processing (filter, sort, bitmask NMS) at the
 processor defaults (conf 0.5, nms 0.65); a batch's NMS runs on a side stream beside the
 next batch's forward, which waits only for the NMS filter pass (the one reader of the
-forward's output) -- --serial-nms runs them back to back on one stream.  Inputs are resident in HBM (bf16 NHWC)
-before the timed region.  With --gpus N (torchrun, one process per GPU) each rank
+forward's output) -- --serial-nms runs them back to back on one stream.  Inputs are resident in HBM (uint8 NHWC, as the
+processor's letterbox hands them to the forward) before the timed region.  With --gpus N (torchrun, one process per GPU) each rank
 runs an independent replica -- inference has no exchange step, so there is no
 collective in the data path -- and value = all images / max
 rank time.
@@ -209,6 +209,7 @@ def layer_table(plan, iters=5):
                          tot[i], flop / tot[i] / 1e9, byt / tot[i] / 1e6))
         else:
             rows.append((i, {N.OP_FOCUS: "focus", N.OP_SPP: "spp", N.OP_STEM: "stem (focus+conv)",
+                             N.OP_STEM2: "stem + dark2.0 (fused, stem_s2)",
                              N.OP_HEAD: f"head preds+decode @{a.get('h')}x{a.get('w')}"}[rec.kind], tot[i],
                          0.0, 0.0))
     print(f"{'op':>3} {'layer':<40} {'ms':>8} {'TFLOP/s':>9} {'GB/s':>8}", file=sys.stderr)
@@ -422,9 +423,11 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     model = YoloxModule.synthetic(args.model, seed=0, device=dev, dtype=dtype)
     B, S = args.batch, args.size
-    plan = model.plan_for(B, S, S, N.NHWC, dtype, chunk=args.chunk or None, parallel_chunks=args.par_chunks)
+    # input: letterboxed uint8 NHWC images resident in HBM -- the form YoloxProcessor's
+    # letterbox_batch hands Yolox.__call__'s forward (forward_nhwc)
+    plan = model.plan_for(B, S, S, N.NHWC, torch.uint8, chunk=args.chunk or None, parallel_chunks=args.par_chunks)
     imgs = torch.from_numpy(synthetic_images(B, S, S, seed=1000 + rank)).to(dev)
-    plan.static_input().copy_(imgs.to(dtype))
+    plan.static_input().copy_(imgs)
     from yolox_amd import engine
     if args.tune_file and os.path.exists(args.tune_file):
         engine.load_tune_cache(args.tune_file)
@@ -518,7 +521,7 @@ def main():
             "baseline_config_index": idx,
             "batch_per_gpu": B, "global_batch": B * world, "image_size": S,
             "parallelism": f"replicas x{world} (no data-path collective)",
-            "input": f"{args.dtype} NHWC resident in HBM",
+            "input": "uint8 NHWC letterboxed images resident in HBM",
             "chunk": plan.chunk,
             "parallel_chunks": plan.parallel_chunks,
             "graph": plan.graph_mode,

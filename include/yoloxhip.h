@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 9
+#define YXH_ABI_VERSION 10
 
 enum yxh_status {
     YXH_OK = 0,
@@ -154,6 +154,31 @@ typedef struct {
     int32_t reserved;
     int64_t dst_bstride;
 } yxh_stem_desc;
+
+/*
+ * yxh_stem_s2: the Focus stem AND the first stride-2 3x3 conv (darknet.py:112-123 stem +
+ * dark2[0], both BaseConv with BN folded) in one launch, from a uint8 / bf16 / f16 NHWC
+ * image: the C1-channel stem map (H/2 x W/2) lives only in LDS, per 16 x 8 output tile.
+ *   w1 [c1][3][3][12] (`dtype`; yxh_fold_bn_pack with cin_pad 12: k = ky*36 + kx*12 +
+ *       q*3 + c over Focus channels q*3 + c, q = TL, BL, TR, BR), b1 [c1] fp32
+ *   w2 [c2][3][3][c1] (`dtype`), b2 [c2] fp32
+ *   dst [B][H/4][W/4] rows of dst_cstride elements (`dtype`), channels [0, c2)
+ * bf16/f16 compute, c1 = 32 / c2 = 64 (yolox_s), h and w multiples of 4.
+ */
+typedef struct {
+    const void* img;
+    int32_t layout, img_dtype, batch, h, w;
+    int32_t dtype, c1, c2, act;
+    const void* w1;
+    const float* b1;
+    const void* w2;
+    const float* b2;
+    void* dst;
+    int32_t dst_cstride;
+    int32_t reserved;
+    int64_t dst_bstride;
+} yxh_stem2_desc;
+int yxh_stem_s2(const yxh_stem2_desc* d, void* stream);
 int yxh_stem_conv(const yxh_stem_desc* d, void* stream);
 int yxh_stem_pack(const float* conv_w, const float* bn_gamma, const float* bn_beta, const float* bn_mean,
                   const float* bn_var, float eps, int32_t cout, int32_t dtype, void* w_out, float* b_out,
@@ -355,7 +380,8 @@ int yxh_yolox_loss_bwd(const float* preds, const float* raw, const float* labels
  * captured once into a hipGraph and replayed (the MI355X replacement for the
  * reference's eager per-module dispatch).
  */
-enum yxh_op_kind { YXH_OP_CONV = 0, YXH_OP_FOCUS = 1, YXH_OP_SPP = 2, YXH_OP_STEM = 3, YXH_OP_HEAD = 4 };
+enum yxh_op_kind { YXH_OP_CONV = 0, YXH_OP_FOCUS = 1, YXH_OP_SPP = 2, YXH_OP_STEM = 3, YXH_OP_HEAD = 4,
+                   YXH_OP_STEM2 = 5 };
 typedef struct {
     const void* img;
     int32_t layout, img_dtype, batch, h, w, dst_dtype;
@@ -396,6 +422,7 @@ typedef struct {
         yxh_spp_desc spp;
         yxh_stem_desc stem;
         yxh_head_desc head;
+        yxh_stem2_desc stem2;
     } u;
 } yxh_op;
 

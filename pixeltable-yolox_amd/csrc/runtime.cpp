@@ -66,6 +66,7 @@ int yolox_loss_bwd(const float* preds, const float* raw, const float* labels, in
 int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
                 float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t filter_done);
 int head_pred_launch(const yxh_head_desc* d, hipStream_t st);
+int stem_s2_launch(const yxh_stem2_desc* d, hipStream_t st);
 
 static int run_op(const yxh_op& op, hipStream_t st) {
     switch (op.kind) {
@@ -79,6 +80,8 @@ static int run_op(const yxh_op& op, hipStream_t st) {
             return stem_launch(&op.u.stem, st);
         case YXH_OP_HEAD:
             return head_pred_launch(&op.u.head, st);
+        case YXH_OP_STEM2:
+            return stem_s2_launch(&op.u.stem2, st);
         case YXH_OP_SPP: {
             const yxh_spp_desc& s = op.u.spp;
             return spp_launch(s.buf, s.dtype, s.batch, s.h, s.w, s.c, s.cstride, s.bstride, st);
@@ -110,6 +113,8 @@ int yxh_focus_pack(const void* img, int32_t layout, int32_t img_dtype, int32_t b
 }
 
 int yxh_stem_conv(const yxh_stem_desc* d, void* stream) { return stem_launch(d, (hipStream_t)stream); }
+
+int yxh_stem_s2(const yxh_stem2_desc* d, void* stream) { return stem_s2_launch(d, (hipStream_t)stream); }
 
 int yxh_stem_pack(const float* conv_w, const float* bn_gamma, const float* bn_beta, const float* bn_mean,
                   const float* bn_var, float eps, int32_t cout, int32_t dtype, void* w_out, float* b_out,

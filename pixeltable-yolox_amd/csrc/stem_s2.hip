@@ -1,0 +1,351 @@
+// Fused Focus stem + first stride-2 3x3 conv on gfx950 (reference darknet.py:112-123:
+// stem = Focus(3, C1, ksize=3) = space-to-depth + BaseConv(4*3 -> C1, 3x3 s1), then
+// dark2[0] = BaseConv(C1 -> 2*C1, 3x3 s2); network_blocks.py:27-52, 186-208).
+//
+// The unfused forms write the C1-channel stem map at H/2 x W/2 (yolox_s @640 bs32: 210 MB)
+// and read it back for the stride-2 conv.  Here one persistent block computes a 16 x 8 tile
+// of the stride-2 conv's output directly from the image:
+//   1. the image patch the tile needs (38 rows x 70 pixels x 3 channels, zero outside the
+//      image) arrives by buffer loads issued one tile ahead into registers (groups of 4
+//      pixels) and is written to LDS as RGB0 pixels of 8 bytes;
+//   2. the stem conv over the 17 x 33 stem pixels the stride-2 conv reads.  Focus + 3x3 is
+//      a 6x6 stride-2 conv on the image (stem.hip); one kernel row of it is 6 RGB0 pixels =
+//      24 contiguous LDS values = three 16-byte K chunks, so K = 6 x 24 = 144 (108 real,
+//      5 MFMA slabs) and every B fragment is one aligned ds_read_b128 -- bias + SiLU, zeros
+//      outside the stem map (the stride-2 conv's zero padding), into a second LDS image laid
+//      out as conv_ws's stride-2 halo (5 16-byte slots per pixel: conflict-free reads);
+//   3. the stride-2 conv (K = 9 taps x C1) from that image with weights stationary in VGPRs,
+//      bias + SiLU, 8-byte stores of 4 channels.
+// Two blocks per CU: one block's image loads / barriers overlap the other's MFMAs.
+#include <algorithm>
+
+#include "conv_common.hpp"
+#include "lds_dma.hpp"
+
+namespace yxh {
+
+struct Stem2Params {
+    const void* img;
+    int B, H, W, OH1, OW1, OH, OW;
+    const void* w1;  // yxh_stem_pack layout [round16(C1)][6][32]: ky6, kx6 * 3 + c
+    const float* b1;
+    const void* w2;  // [C2][9][C1]
+    const float* b2;
+    void* dst;
+    int dst_cs;
+    long long dst_bs;
+    int act1, act2;
+};
+
+namespace {
+
+constexpr int kS2TX = 16, kS2TY = 8;                       // output tile of the stride-2 conv
+constexpr int kS2SX = 2 * kS2TX + 1, kS2SY = 2 * kS2TY + 1;  // stem pixels the tile needs
+constexpr int kS2IY = 4 * kS2TY + 6, kS2IX = 4 * kS2TX + 6;  // image rows / pixels of the patch
+constexpr int kS2G = (kS2IX + 3) / 4;                       // 4-pixel groups per patch row (18)
+constexpr int kS2IXP = 4 * kS2G;                            // LDS pixels per patch row (72)
+constexpr int kS2NSP = kS2SX * kS2SY;                       // 561 stem pixels
+constexpr int kS2NF1 = (kS2NSP + 15) / 16;                  // 36 stem pixel fragments
+constexpr int kS2FBYTES = kS2IY * kS2IXP * 8;               // RGB0 image patch (21.9 KB)
+
+// element q of a group of 4 RGB pixels (12 image values) held in 12 / (4 / sizeof(TI)) dwords
+template <typename T, typename TI>
+__device__ __forceinline__ T group_elem(const uint32_t* w, int q) {
+    if constexpr (sizeof(TI) == 1) {
+        return from_f32<T>((float)((w[q >> 2] >> (8 * (q & 3))) & 0xffu));
+    } else {
+        const uint32_t v = w[q >> 1] >> (16 * (q & 1));
+        const uint16_t h = (uint16_t)v;
+        TI x;
+        __builtin_memcpy(&x, &h, 2);
+        return from_f32<T>(to_f32(x));
+    }
+}
+
+}  // namespace
+
+template <typename T, typename TI, int C1>
+__global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, int tiles_y, int ntiles) {
+    static_assert(sizeof(T) == 2, "16-bit compute");
+    static_assert(C1 == 32, "stem width");
+    constexpr int C2 = 2 * C1;
+    constexpr int GDW = 3 * (int)sizeof(TI);       // dwords per 4-pixel group (12 values)
+    constexpr int NGR = kS2IY * kS2G;              // groups per patch (684)
+    constexpr int NPT = (NGR + 255) / 256;         // groups per thread
+    constexpr int HXP = kS2SX, PS = 5, PSB = PS * 16;  // stem image: conv_ws stride-2 halo layout
+    constexpr int SBYTES = kS2SY * HXP * PSB;
+    constexpr int FR2 = 2, FC2 = 4;                // stride-2 conv: 2 waves x 32 channels, 2 waves x 64 pixels
+    static_assert(C2 == 2 * 16 * FR2 && kS2TX * kS2TY == 2 * 16 * FC2, "wave tiling");
+    __shared__ __attribute__((aligned(16))) char smem[kS2FBYTES + SBYTES];
+    char* fimg = smem;
+    char* simg = smem + kS2FBYTES;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int frow = lane & 15, fq = lane >> 4;
+    const int wn = wave & 1, wm = wave >> 1;
+
+    // ---- stationary weights
+    // stem A fragments, K = ky * 24 + kx * 4 + c (c = 3 and k >= 144 are zero), from the
+    // yxh_stem_pack rows [6][32] (ky, kx * 3 + c)
+    const T* w1 = (const T*)p.w1;
+    uint4 a1[2][5];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int s = 0; s < 5; ++s) {
+            T t[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int k = 32 * s + 8 * fq + e;
+                const int ky = k / 24, kx = (k % 24) >> 2, c = k & 3;
+                t[e] = (k < 144 && c < 3) ? w1[((i * 16 + frow) * 6 + ky) * 32 + kx * 3 + c] : from_f32<T>(0.0f);
+            }
+            __builtin_memcpy(&a1[i][s], t, 16);
+        }
+    const T* w2 = (const T*)p.w2;
+    uint4 a2[FR2][9];
+#pragma unroll
+    for (int i = 0; i < FR2; ++i)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+            a2[i][tap] = *(const uint4*)(w2 + ((wn * 32 + i * 16 + frow) * 9 + tap) * C1 + fq * 8);
+    float bias1[2][4], bias2[FR2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias1[i][r] = p.b1[i * 16 + fq * 4 + r];
+#pragma unroll
+    for (int i = 0; i < FR2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias2[i][r] = p.b2[wn * 32 + i * 16 + fq * 4 + r];
+    const bool silu1 = p.act1 == YXH_ACT_SILU, silu2 = p.act2 == YXH_ACT_SILU;
+
+    // ---- per-lane stem K-chunk offsets (bytes from a stem pixel's base in the RGB0 patch):
+    // chunk k0 = 32 s + 8 fq = kernel row k0 / 24, pixels (k0 % 24) / 4 .. +1; k0 >= 144 is
+    // weight padding and re-reads a real chunk (finite values)
+    uint32_t off1[5];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        int k = 32 * s + 8 * fq;
+        if (k >= 144) k = 136;
+        off1[s] = (uint32_t)(((k / 24) * kS2IXP + (k % 24) / 4) * 8);
+    }
+
+    const int W3 = p.W * 3;
+    const uint32_t ibytes = (uint32_t)((long long)p.H * W3 * sizeof(TI));
+    const unsigned txy = (unsigned)(tiles_x * tiles_y);
+    struct TileC { int b, oy0, ox0; };
+    auto coords = [&](int t) -> TileC {
+        const unsigned b = (unsigned)t / txy, r = (unsigned)t - b * txy;
+        const unsigned ty = r / (unsigned)tiles_x, tx = r - ty * (unsigned)tiles_x;
+        return TileC{(int)b, (int)ty * kS2TY, (int)tx * kS2TX};
+    };
+    uint32_t img[NPT][GDW];
+    auto load_image = [&](const TileC& c) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)((const TI*)p.img + (long long)c.b * p.H * W3), (short)0, (int)ibytes, 0x00020000);
+        const int iy0 = 4 * c.oy0 - 4, ix0 = 4 * c.ox0 - 4;
+#pragma unroll
+        for (int t = 0; t < NPT; ++t) {
+            const int g = tid + 256 * t;
+            const int row = g / kS2G, gc = g - kS2G * (g / kS2G);
+            const int iy = iy0 + row, ix = ix0 + 4 * gc;
+            // a group (4 pixels, W % 4 == 0, ix % 4 == 0) is wholly inside the image or outside
+            const bool ok = g < NGR && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+            const int voff = ok ? (iy * W3 + ix * 3) * (int)sizeof(TI) : (int)dma::kOob;
+#pragma unroll
+            for (int d = 0; d < GDW; ++d) img[t][d] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 4 * d, 0, 0);
+        }
+    };
+    auto store_image = [&]() {
+#pragma unroll
+        for (int t = 0; t < NPT; ++t) {
+            const int g = tid + 256 * t;
+            if (g >= NGR) continue;
+            const int row = g / kS2G, gc = g - kS2G * (g / kS2G);
+            char* d = fimg + (row * kS2IXP + 4 * gc) * 8;
+#pragma unroll
+            for (int px = 0; px < 4; ++px) {
+                T t4[4] = {group_elem<T, TI>(img[t], 3 * px), group_elem<T, TI>(img[t], 3 * px + 1),
+                           group_elem<T, TI>(img[t], 3 * px + 2), from_f32<T>(0.0f)};
+                uint2 u;
+                __builtin_memcpy(&u, t4, 8);
+                *(uint2*)(d + px * 8) = u;
+            }
+        }
+    };
+
+    const int bid = dma::xcd_remap(blockIdx.x, gridDim.x);
+    int tile = bid;
+    if (tile >= ntiles) return;  // block-uniform
+    TileC cur = coords(tile);
+    load_image(cur);
+    for (; tile < ntiles; tile += gridDim.x) {
+        store_image();
+        // image patch complete; every wave is past the last tile's conv stage (LDS only: the
+        // image loads for the next tile stay in flight across the barrier)
+        dma::barrier();
+        const int next = tile + gridDim.x;
+        TileC nc = cur;
+        if (next < ntiles) {
+            nc = coords(next);
+            load_image(nc);  // lands during this tile's two GEMMs
+        }
+
+        // ---- stem: 36 fragments of 16 stem pixels, wave w takes w, w + 4, ... (3 at a time)
+#pragma unroll
+        for (int g0 = 0; g0 < kS2NF1 / 4; g0 += 3) {
+            f32x4 acc[2][3];
+            uint32_t pb[3];
+#pragma unroll
+            for (int jj = 0; jj < 3; ++jj) {
+                const int pix = min((wave + 4 * (g0 + jj)) * 16 + frow, kS2NSP - 1);
+                const int sy = pix / kS2SX, sx = pix - kS2SX * (pix / kS2SX);
+                pb[jj] = (uint32_t)((2 * sy * kS2IXP + 2 * sx) * 8);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int s = 0; s < 5; ++s) {
+                uint4 b[3];
+#pragma unroll
+                for (int jj = 0; jj < 3; ++jj) b[jj] = *(const uint4*)(fimg + pb[jj] + off1[s]);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < 3; ++jj) Mma<T>::run(acc[i][jj], a1[i][s], b[jj]);
+            }
+#pragma unroll
+            for (int jj = 0; jj < 3; ++jj) {
+                const int pix = (wave + 4 * (g0 + jj)) * 16 + frow;
+                const int sy = pix / kS2SX, sx = pix - kS2SX * (pix / kS2SX);
+                const int gy = 2 * cur.oy0 - 1 + sy, gx = 2 * cur.ox0 - 1 + sx;
+                const bool valid = (unsigned)gy < (unsigned)p.OH1 && (unsigned)gx < (unsigned)p.OW1;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    T t[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float x = acc[i][jj][r] + bias1[i][r];
+                        t[r] = from_f32<T>(valid ? (silu1 ? yxh::silu<false>(x) : x) : 0.0f);
+                    }
+                    uint2 u;
+                    __builtin_memcpy(&u, t, 8);
+                    if (pix < kS2NSP) *(uint2*)(simg + (sy * HXP + sx) * PSB + (i * 16 + fq * 4) * 2) = u;
+                }
+            }
+        }
+        dma::barrier();  // stem image complete
+
+        // ---- stride-2 conv: wave (wn, wm) = 32 channels x 64 pixels of the 16 x 8 tile
+        f32x4 acc2[FR2][FC2];
+        uint32_t boff[FC2];
+#pragma unroll
+        for (int j = 0; j < FC2; ++j) {
+            const int pl = (wm * FC2 + j) * 16 + frow;
+            const int ty = pl / kS2TX, tx = pl - kS2TX * (pl / kS2TX);
+            boff[j] = (uint32_t)(((2 * ty) * HXP + 2 * tx) * PSB + fq * 16);
+#pragma unroll
+            for (int i = 0; i < FR2; ++i) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+            const uint32_t so = (uint32_t)((ky * HXP + kx) * PSB);
+            uint4 b[FC2];
+#pragma unroll
+            for (int j = 0; j < FC2; ++j) b[j] = *(const uint4*)(simg + boff[j] + so);
+#pragma unroll
+            for (int i = 0; i < FR2; ++i)
+#pragma unroll
+                for (int j = 0; j < FC2; ++j) Mma<T>::run(acc2[i][j], a2[i][tap], b[j]);
+        }
+        T* dst = (T*)p.dst + (long long)cur.b * p.dst_bs;
+#pragma unroll
+        for (int j = 0; j < FC2; ++j) {
+            const int pl = (wm * FC2 + j) * 16 + frow;
+            const int ty = pl / kS2TX, tx = pl - kS2TX * (pl / kS2TX);
+            const int oy = cur.oy0 + ty, ox = cur.ox0 + tx;
+            if (oy >= p.OH || ox >= p.OW) continue;
+#pragma unroll
+            for (int i = 0; i < FR2; ++i) {
+                const int n = wn * 32 + i * 16 + fq * 4;
+                T t[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float x = acc2[i][j][r] + bias2[i][r];
+                    t[r] = from_f32<T>(silu2 ? yxh::silu<false>(x) : x);
+                }
+                uint2 u;
+                __builtin_memcpy(&u, t, 8);
+                *(uint2*)(dst + (long long)(oy * p.OW + ox) * p.dst_cs + n) = u;
+            }
+        }
+        cur = nc;
+    }
+}
+
+template <typename T, typename TI>
+static int launch_s2(const Stem2Params& p, hipStream_t st) {
+    const int tiles_x = (p.OW + kS2TX - 1) / kS2TX, tiles_y = (p.OH + kS2TY - 1) / kS2TY;
+    const long long ntiles = (long long)tiles_x * tiles_y * p.B;
+    if (ntiles >= (1LL << 30)) {
+        set_error("stem_s2: too many tiles");
+        return YXH_EINVAL;
+    }
+    const int grid = (int)std::min<long long>(ntiles, 256 * 2);
+    hipLaunchKernelGGL((stem_s2<T, TI, 32>), dim3(grid), dim3(256), 0, st, p, tiles_x, tiles_y, (int)ntiles);
+    YXH_CHECK_LAUNCH("stem_s2 launch");
+    return YXH_OK;
+}
+
+template <typename T>
+static int launch_s2_t(int idt, const Stem2Params& p, hipStream_t st) {
+    switch (idt) {
+        case YXH_U8: return launch_s2<T, uint8_t>(p, st);
+        case YXH_BF16: return launch_s2<T, bf16>(p, st);
+        case YXH_F16: return launch_s2<T, f16>(p, st);
+        default: set_error("stem_s2 image dtype %d", idt); return YXH_EINVAL;
+    }
+}
+
+int stem_s2_launch(const yxh_stem2_desc* d, hipStream_t st) {
+    YXH_CHECK_ARG(d && d->img && d->w1 && d->b1 && d->w2 && d->b2 && d->dst, "null pointer");
+    YXH_CHECK_ARG(d->layout == YXH_NHWC, "stem_s2 reads NHWC images");
+    YXH_CHECK_ARG(d->dtype == YXH_BF16 || d->dtype == YXH_F16, "stem_s2 computes in bf16/f16");
+    YXH_CHECK_ARG(d->c1 == 32 && d->c2 == 64, "stem_s2 is built for 32 stem / 64 conv channels (got %d/%d)", d->c1,
+                  d->c2);
+    YXH_CHECK_ARG(d->batch > 0 && d->h >= 4 && d->w >= 4 && d->h % 4 == 0 && d->w % 4 == 0, "image %dx%d", d->h,
+                  d->w);
+    YXH_CHECK_ARG(d->img_dtype == YXH_U8 || d->img_dtype == YXH_BF16 || d->img_dtype == YXH_F16,
+                  "stem_s2 reads u8 / bf16 / f16 images");
+    const int es = d->img_dtype == YXH_U8 ? 1 : 2;
+    YXH_CHECK_ARG(((uintptr_t)d->img % 4) == 0 && (long long)d->h * d->w * 3 * es < (1LL << 31),
+                  "stem_s2 image alignment / size");
+    YXH_CHECK_ARG(((uintptr_t)d->dst % 8) == 0 && d->dst_cstride % 4 == 0 && d->dst_cstride >= 64 &&
+                      d->dst_bstride % 4 == 0,
+                  "stem_s2 dst alignment");
+    Stem2Params p;
+    p.img = d->img;
+    p.B = d->batch;
+    p.H = d->h;
+    p.W = d->w;
+    p.OH1 = d->h / 2;
+    p.OW1 = d->w / 2;
+    p.OH = (p.OH1 - 1) / 2 + 1;
+    p.OW = (p.OW1 - 1) / 2 + 1;
+    p.w1 = d->w1;
+    p.b1 = d->b1;
+    p.w2 = d->w2;
+    p.b2 = d->b2;
+    p.dst = d->dst;
+    p.dst_cs = d->dst_cstride;
+    p.dst_bs = d->dst_bstride;
+    p.act1 = d->act;
+    p.act2 = d->act;
+    if (d->dtype == YXH_BF16) return launch_s2_t<bf16>(d->img_dtype, p, st);
+    return launch_s2_t<f16>(d->img_dtype, p, st);
+}
+
+}  // namespace yxh

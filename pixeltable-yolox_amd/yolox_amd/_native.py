@@ -17,14 +17,14 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
 F32, BF16, F16, U8 = 0, 1, 2, 3
 ACT_NONE, ACT_SILU, ACT_RELU, ACT_LRELU, ACT_DECODE, ACT_DECODE_TRAIN = range(6)
 NCHW, NHWC = 0, 1
-OP_CONV, OP_FOCUS, OP_SPP, OP_STEM, OP_HEAD = 0, 1, 2, 3, 4
+OP_CONV, OP_FOCUS, OP_SPP, OP_STEM, OP_HEAD, OP_STEM2 = 0, 1, 2, 3, 4, 5
 LB_F32_NCHW, LB_U8_NHWC, LB_BF16_NHWC = 0, 1, 2
 
 TORCH_DTYPE = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16, U8: torch.uint8}
@@ -102,6 +102,13 @@ class StemDesc(C.Structure):
                 ("reserved", C.c_int32), ("dst_bstride", C.c_int64)]
 
 
+class Stem2Desc(C.Structure):
+    _fields_ = [("img", C.c_void_p), ("layout", C.c_int32), ("img_dtype", C.c_int32), ("batch", C.c_int32),
+                ("h", C.c_int32), ("w", C.c_int32), ("dtype", C.c_int32), ("c1", C.c_int32), ("c2", C.c_int32),
+                ("act", C.c_int32), ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p),
+                ("dst", C.c_void_p), ("dst_cstride", C.c_int32), ("reserved", C.c_int32), ("dst_bstride", C.c_int64)]
+
+
 class HeadDesc(C.Structure):
     _fields_ = [("dtype", C.c_int32), ("batch", C.c_int32), ("h", C.c_int32), ("w", C.c_int32), ("cin", C.c_int32),
                 ("num_classes", C.c_int32), ("reg", Src), ("cls", Src), ("w_reg", C.c_void_p), ("b_reg", C.c_void_p),
@@ -110,7 +117,8 @@ class HeadDesc(C.Structure):
 
 
 class _OpU(C.Union):
-    _fields_ = [("conv", ConvDesc), ("focus", FocusDesc), ("spp", SppDesc), ("stem", StemDesc), ("head", HeadDesc)]
+    _fields_ = [("conv", ConvDesc), ("focus", FocusDesc), ("spp", SppDesc), ("stem", StemDesc), ("head", HeadDesc),
+                ("stem2", Stem2Desc)]
 
 
 class Op(C.Structure):
@@ -150,6 +158,7 @@ def lib():
             "yxh_focus_pack": ([vp, i32, i32, i32, i32, i32, vp, i32, vp], C.c_int),
             "yxh_spp_maxpool": ([vp, i32, i32, i32, i32, i32, i32, i64, vp], C.c_int),
             "yxh_stem_conv": ([C.POINTER(StemDesc), vp], C.c_int),
+            "yxh_stem_s2": ([C.POINTER(Stem2Desc), vp], C.c_int),
             "yxh_stem_pack": ([vp, vp, vp, vp, vp, f32, i32, i32, vp, vp, vp], C.c_int),
             "yxh_fold_bn_pack": ([vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, i32, vp, vp, vp],
                                  C.c_int),
@@ -202,7 +211,7 @@ def lib():
 
 
 EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d", "yxh_head_pred",
-            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_postprocess_workspace_bytes", "yxh_set_nms_mask_budget",
+            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_s2", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_postprocess_workspace_bytes", "yxh_set_nms_mask_budget",
             "yxh_postprocess", "yxh_postprocess_ev", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes", "yxh_graph_create_dag",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
             "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_spp_bwd",

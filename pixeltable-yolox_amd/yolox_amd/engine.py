@@ -111,7 +111,7 @@ _FUSE_BOTTLENECK = os.environ.get("YOLOX_AMD_FUSE_BOTTLENECK", "0") == "1"
 
 class PlanCtx:
     def __init__(self, batch: int, dtype: torch.dtype, device: torch.device, fuse_stem: bool = True,
-                 fuse_bottleneck: bool = _FUSE_BOTTLENECK):
+                 fuse_bottleneck: bool = _FUSE_BOTTLENECK, fuse_stem_s2: bool = True):
         if dtype not in (torch.float32, torch.bfloat16, torch.float16):
             raise ValueError(f"compute dtype {dtype} not supported (float32, bfloat16, float16)")
         self.batch = batch
@@ -121,6 +121,10 @@ class PlanCtx:
         self.epc = 16 // self.esize
         self.device = device
         self.fuse_stem = fuse_stem
+        self.fuse_stem_s2 = fuse_stem_s2  # Focus stem + dark2[0] as one yxh_stem_s2 launch
+        # the image the plan reads (set by Plan): the fused stem + stride-2 conv needs NHWC
+        self.input_layout = N.NHWC
+        self.input_dtype = torch.uint8
         # Bottleneck conv1 (1x1) folded into conv2's 3x3 (conv_ws fused tiles): 16-bit only
         self.fuse_bottleneck = fuse_bottleneck and dtype != torch.float32
         self.buffers: list[Buffer] = []
@@ -155,6 +159,35 @@ class PlanCtx:
         self.ops.append(OpRec(N.OP_STEM, dict(dst=out.full(), h=img.h, w=img.w, spec=spec,
                                               act=N.ACT_CODE[getattr(m, "act_name", "silu")])))
         self.flops += 2.0 * self.batch * out.h * out.w * conv.out_channels * 9 * 12
+        return out.full()
+
+    def stem_s2_fusable(self, stem, conv) -> bool:
+        """Focus stem + dark2[0] as one yxh_stem_s2 launch: 16-bit compute, an NHWC
+        u8/bf16/f16 image, 12 -> 32 stem channels, BaseConv 32 -> 64 3x3 s2, SiLU both."""
+        c1 = stem.conv
+        c2 = getattr(conv, "conv", None)
+        return (self.fuse_stem and self.fuse_stem_s2 and self.dtype != torch.float32 and self.input_layout == N.NHWC
+                and self.input_dtype in (torch.uint8, torch.bfloat16, torch.float16) and c2 is not None
+                and self.stem_fusable(stem) and c1.out_channels == 32 and c2.in_channels == 32
+                and c2.out_channels == 64 and c2.kernel_size == (3, 3) and c2.stride == (2, 2)
+                and c2.padding == (1, 1) and c2.groups == 1
+                and getattr(stem, "act_name", "silu") == getattr(conv, "act_name", "silu") == "silu")
+
+    def stem_s2(self, stem, conv, img: ImageRef) -> View:
+        """Focus + stem BaseConv + dark2[0] (darknet.py:112-123) as ONE launch: the stem map
+        exists only per tile in LDS (csrc/stem_s2.hip)."""
+        if img.h % 4 or img.w % 4:
+            raise ValueError("stem_s2 needs image sides that are multiples of 4")
+        oh1, ow1 = img.h // 2, img.w // 2
+        oh, ow = (oh1 - 1) // 2 + 1, (ow1 - 1) // 2 + 1
+        c1, c2 = stem.conv.out_channels, conv.conv.out_channels
+        out = self.buffer(oh, ow, c2)
+        s1 = WeightSpec([(stem.conv, stem.bn)], c1, 12, 3, 3, 12, stem=True)
+        self.weights.append(s1)
+        s2 = self._weights([(conv.conv, conv.bn)], c1)
+        self.ops.append(OpRec(N.OP_STEM2, dict(dst=out.full(), h=img.h, w=img.w, spec1=s1, spec2=s2, c1=c1, c2=c2,
+                                               act=N.ACT_SILU)))
+        self.flops += 2.0 * self.batch * oh1 * ow1 * c1 * 9 * 12 + 2.0 * self.batch * oh * ow * c2 * 9 * c1
         return out.full()
 
     def focus(self, h: int, w: int) -> View:
@@ -343,7 +376,7 @@ def op_buffers(r: OpRec) -> tuple:
     a = r.args
     if r.kind == N.OP_SPP:
         return [a["buf"]], [a["buf"]]
-    if r.kind in (N.OP_FOCUS, N.OP_STEM):
+    if r.kind in (N.OP_FOCUS, N.OP_STEM, N.OP_STEM2):
         return [], [a["dst"].buf]
     if r.kind == N.OP_HEAD:
         return [a["reg"].buf, a["cls"].buf], []
@@ -402,7 +435,7 @@ class Plan:
     def __init__(self, model, batch: int, height: int, width: int, dtype: torch.dtype, device,
                  input_layout: int = N.NCHW, input_dtype: torch.dtype = torch.float32, train: bool = False,
                  fuse_stem: bool = True, chunk: Optional[int] = None, fuse_bottleneck: bool = _FUSE_BOTTLENECK,
-                 parallel_chunks: bool = False):
+                 parallel_chunks: bool = False, fuse_stem_s2: bool = True):
         if height % 32 or width % 32:
             raise ValueError("input size must be multiples of 32")
         chunk = chunk or batch
@@ -418,7 +451,9 @@ class Plan:
         self.dtype = dtype
         head = model.head
         self.num_classes = head.num_classes
-        ctx = PlanCtx(chunk, dtype, self.device, fuse_stem=fuse_stem, fuse_bottleneck=fuse_bottleneck)
+        ctx = PlanCtx(chunk, dtype, self.device, fuse_stem=fuse_stem, fuse_bottleneck=fuse_bottleneck,
+                      fuse_stem_s2=fuse_stem_s2)
+        ctx.input_layout, ctx.input_dtype = input_layout, input_dtype
         feats = model.backbone.plan(ctx, ctx.image(height, width))
         anchors = sum(f.lh * f.lw for f in feats)
         self.out_spec = OutBuffer(anchors, 5 + self.num_classes)
@@ -429,9 +464,12 @@ class Plan:
         self.nlanes = 1 + max((r.lane for r in ctx.ops), default=0)
         self._deps = op_dependencies(ctx.ops)
         self.use_lanes = os.environ.get("YOLOX_AMD_LANES", "1") != "0"
-        # captured graph form: "dag" (one node per op, dataflow edges; default), "lanes"
-        # (multi-stream capture, head levels on lanes), "linear" (one stream)
-        self.graph_mode = os.environ.get("YOLOX_AMD_GRAPH", "dag")
+        # captured graph form: "lanes" (multi-stream capture: head levels on lanes, or one lane
+        # per chunk with parallel_chunks; default), "dag" (one child-graph node per op, dataflow
+        # edges), "linear" (one stream).  Measured on MI355X (profiles/r03/graph_forms.txt):
+        # yolox_s bs32 forward 1.97 ms as lanes vs 2.27 ms as the DAG -- the runtime pays for
+        # every cross-stream edge of a many-branch graph
+        self.graph_mode = os.environ.get("YOLOX_AMD_GRAPH", "lanes")
         self.flops = ctx.flops * self.nchunks
         # ------------------------------------------------ arenas
         off = 0
@@ -505,6 +543,21 @@ class Plan:
                 t.dtype, t.cout, t.act = ctx.dcode, a["spec"].cout, a["act"]
                 t.weight = self.warena.data_ptr() + a["spec"].w_off
                 t.bias = self.barena.data_ptr() + a["spec"].b_off
+                v = a["dst"]
+                t.dst = self._ptr(v, c)
+                t.dst_cstride, t.dst_bstride = v.buf.c, v.buf.nelem_image
+                t.img = None
+                self._input_index = i
+            elif rec.kind == N.OP_STEM2:
+                t = op.u.stem2
+                t.layout = self.input_layout
+                t.img_dtype = N.DTYPE_CODE[self.input_dtype]
+                t.batch, t.h, t.w = B, a["h"], a["w"]
+                t.dtype, t.c1, t.c2, t.act = ctx.dcode, a["c1"], a["c2"], a["act"]
+                t.w1 = self.warena.data_ptr() + a["spec1"].w_off
+                t.b1 = self.barena.data_ptr() + a["spec1"].b_off
+                t.w2 = self.warena.data_ptr() + a["spec2"].w_off
+                t.b2 = self.barena.data_ptr() + a["spec2"].b_off
                 v = a["dst"]
                 t.dst = self._ptr(v, c)
                 t.dst_cstride, t.dst_bstride = v.buf.c, v.buf.nelem_image
@@ -637,6 +690,8 @@ class Plan:
             op = self._ops[c * self._nops + self._input_index]
             if op.kind == N.OP_STEM:
                 op.u.stem.img = x.data_ptr() + c * step
+            elif op.kind == N.OP_STEM2:
+                op.u.stem2.img = x.data_ptr() + c * step
             else:
                 op.u.focus.img = x.data_ptr() + c * step
         return x
@@ -690,6 +745,13 @@ class Plan:
             off, deps = self._dag_arrays()
             N.check(self.lib.yxh_graph_create_dag(self._ops, len(self._ops), off, deps, N.stream_ptr(self.device),
                                                   C.byref(g)), "graph capture (dag)")
+        elif self.graph_mode == "lanes" and self.parallel_chunks and self.nchunks <= 4:
+            # one capture stream per chunk: independent chains, joined at the end
+            lanes = [c for c in range(self.nchunks) for _ in self.ctx.ops]
+            off, deps = self._dag_arrays()
+            arr = (C.c_int32 * len(lanes))(*lanes)
+            N.check(self.lib.yxh_graph_create_lanes(self._ops, len(self._ops), arr, off, deps, self.nchunks,
+                                                    N.stream_ptr(self.device), C.byref(g)), "graph capture (chunk lanes)")
         elif self.graph_mode == "lanes" and self.use_lanes and self.nlanes > 1 and not self.parallel_chunks:
             lanes, off, deps = self._lane_arrays()
             N.check(self.lib.yxh_graph_create_lanes(self._ops, len(self._ops), lanes, off, deps, self.nlanes,

@@ -168,10 +168,13 @@ class CspDarknet(_Planned):
                                    CspLayer(bc * 16, bc * 16, n=bd, shortcut=False, depthwise=depthwise, act=act))
 
     def plan(self, ctx, packed):
-        x = self.stem.plan(ctx, packed)
+        fused = ctx.stem_s2_fusable(self.stem.conv, self.dark2[0])
+        # Focus stem + dark2[0] as one launch where the geometry allows (yxh_stem_s2)
+        x = ctx.stem_s2(self.stem.conv, self.dark2[0], packed) if fused else self.stem.plan(ctx, packed)
         feats = []
         for stage in (self.dark2, self.dark3, self.dark4, self.dark5):
-            x = stage[0].plan(ctx, [x])
+            if not (fused and stage is self.dark2):
+                x = stage[0].plan(ctx, [x])
             for blk in list(stage)[1:]:
                 x = blk.plan(ctx, [x])
             feats.append(x)

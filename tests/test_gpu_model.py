@@ -195,3 +195,25 @@ def test_graph_forms_match_single_stream_graph():
                 assert torch.equal(p.run(x).clone(), outs[0])  # eager: chunks in order, one stream
     torch.cuda.synchronize()
     assert all(torch.equal(o, outs[0]) for o in outs)
+
+
+def test_fused_stem_s2_plan_matches_unfused_plan():
+    """The planned forward with Focus stem + dark2[0] as one yxh_stem_s2 launch (uint8 NHWC
+    input, the bench / processor form) vs the same plan with the two as separate launches:
+    same decoded output within the bf16 bounds (the fused stem sums K in another order)."""
+    from yolox_amd import _native as N
+    from yolox_amd.engine import Plan
+    from yolox_amd.weights import synthetic_images
+    m = model("yolox_s", torch.bfloat16)
+    x = torch.from_numpy(synthetic_images(3, 160, 192, seed=12)).cuda()
+    fused = Plan(m, 3, 160, 192, torch.bfloat16, "cuda", N.NHWC, torch.uint8)
+    assert any(r.kind == N.OP_STEM2 for r in fused.ctx.ops)
+    unf = Plan(m, 3, 160, 192, torch.bfloat16, "cuda", N.NHWC, torch.uint8, fuse_stem_s2=False)
+    assert not any(r.kind == N.OP_STEM2 for r in unf.ctx.ops)
+    a = fused.run(x).clone()
+    b = unf.run(x).clone()
+    dp = (a[..., 4:] - b[..., 4:]).abs()
+    assert dp.max().item() < 0.1 and dp.float().quantile(0.99).item() < 0.02
+    assert (a[..., :2] - b[..., :2]).abs().max().item() < 1.0
+    fused.static_input().copy_(x)
+    assert torch.equal(fused.replay().clone(), a)

@@ -867,3 +867,62 @@ def test_head_pred_fused_level(dtype, cin, h, w, train):
     lvl = got[:, a_off:a_off + h * w]
     torch.testing.assert_close(lvl, want, rtol=1e-4, atol=1e-4)
     assert (got[:, :a_off] == -7.0).all() and (got[:, a_off + h * w:] == -7.0).all()
+
+
+@pytest.mark.parametrize("idt", [torch.uint8, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("hw", [(128, 128), (100, 68), (36, 260), (4, 8)])
+def test_stem_s2_fused_vs_reference(idt, dtype, hw):
+    """yxh_stem_s2 (Focus + stem BaseConv + dark2[0] 3x3 s2 in one launch, the stem map only
+    in LDS) vs the reference order in fp32: space-to-depth, conv, BN, SiLU, rounded to the
+    compute dtype (the map the unfused path stores), conv s2, BN, SiLU.  Partial tiles at the
+    right / bottom edges; a wider destination whose extra channels must stay untouched."""
+    n = N()
+    H, W = hw
+    img = torch.randint(0, 256, (2, 3, H, W)).float()
+    src = img.permute(0, 2, 3, 1).to(DEV, idt).contiguous()
+    c1, bn1 = make_conv(12, 32, 3, 1, seed=5)
+    c2, bn2 = make_conv(32, 64, 3, 2, seed=6)
+    f = lambda t: t.detach().float().contiguous().to(DEV)  # noqa: E731
+    args = [f(c1.weight), f(bn1.weight), f(bn1.bias), f(bn1.running_mean), f(bn1.running_var)]
+    w1 = torch.empty(32 * 6 * 32, dtype=dtype, device=DEV)
+    b1 = torch.empty(32, dtype=torch.float32, device=DEV)
+    n.check(n.lib().yxh_stem_pack(*[a.data_ptr() for a in args], float(bn1.eps), 32, n.DTYPE_CODE[dtype],
+                                  w1.data_ptr(), b1.data_ptr(), n.stream_ptr()), "stem pack")
+    w2, b2 = pack(c2, bn2, dtype)
+    oh, ow = (H // 2 - 1) // 2 + 1, (W // 2 - 1) // 2 + 1
+    cs = 80
+    dst = torch.full((2, oh, ow, cs), 7.0, dtype=dtype, device=DEV)
+    d = n.Stem2Desc()
+    d.img, d.layout, d.img_dtype, d.batch, d.h, d.w = src.data_ptr(), n.NHWC, n.DTYPE_CODE[idt], 2, H, W
+    d.dtype, d.c1, d.c2, d.act = n.DTYPE_CODE[dtype], 32, 64, n.ACT_SILU
+    d.w1, d.b1, d.w2, d.b2 = w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr()
+    d.dst, d.dst_cstride, d.dst_bstride = dst.data_ptr(), cs, oh * ow * cs
+    n.check(n.lib().yxh_stem_s2(ctypes.byref(d), n.stream_ptr()), "stem_s2")
+    torch.cuda.synchronize()
+    x = torch.cat([img[..., ::2, ::2], img[..., 1::2, ::2], img[..., ::2, 1::2], img[..., 1::2, 1::2]], 1)
+    x = x.to(idt).float()
+    s = ref_conv(x, c1, bn1, "silu").to(dtype).float()
+    want = ref_conv(s, c2, bn2, "silu")
+    got = dst.float().cpu().permute(0, 3, 1, 2)
+    assert (got[:, 64:] == 7.0).all()
+    err = (got[:, :64] - want).abs().max().item() / want.abs().max().item()
+    assert err < TOL[dtype], err
+
+
+def test_stem_s2_rejects_what_it_does_not_build():
+    n = N()
+    d = n.Stem2Desc()
+    x = torch.zeros(1, 64, 64, 3, dtype=torch.uint8, device=DEV)
+    w = torch.zeros(64 * 9 * 32, dtype=torch.bfloat16, device=DEV)
+    b = torch.zeros(64, dtype=torch.float32, device=DEV)
+    y = torch.zeros(1, 16, 16, 64, dtype=torch.bfloat16, device=DEV)
+    d.img, d.layout, d.img_dtype, d.batch, d.h, d.w = x.data_ptr(), n.NHWC, n.U8, 1, 64, 64
+    d.dtype, d.c1, d.c2, d.act = n.BF16, 32, 64, n.ACT_SILU
+    d.w1, d.b1, d.w2, d.b2, d.dst, d.dst_cstride, d.dst_bstride = (w.data_ptr(), b.data_ptr(), w.data_ptr(),
+                                                                   b.data_ptr(), y.data_ptr(), 64, 16 * 16 * 64)
+    for field, bad in (("layout", n.NCHW), ("dtype", n.F32), ("c1", 48), ("h", 66)):
+        good = getattr(d, field)
+        setattr(d, field, bad)
+        assert n.lib().yxh_stem_s2(ctypes.byref(d), n.stream_ptr()) == n.EINVAL
+        setattr(d, field, good)
