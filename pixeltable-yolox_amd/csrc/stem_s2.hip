@@ -119,7 +119,6 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
     for (int i = 0; i < FR2; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) bias2[i][r] = p.b2[wn * 32 + i * 16 + fq * 4 + r];
-    const bool silu1 = p.act1 == YXH_ACT_SILU, silu2 = p.act2 == YXH_ACT_SILU;
 
     // ---- per-lane stem K-chunk offsets (bytes from a stem pixel's base in the RGB0 patch):
     // chunk k0 = 32 s + 8 fq = kernel row k0 / 24, pixels (k0 % 24) / 4 .. +1; k0 >= 144 is
@@ -167,10 +166,19 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
             char* d = fimg + (row * kS2IXP + 4 * gc) * 8;
 #pragma unroll
             for (int px = 0; px < 4; ++px) {
-                T t4[4] = {group_elem<T, TI>(img[t], 3 * px), group_elem<T, TI>(img[t], 3 * px + 1),
-                           group_elem<T, TI>(img[t], 3 * px + 2), from_f32<T>(0.0f)};
                 uint2 u;
-                __builtin_memcpy(&u, t4, 8);
+                if constexpr (sizeof(TI) == 1 && __is_same(T, bf16)) {
+                    // integers 0..255 are exact in bf16: the f32's upper half IS the bf16 value
+                    const float r = (float)((img[t][(3 * px) >> 2] >> (8 * ((3 * px) & 3))) & 0xffu);
+                    const float g = (float)((img[t][(3 * px + 1) >> 2] >> (8 * ((3 * px + 1) & 3))) & 0xffu);
+                    const float b = (float)((img[t][(3 * px + 2) >> 2] >> (8 * ((3 * px + 2) & 3))) & 0xffu);
+                    u.x = __builtin_amdgcn_perm(__float_as_uint(g), __float_as_uint(r), 0x07060302u);
+                    u.y = __float_as_uint(b) >> 16;
+                } else {
+                    T t4[4] = {group_elem<T, TI>(img[t], 3 * px), group_elem<T, TI>(img[t], 3 * px + 1),
+                               group_elem<T, TI>(img[t], 3 * px + 2), from_f32<T>(0.0f)};
+                    __builtin_memcpy(&u, t4, 8);
+                }
                 *(uint2*)(d + px * 8) = u;
             }
         }
@@ -193,6 +201,9 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
             load_image(nc);  // lands during this tile's two GEMMs
         }
 
+        // a tile whose stem halo lies inside the stem map needs no zero-padding selects
+        const bool interior = 2 * cur.oy0 - 1 >= 0 && 2 * cur.ox0 - 1 >= 0 && 2 * cur.oy0 + 2 * kS2TY - 1 < p.OH1 &&
+                              2 * cur.ox0 + 2 * kS2TX - 1 < p.OW1;
         // ---- stem: 36 fragments of 16 stem pixels, wave w takes w, w + 4, ... (3 at a time)
 #pragma unroll
         for (int g0 = 0; g0 < kS2NF1 / 4; g0 += 3) {
@@ -216,19 +227,20 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
 #pragma unroll
                     for (int jj = 0; jj < 3; ++jj) Mma<T>::run(acc[i][jj], a1[i][s], b[jj]);
             }
+            // bias + SiLU; zeros outside the stem map (the stride-2 conv's padding)
 #pragma unroll
             for (int jj = 0; jj < 3; ++jj) {
                 const int pix = (wave + 4 * (g0 + jj)) * 16 + frow;
                 const int sy = pix / kS2SX, sx = pix - kS2SX * (pix / kS2SX);
                 const int gy = 2 * cur.oy0 - 1 + sy, gx = 2 * cur.ox0 - 1 + sx;
-                const bool valid = (unsigned)gy < (unsigned)p.OH1 && (unsigned)gx < (unsigned)p.OW1;
+                const bool valid = interior || ((unsigned)gy < (unsigned)p.OH1 && (unsigned)gx < (unsigned)p.OW1);
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     T t[4];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float x = acc[i][jj][r] + bias1[i][r];
-                        t[r] = from_f32<T>(valid ? (silu1 ? yxh::silu<false>(x) : x) : 0.0f);
+                        const float y = yxh::silu<false>(acc[i][jj][r] + bias1[i][r]);
+                        t[r] = from_f32<T>(valid ? y : 0.0f);
                     }
                     uint2 u;
                     __builtin_memcpy(&u, t, 8);
@@ -275,7 +287,7 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float x = acc2[i][j][r] + bias2[i][r];
-                    t[r] = from_f32<T>(silu2 ? yxh::silu<false>(x) : x);
+                    t[r] = from_f32<T>(yxh::silu<false>(x));
                 }
                 uint2 u;
                 __builtin_memcpy(&u, t, 8);
@@ -314,6 +326,7 @@ int stem_s2_launch(const yxh_stem2_desc* d, hipStream_t st) {
     YXH_CHECK_ARG(d && d->img && d->w1 && d->b1 && d->w2 && d->b2 && d->dst, "null pointer");
     YXH_CHECK_ARG(d->layout == YXH_NHWC, "stem_s2 reads NHWC images");
     YXH_CHECK_ARG(d->dtype == YXH_BF16 || d->dtype == YXH_F16, "stem_s2 computes in bf16/f16");
+    YXH_CHECK_ARG(d->act == YXH_ACT_SILU, "stem_s2 is built for SiLU (got act %d)", d->act);
     YXH_CHECK_ARG(d->c1 == 32 && d->c2 == 64, "stem_s2 is built for 32 stem / 64 conv channels (got %d/%d)", d->c1,
                   d->c2);
     YXH_CHECK_ARG(d->batch > 0 && d->h >= 4 && d->w >= 4 && d->h % 4 == 0 && d->w % 4 == 0, "image %dx%d", d->h,

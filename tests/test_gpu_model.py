@@ -119,7 +119,7 @@ def test_fused_stem_plan_matches_focus_plan(golden, dtype):
     d = golden("fwd_yolox_s_128.npz")
     m = model("yolox_s", dtype)
     x = torch.from_numpy(d["input_u8"]).cuda()
-    fused = Plan(m, 2, 128, 128, dtype, "cuda", N.NHWC, torch.uint8)
+    fused = Plan(m, 2, 128, 128, dtype, "cuda", N.NHWC, torch.uint8, fuse_stem_s2=False)
     split = Plan(m, 2, 128, 128, dtype, "cuda", N.NHWC, torch.uint8, fuse_stem=False)
     assert [o.kind for o in fused.ctx.ops].count(N.OP_STEM) == 1
     assert [o.kind for o in split.ctx.ops].count(N.OP_FOCUS) == 1

@@ -13,8 +13,8 @@ import json
 import sys
 from collections import defaultdict
 
-FWD_KEYS = ("conv_igemm", "conv_glds", "conv_rows", "conv_pw", "conv_r3", "conv_ws", "head_pred", "stem_conv", "stem_rows", "spp_maxpool",
-            "focus_pack", "dwconv")
+FWD_KEYS = ("conv_igemm", "conv_glds", "conv_rows", "conv_pw", "conv_r3", "conv_ws", "head_pred", "stem_conv", "stem_rows",
+            "stem_s2", "spp_maxpool", "focus_pack", "dwconv")
 
 
 def load(path):
@@ -25,7 +25,7 @@ def load(path):
             name = row["Kernel_Name"]
             if not any(k in name for k in FWD_KEYS):
                 continue
-            if "stem_conv" in name or "stem_rows" in name or "focus_pack" in name:
+            if "stem_conv" in name or "stem_rows" in name or "stem_s2" in name or "focus_pack" in name:
                 n_stem += 1
             per_kernel[name] += float(row["Counter_Value"])
     return per_kernel, n_stem
