@@ -435,7 +435,14 @@ class Plan:
     def __init__(self, model, batch: int, height: int, width: int, dtype: torch.dtype, device,
                  input_layout: int = N.NCHW, input_dtype: torch.dtype = torch.float32, train: bool = False,
                  fuse_stem: bool = True, chunk: Optional[int] = None, fuse_bottleneck: bool = _FUSE_BOTTLENECK,
-                 parallel_chunks: bool = False, fuse_stem_s2: bool = True):
+                 parallel_chunks: bool = False, fuse_stem_s2: bool = True, stage: str = "full",
+                 head_inputs: Optional[list] = None):
+        """``stage``: "full" (image -> decoded rows), "features" (image -> the three PAFPN
+        maps: YoloPafpn.forward) or "head" (three feature maps of ``head_inputs`` shapes
+        [(C, H, W)] -> decoded rows: YoloxHead.forward)."""
+        if stage not in ("full", "features", "head"):
+            raise ValueError(f"unknown plan stage {stage!r}")
+        self.stage = stage
         if height % 32 or width % 32:
             raise ValueError("input size must be multiples of 32")
         chunk = chunk or batch
@@ -450,14 +457,23 @@ class Plan:
         self.input_dtype = input_dtype
         self.dtype = dtype
         head = model.head
-        self.num_classes = head.num_classes
+        self.num_classes = head.num_classes if head is not None else 0
         ctx = PlanCtx(chunk, dtype, self.device, fuse_stem=fuse_stem, fuse_bottleneck=fuse_bottleneck,
                       fuse_stem_s2=fuse_stem_s2)
         ctx.input_layout, ctx.input_dtype = input_layout, input_dtype
-        feats = model.backbone.plan(ctx, ctx.image(height, width))
+        if stage == "head":
+            if chunk != batch or not head_inputs or len(head_inputs) != 3:
+                raise ValueError("a head plan takes three feature maps and no chunking")
+            feats = [ctx.buffer(h, w, c).full() for c, h, w in head_inputs]
+        else:
+            feats = model.backbone.plan(ctx, ctx.image(height, width))
+        self.feats = feats
         anchors = sum(f.lh * f.lw for f in feats)
         self.out_spec = OutBuffer(anchors, 5 + self.num_classes)
-        head.plan(ctx, feats, self.out_spec, train=train)
+        if stage != "features":
+            head.plan(ctx, feats, self.out_spec, train=train)
+        elif chunk != batch:
+            raise ValueError("a features plan takes no chunking")
         self.ctx = ctx
         self.anchors = anchors
         # independent head levels run as separate graph branches (YOLOX_AMD_LANES=0: one stream)
@@ -492,7 +508,8 @@ class Plan:
                 boff += _align(s.cout * 4)
         self.warena = torch.empty(max(woff, 1), dtype=torch.uint8, device=self.device)
         self.barena = torch.empty(max(boff, 1), dtype=torch.uint8, device=self.device)
-        self.output = torch.empty(batch, anchors, 5 + self.num_classes, dtype=torch.float32, device=self.device)
+        self.output = torch.empty(batch, anchors if stage != "features" else 0, 5 + self.num_classes,
+                                  dtype=torch.float32, device=self.device)
         self._input_slot: Optional[torch.Tensor] = None
         self._nops = len(ctx.ops)
         self._ops = (N.Op * (len(ctx.ops) * self.nchunks))()  # chunk c = ops [c*nops, (c+1)*nops)
@@ -720,6 +737,37 @@ class Plan:
         self._bind_output(out)
         try:
             N.check(self.lib.yxh_run_ops(self._ops, len(self._ops), N.stream_ptr(self.device)), "forward")
+        finally:
+            self._bind_output(None)
+        return out
+
+    def feature_view(self, v: View) -> torch.Tensor:
+        """An arena view as an NCHW tensor (a copy) in the compute dtype."""
+        b = v.buf
+        t = self.arena[b.offset:b.offset + self.batch * b.nelem_image * b.esize].view(self.dtype)
+        return t.view(self.batch, b.h, b.w, b.c)[..., v.coff:v.coff + v.ch].permute(0, 3, 1, 2).contiguous()
+
+    def run_features(self, x: torch.Tensor) -> tuple:
+        """stage "features": the PAFPN outputs (pan_out2, pan_out1, pan_out0), NCHW."""
+        if self.stage != "features":
+            raise RuntimeError("run_features needs a features plan")
+        self.pack_weights()
+        self._bind_input(x)
+        N.check(self.lib.yxh_run_ops(self._ops, len(self._ops), N.stream_ptr(self.device)), "backbone")
+        return tuple(self.feature_view(v) for v in self.feats)
+
+    def run_head(self, xin, out: torch.Tensor) -> torch.Tensor:
+        """stage "head": decoded [B, A, 5+C] rows of three NCHW feature maps."""
+        if self.stage != "head":
+            raise RuntimeError("run_head needs a head plan")
+        self.pack_weights()
+        for v, x in zip(self.feats, xin):
+            b = v.buf
+            dst = self.arena[b.offset:b.offset + self.batch * b.nelem_image * b.esize].view(self.dtype)
+            dst.view(self.batch, b.h, b.w, b.c).copy_(x.to(self.device).permute(0, 2, 3, 1))
+        self._bind_output(out)
+        try:
+            N.check(self.lib.yxh_run_ops(self._ops, len(self._ops), N.stream_ptr(self.device)), "head")
         finally:
             self._bind_output(None)
         return out

@@ -35,6 +35,31 @@ class _Planned(nn.Module):
             f"{type(self).__name__} is executed by the HIP plan of YoloxModule; call the YoloxModule")
 
 
+class _StageModel:
+    """What engine.Plan needs of a model (backbone / head / parameters) for a plan of one
+    submodule: YoloPafpn.forward ("features") and YoloxHead.forward ("head")."""
+
+    def __init__(self, owner: nn.Module, backbone=None, head=None):
+        self.owner, self.backbone, self.head = owner, backbone, head
+
+    def parameters(self):
+        return self.owner.parameters()
+
+    def buffers(self):
+        return self.owner.buffers()
+
+
+def _stage_plan(owner: nn.Module, key: tuple, make):
+    cache = owner.__dict__.setdefault("_stage_plans", {})
+    if key not in cache:
+        cache[key] = make()
+    return cache[key]
+
+
+def _param0(m: nn.Module) -> torch.Tensor:
+    return next(m.parameters())
+
+
 class BaseConv(_Planned):
     """Conv2d(bias=False, same padding) -> BatchNorm2d -> activation."""
 
@@ -201,6 +226,29 @@ class YoloPafpn(_Planned):
         self.bu_conv1 = Conv(c1, c1, 3, 2, act=act)
         self.C3_n4 = CspLayer(2 * c1, c2, n, False, depthwise=depthwise, act=act)
 
+    def forward(self, input):
+        """yolo_pafpn.py:83-116 standalone: [B, 3, H, W] images -> (pan_out2, pan_out1,
+        pan_out0) NCHW in the parameters' dtype, computed by a features-only HIP plan."""
+        from .. import _native as N
+        from ..engine import Plan
+        x = input
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise ValueError(f"expected [B, 3, H, W] images, got {tuple(x.shape)}")
+        p = _param0(self)
+        if p.device.type != "cuda":
+            raise RuntimeError("YoloPafpn runs on a ROCm device only; call .to('cuda') first")
+        if x.dtype not in (torch.float32, torch.bfloat16, torch.float16, torch.uint8):
+            x = x.float()
+        B, _, H, W = x.shape
+        key = ("features", B, H, W, x.dtype, p.dtype, str(p.device))
+        plan = _stage_plan(self, key, lambda: Plan(_StageModel(self, backbone=self), B, H, W, p.dtype, p.device,
+                                                   N.NCHW, x.dtype, stage="features"))
+        return plan.run_features(x)
+
+    def _apply(self, fn, *args, **kwargs):
+        self.__dict__.pop("_stage_plans", None)
+        return super()._apply(fn, *args, **kwargs)
+
     def plan(self, ctx, packed):
         """yolo_pafpn.py:83-116.  Every torch.cat is a pre-sliced buffer and every
         upsample a strided read: fpn_out0 / fpn_out1 are written straight into the
@@ -250,6 +298,35 @@ class YoloxHead(_Planned):
             self.obj_preds.append(nn.Conv2d(hw_, 1, 1, 1, 0))
         self.use_l1 = False
         self.strides = list(strides)
+
+    def forward(self, xin, labels=None, imgs=None):
+        """yolo_head.py:140-211 standalone, eval mode: three NCHW feature maps -> decoded
+        [B, A, 5+C] rows (in xin[0]'s dtype, as decode_outputs returns them), by a head-only
+        HIP plan.  The training form (losses) runs inside YoloxModule.forward."""
+        from .. import _native as N
+        from ..engine import Plan
+        if self.training:
+            raise NotImplementedError("YoloxHead.forward in training mode: call YoloxModule.forward(x, targets)")
+        if not self.decode_in_inference:
+            raise NotImplementedError("decode_in_inference=False (raw head outputs) is not planned")
+        if len(xin) != 3:
+            raise ValueError("YoloxHead takes three feature maps")
+        p = _param0(self)
+        if p.device.type != "cuda":
+            raise RuntimeError("YoloxHead runs on a ROCm device only; call .to('cuda') first")
+        B = xin[0].shape[0]
+        shapes = [tuple(int(v) for v in t.shape[1:]) for t in xin]
+        key = ("head", B, tuple(shapes), p.dtype, str(p.device))
+        owner = self
+        plan = _stage_plan(self, key, lambda: Plan(_StageModel(owner, head=owner), B, 32, 32, p.dtype, p.device,
+                                                   stage="head", head_inputs=shapes))
+        out = torch.empty(B, plan.anchors, 5 + self.num_classes, dtype=torch.float32, device=p.device)
+        plan.run_head(xin, out)
+        return out.to(xin[0].dtype)
+
+    def _apply(self, fn, *args, **kwargs):
+        self.__dict__.pop("_stage_plans", None)
+        return super()._apply(fn, *args, **kwargs)
 
     def initialize_biases(self, prior_prob: float) -> None:
         """yolo_head.py:129-138: cls/obj pred biases = -log((1 - p) / p)."""

@@ -217,3 +217,24 @@ def test_fused_stem_s2_plan_matches_unfused_plan():
     assert (a[..., :2] - b[..., :2]).abs().max().item() < 1.0
     fused.static_input().copy_(x)
     assert torch.equal(fused.replay().clone(), a)
+
+
+def test_submodules_are_callable_like_the_reference(golden):
+    """module.backbone(x) and module.head(feats) run standalone (reference YoloPafpn.forward,
+    yolo_pafpn.py:83-116; YoloxHead.forward eval, yolo_head.py:140-211): the PAFPN maps match
+    the reference fixture's, and the head over them gives the full forward bit for bit."""
+    d = golden("fwd_yolox_s_128.npz")
+    m = model("yolox_s", torch.float32)
+    x = torch.from_numpy(d["input_u8"]).permute(0, 3, 1, 2).float().cuda()
+    feats = m.backbone(x)
+    assert len(feats) == 3
+    for i, f in enumerate(feats):
+        ref = torch.from_numpy(d[f"fpn{i}"])
+        assert tuple(f.shape) == tuple(ref.shape) and f.dtype == torch.float32
+        assert (f.cpu() - ref).abs().max().item() / ref.abs().max().item() < 1e-3, i
+    out = m.head(list(feats))
+    assert torch.equal(out, m(x))
+    with pytest.raises(NotImplementedError):
+        m.train()
+        m.head(list(feats))
+    m.eval()
