@@ -486,6 +486,7 @@ class Plan:
         # yolox_s bs32 forward 1.97 ms as lanes vs 2.27 ms as the DAG -- the runtime pays for
         # every cross-stream edge of a many-branch graph
         self.graph_mode = os.environ.get("YOLOX_AMD_GRAPH", "lanes")
+        self._segments = None  # graph_mode "streams": per-segment graphs + lane streams / events
         self.flops = ctx.flops * self.nchunks
         # ------------------------------------------------ arenas
         off = 0
@@ -780,15 +781,95 @@ class Plan:
             self._input_slot = torch.zeros(shape, dtype=self.input_dtype, device=self.device)
         return self._input_slot
 
+    def _stream_segments(self):
+        """graph_mode "streams": the op list cut into graph segments per lane.  A head lane
+        k (one level, yolo_head.py:140-211) is one segment that may start as soon as the
+        neck op producing its feature map is done (its fork point); the neck / backbone
+        lane is cut at every fork point.  None when the lanes do not have that shape."""
+        ops, deps = self.ctx.ops, self._deps
+        lane = [r.lane for r in ops]
+        if max(lane) == 0:
+            return None
+        fork = {}
+        for i, r in enumerate(ops):
+            for j in deps[i]:
+                if lane[j] != lane[i]:
+                    if lane[i] == 0 or lane[j] != 0:
+                        return None  # the neck never waits for a head lane; lanes meet only via lane 0
+                    fork[lane[i]] = max(fork.get(lane[i], -1), j)
+        cuts = sorted(set(fork.values()))
+        segs, start = [], 0
+        main = [i for i in range(len(ops)) if lane[i] == 0]
+        if main != list(range(len(main))):
+            return None
+        for c in cuts + [len(main) - 1]:
+            if c >= start:
+                segs.append((0, list(range(start, c + 1)), [k for k, f in fork.items() if f == c]))
+                start = c + 1
+        lanes = {k: [i for i in range(len(ops)) if lane[i] == k] for k in fork}
+        return segs, lanes
+
+    def _capture_segment(self, idx: list, c: int):
+        n = self._nops
+        arr = (N.Op * len(idx))(*[self._ops[c * n + i] for i in idx])
+        g = C.c_void_p()
+        N.check(self.lib.yxh_graph_create(arr, len(idx), N.stream_ptr(self.device), C.byref(g)), "graph capture")
+        return g
+
+    def _capture_streams(self) -> bool:
+        shape = self._stream_segments()
+        if shape is None:
+            return False
+        segs, lanes = shape
+        plan = []
+        for c in range(self.nchunks):
+            chunk = []
+            for _, idx, forks in segs:
+                chunk.append((self._capture_segment(idx, c), [(k, self._capture_segment(lanes[k], c)) for k in forks]))
+            plan.append(chunk)
+        ks = sorted(lanes)
+        self._lane_streams = {k: torch.cuda.Stream(self.device) for k in ks}
+        self._fork_ev = {k: torch.cuda.Event() for k in ks}
+        self._done_ev = {k: torch.cuda.Event() for k in ks}
+        self._segments = plan
+        return True
+
+    def _launch_streams(self) -> None:
+        main = torch.cuda.current_stream(self.device)
+        mp = main.cuda_stream
+        for chunk in self._segments:
+            for g, forks in chunk:
+                N.check(self.lib.yxh_graph_launch(g, mp), "graph replay")
+                for k, gk in forks:
+                    s = self._lane_streams[k]
+                    self._fork_ev[k].record(main)
+                    s.wait_event(self._fork_ev[k])
+                    N.check(self.lib.yxh_graph_launch(gk, s.cuda_stream), "graph replay (lane)")
+                    self._done_ev[k].record(s)
+            for k in self._lane_streams:  # join: outputs ready / arena free on the caller's stream
+                main.wait_event(self._done_ev[k])
+
+    def _destroy_graphs(self) -> None:
+        if self._graph is not None:
+            N.check(self.lib.yxh_graph_destroy(self._graph))
+            self._graph = None
+        if self._segments is not None:
+            for chunk in self._segments:
+                for g, forks in chunk:
+                    self.lib.yxh_graph_destroy(g)
+                    for _, gk in forks:
+                        self.lib.yxh_graph_destroy(gk)
+            self._segments = None
+
     def capture(self) -> None:
         """Capture the whole forward into a hipGraph reading ``static_input()``."""
         self.pack_weights()
         self._bind_input(self.static_input())
-        if self._graph is not None:
-            N.check(self.lib.yxh_graph_destroy(self._graph))
-            self._graph = None
+        self._destroy_graphs()
         g = C.c_void_p()
         torch.cuda.synchronize(self.device)
+        if self.graph_mode == "streams" and not self.parallel_chunks and self._capture_streams():
+            return
         if self.graph_mode == "dag":
             off, deps = self._dag_arrays()
             N.check(self.lib.yxh_graph_create_dag(self._ops, len(self._ops), off, deps, N.stream_ptr(self.device),
@@ -857,18 +938,19 @@ class Plan:
         ``run()`` (the eager API path) compares every parameter's version instead."""
         if self._packed_epoch != self._epoch():
             self.pack_weights()
-        if self._graph is None:
+        if self._graph is None and self._segments is None:
             self.capture()
-        N.check(self.lib.yxh_graph_launch(self._graph, N.stream_ptr(self.device)), "graph replay")
+        if self._segments is not None:
+            self._launch_streams()
+        else:
+            N.check(self.lib.yxh_graph_launch(self._graph, N.stream_ptr(self.device)), "graph replay")
         return self.output
 
     def __del__(self):
-        g = getattr(self, "_graph", None)
-        if g is not None:
-            try:
-                self.lib.yxh_graph_destroy(g)
-            except Exception:
-                pass
+        try:
+            self._destroy_graphs()
+        except Exception:
+            pass
 
     # -------------------------------------------------------------- autotune
     def autotune(self, reps: int = 5, verbose: bool = False) -> dict:
@@ -920,7 +1002,7 @@ class Plan:
             for i, t in chosen.items():
                 self._ops[c * self._nops + i].u.conv.tile = t
         torch.cuda.synchronize(self.device)
-        if self._graph is not None:  # a captured graph holds the old tiles
+        if self._graph is not None or self._segments is not None:  # captured graphs hold the old tiles
             self.capture()
         return chosen
 

@@ -174,7 +174,8 @@ def test_chunked_plan_matches_whole_batch():
 
 def test_graph_forms_match_single_stream_graph():
     """The captured forms of one plan -- the dataflow DAG (one node per op; head levels
-    concurrent), lanes (head levels on capture streams) and one stream -- give the same
+    concurrent), lanes (head levels on capture streams), streams (per-lane graph segments on
+    streams of their own, forked at the neck op each level needs) and one stream -- give the same
     output bit for bit, chunked with a shared arena and with parallel chunks (arenas of
     their own, the chunks side by side), replayed twice each."""
     from yolox_amd import _native as N
@@ -184,7 +185,7 @@ def test_graph_forms_match_single_stream_graph():
     x = torch.from_numpy(synthetic_images(4, 160, 160, seed=4)).cuda()
     outs = []
     for par in (False, True):
-        for mode in ("dag", "lanes", "linear"):
+        for mode in ("dag", "lanes", "linear", "streams"):
             p = Plan(m, 4, 160, 160, torch.bfloat16, "cuda", N.NHWC, torch.uint8, chunk=2, parallel_chunks=par)
             assert p.nlanes == 4 and p.parallel_chunks == par
             p.graph_mode = mode
