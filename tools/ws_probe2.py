@@ -31,7 +31,17 @@ for spec in sys.argv[1:]:
     d.weight, d.bias = w.data_ptr(), b.data_ptr()
     d.dst, d.dst_dtype, d.dst_cstride, d.dst_bstride = y.data_ptr(), N.BF16, Nc, Ho * Ho * Nc
     d.act, d.tile = N.ACT_SILU, tile
+    d.tile = 12  # conv_igemm reference output
     assert L.yxh_conv2d(C.byref(d), st) == N.OK
+    torch.cuda.synchronize()
+    ref = y.float().clone()
+    y.zero_()
+    d.tile = tile
+    if L.yxh_conv2d(C.byref(d), st) != N.OK:
+        print(f"{tag} s{S} {H} {K}->{Nc} tile {tile >> 1}: not applicable", flush=True)
+        continue
+    torch.cuda.synchronize()
+    err = float((y.float() - ref).abs().max() / ref.abs().max())
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(20):
@@ -39,5 +49,5 @@ for spec in sys.argv[1:]:
     e.record()
     e.synchronize()
     t = s.elapsed_time(e) / 20 * 1e3
-    print(f"{tag} s{S} {H} {K}->{Nc} tile {tile >> 1}: {t:.1f} us {2.0 * B * Ho * Ho * Nc * 9 * K / t / 1e6:.0f} TF",
-          flush=True)
+    print(f"{tag} s{S} {H} {K}->{Nc} tile {tile >> 1}: {t:.1f} us {2.0 * B * Ho * Ho * Nc * 9 * K / t / 1e6:.0f} TF"
+          f" err {err:.1e}", flush=True)

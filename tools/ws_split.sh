@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/../pixeltable-yolox_amd"
 mkdir -p ../dbg
 FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -I../include -Icsrc -mcode-object-version=5"
-OBJS=$(ls build/*.o | grep -v conv_ws)
+OBJS=$(ls build/*.o | grep -v "conv_ws.hip.o")
 for P in 1 2 3; do
   /opt/rocm/bin/hipcc $FLAGS -DYXH_WS_PROBE=$P -c csrc/conv_ws.hip -o ../dbg/conv_ws_p$P.o &
 done
