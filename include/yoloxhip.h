@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 10
+#define YXH_ABI_VERSION 11
 
 enum yxh_status {
     YXH_OK = 0,
@@ -224,6 +224,43 @@ typedef struct {
 enum yxh_lb_format { YXH_LB_F32_NCHW = 0, YXH_LB_U8_NHWC = 1, YXH_LB_BF16_NHWC = 2 };
 int yxh_letterbox_batch(const uint8_t* pool, const yxh_lb_image* images, int32_t batch, int32_t dst_h,
                         int32_t dst_w, int32_t out_format, void* dst, void* stream);
+
+/*
+ * yxh_augment_batch: the training-time sample pipeline for a whole batch on device, replacing
+ * MosaicDetection.__getitem__ + mixup (datasets/mosaicdetection.py:76-232) and TrainTransform's
+ * image half (data_augment.py:19-30 augment_hsv, :112-138 random_affine / _mirror, :140-156
+ * preproc, :159-208) that the reference runs per image in DataLoader workers.  `pool`: device
+ * bytes holding the dataset's pull_item images (uint8 HWC BGR, cv2.imread order); `images`
+ * (device, one per sample): the parameters the host drew in the reference's random order and
+ * the geometry derived from them (yolox_amd/data/mosaic.py packs them).  Output `out`: float32
+ * [B][3][h][w] (TrainTransform's tensor); `mosaic_ws`: >= B*h*w*3 bytes of scratch (the warped
+ * mosaic).  Labels stay on the host (numpy, as the reference computes them).  cv2's resize /
+ * warpAffine / 8-bit HSV conversions are restated in fixed point (csrc/augment.hip).
+ */
+typedef struct {
+    int32_t mosaic;   /* 1: mosaic + affine (+ mixup); 0: TrainTransform's letterbox of source 0 */
+    int32_t mix;      /* mixup applied */
+    int32_t flip;     /* _mirror applied */
+    int32_t do_hsv;   /* augment_hsv applied */
+    int32_t hsv[3];   /* augment_hsv's int16 gains (hue, saturation, value) */
+    int32_t cp_flip;  /* mixup's FLIP */
+    int64_t src_off[4];                      /* pool byte offset of each mosaic source */
+    int32_t src_h[4], src_w[4];              /* source size */
+    int32_t rh[4], rw[4];                    /* resized size: int(h0 * scale), int(w0 * scale) */
+    double rsx[4], rsy[4];                   /* cv2 scale_x / scale_y = src / resized */
+    int32_t lx1[4], ly1[4], lx2[4], ly2[4];  /* placement in the 2h x 2w canvas */
+    int32_t sx1[4], sy1[4];                  /* crop origin inside the resized source */
+    double minv[6];                          /* cv2.invertAffineTransform(M): output -> canvas */
+    int64_t cp_off;                          /* mixup source (pool offset and size) */
+    int32_t cp_h, cp_w, cp_rh, cp_rw;        /* ... and its letterbox size inside h x w */
+    double cp_sx, cp_sy;
+    int32_t jit_h, jit_w;                    /* jitter-resized letterbox canvas size */
+    double jit_sx, jit_sy;
+    int32_t x_off, y_off;                    /* crop offsets into the zero-padded copy */
+} yxh_aug_image;
+int yxh_augment_batch(const uint8_t* pool, const yxh_aug_image* images, int32_t batch, int32_t h, int32_t w,
+                      uint8_t* mosaic_ws, float* out, void* stream);
+size_t yxh_sizeof_aug_image(void);
 
 /*
  * yxh_postprocess: utils.postprocess (utils/boxes.py:31-75) with torchvision

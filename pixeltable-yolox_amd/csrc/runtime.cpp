@@ -67,6 +67,8 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
                 float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t filter_done);
 int head_pred_launch(const yxh_head_desc* d, hipStream_t st);
 int stem_s2_launch(const yxh_stem2_desc* d, hipStream_t st);
+int augment_batch_launch(const uint8_t* pool, const yxh_aug_image* images, int B, int H, int W, uint8_t* mosaic_ws,
+                         float* out, hipStream_t st);
 
 static int run_op(const yxh_op& op, hipStream_t st) {
     switch (op.kind) {
@@ -139,6 +141,13 @@ int yxh_letterbox_batch(const uint8_t* pool, const yxh_lb_image* images, int32_t
                         int32_t dst_w, int32_t out_format, void* dst, void* stream) {
     return letterbox_batch_launch(pool, images, batch, dst_h, dst_w, out_format, dst, (hipStream_t)stream);
 }
+
+int yxh_augment_batch(const uint8_t* pool, const yxh_aug_image* images, int32_t batch, int32_t h, int32_t w,
+                      uint8_t* mosaic_ws, float* out, void* stream) {
+    return augment_batch_launch(pool, images, batch, h, w, mosaic_ws, out, (hipStream_t)stream);
+}
+
+size_t yxh_sizeof_aug_image(void) { return sizeof(yxh_aug_image); }
 
 size_t yxh_postprocess_workspace_bytes(int32_t batch, int32_t anchors) { return pp_workspace(batch, anchors); }
 

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -109,6 +109,19 @@ class Stem2Desc(C.Structure):
                 ("dst", C.c_void_p), ("dst_cstride", C.c_int32), ("reserved", C.c_int32), ("dst_bstride", C.c_int64)]
 
 
+class AugImage(C.Structure):
+    """yxh_aug_image (include/yoloxhip.h): one training sample's drawn augmentation."""
+    _fields_ = [("mosaic", C.c_int32), ("mix", C.c_int32), ("flip", C.c_int32), ("do_hsv", C.c_int32),
+                ("hsv", C.c_int32 * 3), ("cp_flip", C.c_int32), ("src_off", C.c_int64 * 4),
+                ("src_h", C.c_int32 * 4), ("src_w", C.c_int32 * 4), ("rh", C.c_int32 * 4), ("rw", C.c_int32 * 4),
+                ("rsx", C.c_double * 4), ("rsy", C.c_double * 4), ("lx1", C.c_int32 * 4), ("ly1", C.c_int32 * 4),
+                ("lx2", C.c_int32 * 4), ("ly2", C.c_int32 * 4), ("sx1", C.c_int32 * 4), ("sy1", C.c_int32 * 4),
+                ("minv", C.c_double * 6), ("cp_off", C.c_int64), ("cp_h", C.c_int32), ("cp_w", C.c_int32),
+                ("cp_rh", C.c_int32), ("cp_rw", C.c_int32), ("cp_sx", C.c_double), ("cp_sy", C.c_double),
+                ("jit_h", C.c_int32), ("jit_w", C.c_int32), ("jit_sx", C.c_double), ("jit_sy", C.c_double),
+                ("x_off", C.c_int32), ("y_off", C.c_int32)]
+
+
 class HeadDesc(C.Structure):
     _fields_ = [("dtype", C.c_int32), ("batch", C.c_int32), ("h", C.c_int32), ("w", C.c_int32), ("cin", C.c_int32),
                 ("num_classes", C.c_int32), ("reg", Src), ("cls", Src), ("w_reg", C.c_void_p), ("b_reg", C.c_void_p),
@@ -163,6 +176,8 @@ def lib():
             "yxh_fold_bn_pack": ([vp, vp, vp, vp, vp, vp, f32, i32, i32, i32, i32, i32, i32, vp, vp, vp],
                                  C.c_int),
             "yxh_letterbox_batch": ([vp, vp, i32, i32, i32, i32, vp, vp], C.c_int),
+            "yxh_augment_batch": ([vp, vp, i32, i32, i32, vp, vp, vp], C.c_int),
+            "yxh_sizeof_aug_image": ([], sz),
             "yxh_postprocess_workspace_bytes": ([i32, i32], sz),
             "yxh_set_nms_mask_budget": ([sz], None),
             "yxh_postprocess": ([vp, i32, i32, i32, f32, f64, i32, i64, vp, vp, vp, sz, vp], C.c_int),
@@ -204,14 +219,15 @@ def lib():
             fn.restype = res
         if L.yxh_abi_version() != ABI_VERSION:
             raise NativeError(f"ABI mismatch: library {L.yxh_abi_version()} vs binding {ABI_VERSION}")
-        if L.yxh_sizeof_op() != C.sizeof(Op) or L.yxh_sizeof_conv_desc() != C.sizeof(ConvDesc):
+        if (L.yxh_sizeof_op() != C.sizeof(Op) or L.yxh_sizeof_conv_desc() != C.sizeof(ConvDesc)
+                or L.yxh_sizeof_aug_image() != C.sizeof(AugImage)):
             raise NativeError("struct layout mismatch between yoloxhip.h and _native.py")
         _lib = L
     return _lib
 
 
 EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d", "yxh_head_pred",
-            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_s2", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_postprocess_workspace_bytes", "yxh_set_nms_mask_budget",
+            "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_s2", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_augment_batch", "yxh_sizeof_aug_image", "yxh_postprocess_workspace_bytes", "yxh_set_nms_mask_budget",
             "yxh_postprocess", "yxh_postprocess_ev", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes", "yxh_graph_create_dag",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
             "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_spp_bwd",

@@ -470,6 +470,99 @@ def gen_processor_tiny(ref) -> None:
     save("processor_yolox_tiny_416.npz", **arrays)
 
 
+MOSAIC_HW = (64, 96)
+# (h, w) of the fixture's pull_item images: exact copies, 2x up, exact 2x down (INTER_AREA), odd
+# bilinear factors in both directions, tall and wide
+MOSAIC_SHAPES = [(64, 96), (32, 48), (128, 192), (50, 70), (200, 90), (41, 96), (64, 33), (97, 131), (20, 150),
+                 (64, 96)]
+MOSAIC_CASES = {  # name -> MosaicDetection kwargs (config.py defaults; the nano preset; close_mosaic)
+    "default": dict(mosaic=True, mosaic_scale=(0.1, 2), mixup_scale=(0.5, 1.5), enable_mixup=True,
+                    mosaic_prob=1.0, mixup_prob=1.0),
+    "nano": dict(mosaic=True, mosaic_scale=(0.5, 1.5), mixup_scale=(0.5, 1.5), enable_mixup=False,
+                 mosaic_prob=0.5, mixup_prob=1.0),
+    "no_aug": dict(mosaic=False, mosaic_scale=(0.1, 2), mixup_scale=(0.5, 1.5), enable_mixup=True,
+                   mosaic_prob=1.0, mixup_prob=1.0),
+}
+MOSAIC_SEEDS = 12
+
+
+def mosaic_dataset():
+    """Fixture dataset: seeded BGR images of MOSAIC_SHAPES with structured content and 0-5
+    boxes (x1, y1, x2, y2, cls) each (image 3 has none)."""
+    rng = np.random.default_rng(77)
+    images, labels = [], []
+    for i, (h, w) in enumerate(MOSAIC_SHAPES):
+        yy, xx = np.mgrid[0:h, 0:w]
+        img = np.stack([xx * 255 // max(w - 1, 1), yy * 255 // max(h - 1, 1), (xx * yy) % 256], -1)
+        img = (img + rng.integers(-30, 31, (h, w, 3))).clip(0, 255).astype(np.uint8)
+        n = 0 if i == 3 else int(rng.integers(1, 6))
+        lab = np.zeros((n, 5))
+        for k in range(n):
+            bw, bh = rng.uniform(1.5, w), rng.uniform(1.5, h)
+            x1, y1 = rng.uniform(0, w - bw), rng.uniform(0, h - bh)
+            lab[k] = (x1, y1, x1 + bw, y1 + bh, int(rng.integers(0, 80)))
+            img[int(y1):int(y1 + bh), int(x1):int(x1 + bw)] = rng.integers(0, 256, 3)
+        images.append(img)
+        labels.append(lab)
+    return images, labels
+
+
+def gen_mosaic(ref) -> None:
+    """The reference's own MosaicDetection.__getitem__ / mixup / TrainTransform(max_labels=120)
+    (mosaicdetection.py:76-232, data_augment.py:19-208) over mosaic_dataset(), with the oracle's
+    cv2 restatement (oracle/augment_oracle.py) in place of cv2: pins the random-draw order, the
+    label arithmetic and the image-operation order; pixel values of cv2's kernels stay pinned only
+    to the restatement.  Each sample seeds random / np.random with its seed first."""
+    import random as pyrandom
+
+    sys.path.insert(0, REPO)
+    from oracle import augment_oracle as A
+    cv2 = sys.modules["cv2"]
+    for k in ("INTER_LINEAR", "COLOR_BGR2HSV", "COLOR_HSV2BGR", "resize", "warpAffine", "cvtColor",
+              "getRotationMatrix2D"):
+        setattr(cv2, k, getattr(A.CV2, k))
+    utils = sys.modules["yolox.utils"]
+    utils.adjust_box_anns = ref.boxes.adjust_box_anns
+    utils.get_local_rank = lambda: 0
+    wrapper = _exec("yolox.data.datasets.datasets_wrapper", "data/datasets/datasets_wrapper.py")
+    mosaic = _exec("yolox.data.datasets.mosaicdetection", "data/datasets/mosaicdetection.py")
+    images, labels = mosaic_dataset()
+
+    class FixtureDataset(wrapper.Dataset):
+        def __init__(self):
+            super().__init__(MOSAIC_HW)
+
+        def __len__(self):
+            return len(images)
+
+        def load_anno(self, i):
+            return labels[i]
+
+        def pull_item(self, i):
+            return images[i].copy(), labels[i].copy(), images[i].shape[:2], np.array([i])
+
+    arrays = {"input_hw": np.array(MOSAIC_HW, np.int64), "shapes": np.array(MOSAIC_SHAPES, np.int64),
+              "pixels": np.concatenate([im.reshape(-1) for im in images]),
+              "label_counts": np.array([len(l) for l in labels], np.int64),
+              "labels": np.concatenate(labels, 0).astype(np.float64)}
+    for case, kw in MOSAIC_CASES.items():
+        ds = mosaic.MosaicDetection(FixtureDataset(), MOSAIC_HW,
+                                    preproc=ref.augment.TrainTransform(max_labels=120, flip_prob=0.5, hsv_prob=1.0),
+                                    degrees=10.0, translate=0.1, shear=2.0, **kw)
+        for s in range(MOSAIC_SEEDS):
+            idx = s % len(images)
+            pyrandom.seed(1000 + s)
+            np.random.seed(1000 + s)
+            img, lab, info, img_id = ds[idx]
+            assert img.dtype == np.float32 and np.all(img == np.round(img)), "image not integral"
+            arrays[f"{case}.{s}.image"] = img.astype(np.uint8)
+            arrays[f"{case}.{s}.labels"] = lab
+            arrays[f"{case}.{s}.info"] = np.array(info, np.int64)
+            arrays[f"{case}.{s}.id"] = np.array(img_id, np.int64).reshape(-1)
+        print(f"mosaic {case}: {MOSAIC_SEEDS} samples")
+    save("mosaic_aug.npz", **arrays)
+
+
 def main() -> None:
     if not os.path.isdir(REF):
         sys.exit("reference not present: fixtures can only be generated in the build container")

@@ -1,0 +1,135 @@
+"""CPU tests of the training augmentation pipeline (§8(f)-4): the host half of
+yolox_amd.data.mosaic (random draws in the reference's order + label arithmetic) and the
+oracle's image composition (oracle/augment_oracle.py) against tests/golden/mosaic_aug.npz --
+samples produced by the reference's own MosaicDetection.__getitem__ / mixup / TrainTransform
+with the oracle's cv2 restatement substituted for cv2 (parity vs cv2's pixels is unpinned:
+cv2 is absent).  The device kernels are checked against the same fixture in
+test_gpu_augment.py."""
+import random
+
+import numpy as np
+import pytest
+
+from augment_common import CASES, SEEDS, ArrayDataset, load_fixture
+from oracle import augment_oracle as A
+from yolox_amd.data import mosaic as M
+
+
+@pytest.fixture(scope="module")
+def fixture():
+    return load_fixture()
+
+
+def _dataset(fixture, case):
+    g, images, labels = fixture
+    ds = ArrayDataset(images, labels)
+    res = M.ResidentImages(ds, device="cpu")
+    H, W = (int(v) for v in g["input_hw"])
+    return M.GpuMosaicDetection(ds, (H, W), preproc=M.TrainTransform(max_labels=120), resident=res,
+                                **CASES[case]), images, H, W
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_draws_and_labels_match_reference(fixture, case):
+    g = fixture[0]
+    ds, _, _, _ = _dataset(fixture, case)
+    for s in range(SEEDS):
+        random.seed(1000 + s)
+        np.random.seed(1000 + s)
+        _, lab = ds.draw(s % len(ds))
+        np.testing.assert_array_equal(lab, g[f"{case}.{s}.labels"], err_msg=f"{case} seed {s}")
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_oracle_render_matches_reference(fixture, case):
+    g = fixture[0]
+    ds, images, H, W = _dataset(fixture, case)
+    kinds = set()
+    for s in range(SEEDS):
+        random.seed(1000 + s)
+        np.random.seed(1000 + s)
+        p, _ = ds.draw(s % len(ds))
+        kinds.add((p.mosaic, p.mix, p.flip, p.do_hsv))
+        img = A.render(p, images, H, W)
+        np.testing.assert_array_equal(img.astype(np.uint8), g[f"{case}.{s}.image"], err_msg=f"{case} seed {s}")
+    assert len(kinds) >= 2  # the seeds exercise more than one branch
+
+
+def test_fixture_covers_branches(fixture):
+    """The fixture exercises mosaic + mixup, mosaic without mixup, the letterbox path, both
+    mirror states, HSV on/off and the empty-label image."""
+    seen = set()
+    for case in CASES:
+        ds, _, _, _ = _dataset(fixture, case)
+        for s in range(SEEDS):
+            random.seed(1000 + s)
+            np.random.seed(1000 + s)
+            p, lab = ds.draw(s % len(ds))
+            seen |= {("mosaic", p.mosaic), ("mix", p.mix), ("flip", p.flip), ("hsv", p.do_hsv),
+                     ("empty", not lab.any())}
+    for k in ("mosaic", "mix", "flip", "hsv"):
+        assert (k, True) in seen and (k, False) in seen, k
+    assert ("empty", True) in seen
+
+
+def test_getitem_index_pair_sets_mosaic(fixture):
+    """mosaic_getitem (datasets_wrapper.py:98-122): an (enable_mosaic, index) pair switches mosaic."""
+    ds, _, _, _ = _dataset(fixture, "default")
+    ds.enable_mosaic = True
+    with pytest.raises(ValueError):  # rendering needs the device pool: no CPU image path
+        ds[(False, 0)]
+    assert ds.enable_mosaic is False
+
+
+# ----------------------------------------------------------------- cv2 restatement properties
+def test_resize_paths():
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, (20, 30, 3), dtype=np.uint8)
+    np.testing.assert_array_equal(A.resize(img, (30, 20)), img)  # same size: copy
+    half = A.resize(img, (15, 10))  # exact 2x down: INTER_AREA mean with rounding
+    exp = ((img[0::2, 0::2].astype(int) + img[0::2, 1::2] + img[1::2, 0::2] + img[1::2, 1::2] + 2) >> 2)
+    np.testing.assert_array_equal(half, exp.astype(np.uint8))
+    flat = np.full((7, 9, 3), 77, np.uint8)
+    np.testing.assert_array_equal(A.resize(flat, (23, 11)), np.full((11, 23, 3), 77, np.uint8))
+
+
+def test_warp_affine_identity_and_shift():
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, (12, 17, 3), dtype=np.uint8)
+    eye = np.array([[1.0, 0, 0], [0, 1.0, 0]])
+    np.testing.assert_array_equal(A.warpAffine(img, eye, (17, 12)), img)
+    shift = np.array([[1.0, 0, 3], [0, 1.0, -2]])  # integer translation: shifted copy, border 114
+    out = A.warpAffine(img, shift, (17, 12))
+    np.testing.assert_array_equal(out[:10, 3:], img[2:, :14])
+    assert (out[:, :3] == 114).all() and (out[10:] == 114).all()
+
+
+def test_hsv_known_colours():
+    bgr = np.array([[[0, 0, 255], [0, 255, 0], [255, 0, 0], [255, 255, 255], [0, 0, 0], [128, 128, 128]]],
+                   np.uint8)
+    hsv = A.bgr2hsv(bgr)
+    np.testing.assert_array_equal(hsv[0], [[0, 255, 255], [60, 255, 255], [120, 255, 255], [0, 0, 255], [0, 0, 0],
+                                           [0, 0, 128]])
+    np.testing.assert_array_equal(A.hsv2bgr(hsv), bgr)
+    np.testing.assert_array_equal(A.apply_hsv(bgr, (0, 0, 0)), bgr)  # zero gains: exact for these
+
+
+def test_hsv_roundtrip_close():
+    """8-bit HSV round trip is lossy in cv2 too; it stays within a few levels."""
+    rng = np.random.default_rng(2)
+    img = rng.integers(0, 256, (32, 32, 3), dtype=np.uint8)
+    back = A.hsv2bgr(A.bgr2hsv(img))
+    assert np.abs(back.astype(int) - img).max() <= 6
+
+
+def test_synthetic_detection_dataset():
+    ds = M.SyntheticDetectionDataset(16, (96, 128), seed=3)
+    shapes = set()
+    for i in range(len(ds)):
+        img, lab, info, img_id = ds.pull_item(i)
+        assert img.dtype == np.uint8 and img.shape[2] == 3
+        assert img.shape[0] <= 96 and img.shape[1] <= 128
+        assert lab.shape[1] == 5 and (lab[:, 2] > lab[:, 0]).all() and (lab[:, 3] > lab[:, 1]).all()
+        np.testing.assert_array_equal(ds.load_anno(i), lab)
+        shapes.add(img.shape)
+    assert len(shapes) > 4
