@@ -10,7 +10,9 @@
 //  * wave w computes pixel fragment w (16 pixels) x every output-channel fragment
 //    (1 reg/obj + ceil(C/16) cls) on MFMA 16x16x32 -- no block-diagonal zero work;
 //  * bias + decode in registers: ch 0-1 (v + grid) * stride, ch 2-3 exp(v) * stride,
-//    ch 4.. sigmoid (IEEE expf / divide, as the fp32 path of conv_common.hpp);
+//    ch 4.. sigmoid -- hardware exp2 + reciprocal (hd_exp / hd_sigmoid, ~1 ulp each), NOT
+//    the IEEE expf / divide of conv_common.hpp's fp32 decode path (test_gpu_ops.py
+//    test_head_pred_fused_level: vs torch fp32 exp / sigmoid within 1e-4 abs + rel);
 //  * the decoded [64][5+C] tile is staged in LDS and leaves as 16-byte stores over the
 //    contiguous output rows (a level's rows of one image are consecutive; a tile
 //    straddles at most one image boundary) -- instead of 4-byte scattered stores of
