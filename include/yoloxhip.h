@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 11
+#define YXH_ABI_VERSION 12
 
 enum yxh_status {
     YXH_OK = 0,
@@ -376,6 +376,32 @@ int yxh_conv_wgrad(const yxh_wgrad_desc* d, void* stream);
  */
 int yxh_pack_dgrad_weight(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, int32_t c_begin,
                           int32_t c_count, int32_t cout_pad, int32_t dtype, void* out, void* stream);
+
+/*
+ * yxh_pack_weights_batch: every weight repack of one training step in ONE launch (the
+ * optimizer rewrites conv.weight each step, core/trainer.py:109-115, so the packed
+ * forward / data-gradient layouts are rebuilt before the next forward).  jobs: a DEVICE
+ * array of njobs descriptors, ordered by block0 (the job's first block of 256 elements;
+ * block0 + ceil(elements / 256) is the next job's block0, total_blocks after the last).
+ *   kind YXH_PACK_FWD  : yxh_fold_bn_pack without BN: [cout][kh][kw][pad] (pad = cin_pad >=
+ *                        cin, zeros beyond cin) + bias_out[cout] = conv bias or 0 (bias_out
+ *                        may be NULL)
+ *   kind YXH_PACK_DGRAD: yxh_pack_dgrad_weight for input channels [c_begin, c_begin +
+ *                        c_count): [c_count][kh][kw][pad] (pad = cout_pad), taps flipped
+ * Results are bit-identical to the per-conv entry points.
+ */
+#define YXH_PACK_FWD 0
+#define YXH_PACK_DGRAD 1
+typedef struct {
+    const float* w;    /* [cout][cin][kh][kw] fp32 */
+    const float* cb;   /* conv bias [cout] or NULL (FWD) */
+    void* out;         /* packed weights, `dtype` */
+    float* bias_out;   /* FWD: [cout] or NULL */
+    int32_t kind, cout, cin, kh, kw, pad, c_begin, c_count;
+    int32_t block0, reserved;
+} yxh_pack_job;
+int yxh_pack_weights_batch(const yxh_pack_job* jobs, int32_t njobs, int32_t total_blocks, int32_t dtype,
+                           void* stream);
 
 /*
  * yxh_spp_bwd: SPPBottleneck concat + max_pool2d(5, 9, 13) backward

@@ -56,6 +56,7 @@ int conv_wgrad_launch(const yxh_wgrad_desc* d, hipStream_t st);
 int pack_dgrad_launch(const float* w, int cout, int cin, int kh, int kw, int c_begin, int c_count, int cout_pad, int dt,
                       void* out, hipStream_t st);
 int spp_bwd_launch(int dt, int B, const yxh_src* cat, int c, const float* dcat, float* dx, hipStream_t st);
+int pack_batch_launch(const yxh_pack_job* jobs, int njobs, int total_blocks, int dt, hipStream_t st);
 int upsample_bwd_launch(const float* g, int B, int h, int w, int C, float* dst, hipStream_t st);
 int head_decode_train_launch(const float* raw, int B, int A, int C, const int* lhw, const int* strides, int nlev,
                              float* out, hipStream_t st);
@@ -210,6 +211,11 @@ int yxh_conv_wgrad(const yxh_wgrad_desc* d, void* stream) { return conv_wgrad_la
 int yxh_pack_dgrad_weight(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, int32_t c_begin,
                           int32_t c_count, int32_t cout_pad, int32_t dtype, void* out, void* stream) {
     return pack_dgrad_launch(w, cout, cin, kh, kw, c_begin, c_count, cout_pad, dtype, out, (hipStream_t)stream);
+}
+
+int yxh_pack_weights_batch(const yxh_pack_job* jobs, int32_t njobs, int32_t total_blocks, int32_t dtype,
+                           void* stream) {
+    return pack_batch_launch(jobs, njobs, total_blocks, dtype, (hipStream_t)stream);
 }
 
 int yxh_spp_bwd(int32_t dtype, int32_t batch, const yxh_src* cat, int32_t c, const float* dcat, float* dx,

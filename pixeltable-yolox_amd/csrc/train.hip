@@ -958,6 +958,44 @@ __global__ __launch_bounds__(256) void pack_dgrad(const float* w, int cout, int 
     out[idx] = from_f32<T>(v);
 }
 
+// Every repack of a training step in one launch: block b belongs to the last job whose
+// block0 <= b (binary search over the job table, which stays in L2); element order and
+// values as fold_bn_pack without BN (kind FWD) and pack_dgrad (kind DGRAD).
+template <typename T>
+__global__ __launch_bounds__(256) void pack_batch(const yxh_pack_job* jobs, int njobs) {
+    const int b = blockIdx.x;
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (jobs[mid].block0 <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    const yxh_pack_job& j = jobs[lo];
+    const long long idx = (long long)(b - j.block0) * 256 + threadIdx.x;
+    const int taps = j.kh * j.kw;
+    if (j.kind == YXH_PACK_FWD) {
+        const long long total = (long long)j.cout * taps * j.pad;
+        if (idx >= total) return;
+        const int c = (int)(idx % j.pad);
+        const int t = (int)((idx / j.pad) % taps);
+        const int n = (int)(idx / ((long long)j.pad * taps));
+        const int ky = t / j.kw, kx = t - ky * j.kw;
+        const float v = c < j.cin ? j.w[(((long long)n * j.cin + c) * j.kh + ky) * j.kw + kx] : 0.0f;
+        ((T*)j.out)[idx] = from_f32<T>(v);
+        if (t == 0 && c == 0 && j.bias_out) j.bias_out[n] = j.cb ? j.cb[n] : 0.0f;
+    } else {
+        const long long total = (long long)j.c_count * taps * j.pad;
+        if (idx >= total) return;
+        const int n = (int)(idx % j.pad);
+        const int t = (int)((idx / j.pad) % taps);
+        const int c = (int)(idx / ((long long)j.pad * taps));
+        const int ky = t / j.kw, kx = t - ky * j.kw;
+        float v = 0.0f;
+        if (n < j.cout) v = j.w[(((long long)n * j.cin + j.c_begin + c) * j.kh + (j.kh - 1 - ky)) * j.kw + (j.kw - 1 - kx)];
+        ((T*)j.out)[idx] = from_f32<T>(v);
+    }
+}
+
 // ------------------------------------------------------------------ SPP / upsample backward
 // Block = (kSppCpb channels, image): the plane lives in LDS.  Per pool radius r (2, 4, 6):
 // horizontal pass -> first max column of each row window; vertical pass -> first max
@@ -1393,6 +1431,19 @@ int pack_dgrad_launch(const float* w, int cout, int cin, int kh, int kw, int c_b
         return YXH_EINVAL;
     }
     YXH_CHECK_LAUNCH("pack_dgrad");
+    return YXH_OK;
+}
+
+int pack_batch_launch(const yxh_pack_job* jobs, int njobs, int total_blocks, int dt, hipStream_t st) {
+    YXH_CHECK_ARG(jobs && njobs > 0 && total_blocks > 0, "pack_batch: empty job table");
+    if (dt == YXH_BF16) hipLaunchKernelGGL(pack_batch<bf16>, dim3(total_blocks), dim3(256), 0, st, jobs, njobs);
+    else if (dt == YXH_F16) hipLaunchKernelGGL(pack_batch<f16>, dim3(total_blocks), dim3(256), 0, st, jobs, njobs);
+    else if (dt == YXH_F32) hipLaunchKernelGGL(pack_batch<float>, dim3(total_blocks), dim3(256), 0, st, jobs, njobs);
+    else {
+        set_error("pack_batch dtype %d", dt);
+        return YXH_EINVAL;
+    }
+    YXH_CHECK_LAUNCH("pack_batch");
     return YXH_OK;
 }
 

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -129,6 +129,17 @@ class HeadDesc(C.Structure):
                 ("a_off", C.c_int32), ("stride", C.c_float), ("train", C.c_int32), ("reserved", C.c_int32)]
 
 
+class PackJob(C.Structure):
+    """yxh_pack_job (include/yoloxhip.h): one repack of yxh_pack_weights_batch."""
+    _fields_ = [("w", C.c_void_p), ("cb", C.c_void_p), ("out", C.c_void_p), ("bias_out", C.c_void_p),
+                ("kind", C.c_int32), ("cout", C.c_int32), ("cin", C.c_int32), ("kh", C.c_int32), ("kw", C.c_int32),
+                ("pad", C.c_int32), ("c_begin", C.c_int32), ("c_count", C.c_int32), ("block0", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+PACK_FWD, PACK_DGRAD = 0, 1
+
+
 class _OpU(C.Union):
     _fields_ = [("conv", ConvDesc), ("focus", FocusDesc), ("spp", SppDesc), ("stem", StemDesc), ("head", HeadDesc),
                 ("stem2", Stem2Desc)]
@@ -193,6 +204,7 @@ def lib():
             "yxh_channel_sum": ([i32, i32, C.POINTER(Src), vp, vp, sz, vp], C.c_int),
             "yxh_conv_wgrad": ([C.POINTER(WgradDesc), vp], C.c_int),
             "yxh_pack_dgrad_weight": ([vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp], C.c_int),
+            "yxh_pack_weights_batch": ([vp, i32, i32, i32, vp], C.c_int),
             "yxh_spp_bwd": ([i32, i32, C.POINTER(Src), i32, vp, vp, vp], C.c_int),
             "yxh_upsample_bwd": ([vp, i32, i32, i32, i32, vp, vp], C.c_int),
             "yxh_head_decode_train": ([vp, i32, i32, i32, vp, vp, i32, vp, vp], C.c_int),
@@ -230,7 +242,7 @@ EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_co
             "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_s2", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_augment_batch", "yxh_sizeof_aug_image", "yxh_postprocess_workspace_bytes", "yxh_set_nms_mask_budget",
             "yxh_postprocess", "yxh_postprocess_ev", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes", "yxh_graph_create_dag",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
-            "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_spp_bwd",
+            "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_pack_weights_batch", "yxh_spp_bwd",
             "yxh_upsample_bwd", "yxh_head_decode_train", "yxh_yolox_loss_bwd", "yxh_opt_chunk_elems",
             "yxh_sgd_ema_step", "yxh_amp_found_inf", "yxh_amp_update_scale", "yxh_coco_eval", "yxh_coco_iou"]
 

@@ -164,6 +164,14 @@ class TrainGraph:
         self.grad_total = torch.ones((), dtype=torch.float32, device=self.device)
         self.tune = os.environ.get("YOLOX_AMD_TRAIN_TUNE", "1") != "0"
         self._scratch = torch.empty(0, dtype=torch.uint8, device=self.device)
+        # weight repacks: the first step launches one pack per conv (forward layout) and per
+        # data-gradient input slice, recording each as a yxh_pack_job; later steps repack
+        # everything in ONE yxh_pack_weights_batch launch at the start of the forward
+        self._dgrad_w: dict = {}
+        self._pack_jobs: dict = {}  # key -> (PackJob, (weight, bias) tensors it reads)
+        self._pack_table = None     # (device job table, njobs, total blocks, signature)
+        self._batched = False       # this step's repacks were done by the batch launch
+        self.batch_pack = os.environ.get("YOLOX_AMD_BATCH_PACK", "1") != "0"
 
     # ------------------------------------------------------------ helpers
     @property
@@ -186,6 +194,9 @@ class TrainGraph:
             w = (torch.empty(conv.out_channels * kh * kw * cin_pad, dtype=self.dtype, device=self.device),
                  torch.empty(conv.out_channels, dtype=torch.float32, device=self.device))
             self._fwd_w[id(conv)] = w
+        key = ("fwd", id(conv))
+        if self._batched and key in self._pack_jobs:
+            return w
         wt = conv.weight.detach()
         if wt.dtype != torch.float32:
             raise ValueError("training keeps fp32 master weights; the compute dtype comes from autocast")
@@ -194,7 +205,41 @@ class TrainGraph:
             wt.data_ptr(), b.data_ptr() if b is not None else None, None, None, None, None, 0.0,
             conv.out_channels, conv.in_channels // conv.groups, kh, kw, cin_pad, self.dcode, w[0].data_ptr(),
             w[1].data_ptr(), self.stream), "pack weights")
+        job = N.PackJob(wt.data_ptr(), b.data_ptr() if b is not None else None, w[0].data_ptr(), w[1].data_ptr(),
+                        N.PACK_FWD, conv.out_channels, conv.in_channels // conv.groups, kh, kw, cin_pad, 0, 0)
+        self._pack_jobs[key] = (job, conv.out_channels * kh * kw * cin_pad, (conv.weight, conv.bias))
+        self._pack_table = None  # a job the table lacks: rebuild it after this step
         return w
+
+    # ------------------------------------------------------------ batched repacks
+    def _pack_signature(self) -> tuple:
+        return tuple((p.data_ptr() if p is not None else 0) for _, _, ts in self._pack_jobs.values() for p in ts)
+
+    def _build_pack_table(self) -> None:
+        """After a step that launched its repacks one by one: the job table for later steps."""
+        jobs, block = [], 0
+        for job, elems, _ in self._pack_jobs.values():
+            job.block0 = block
+            block += (elems + 255) // 256
+            jobs.append(job)
+        raw = (N.PackJob * len(jobs))(*jobs)
+        table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+        self._pack_table = (table, len(jobs), block, self._pack_signature())
+
+    def _pack_all(self) -> None:
+        """One launch for every repack of this step, when the recorded table still matches
+        the parameters' storage; otherwise this step packs per conv (and re-records)."""
+        self._batched = False
+        t = self._pack_table
+        if not self.batch_pack or t is None:
+            return
+        if t[3] != self._pack_signature():
+            self._pack_table = None
+            self._pack_jobs = {}
+            return
+        self._chk(self.lib.yxh_pack_weights_batch(t[0].data_ptr(), t[1], t[2], self.dcode, self.stream),
+                  "pack weights (batch)")
+        self._batched = True
 
     def _conv(self, srcs: list, cin: int, cout: int, k: int, stride: int, pad: int, weight: int, bias: int,
               dst: int, dst_f32: bool, dst_cs: int, dst_bs: int, in_h: int, in_w: int, out_h: int, out_w: int,
@@ -281,10 +326,19 @@ class TrainGraph:
             if not act.needs_grad:
                 continue
             cs = act.ch
-            wt = torch.empty(cs * kh * kh * cout_pad, dtype=self.dtype, device=self.device)
-            self._chk(self.lib.yxh_pack_dgrad_weight(
-                conv.weight.detach().data_ptr(), conv.out_channels, conv.in_channels, kh, kh, cb, cs, cout_pad,
-                self.dcode, wt.data_ptr(), self.stream), "pack dgrad")
+            key = ("dgrad", id(conv), cb, cs, cout_pad)
+            wt = self._dgrad_w.get(key)
+            if wt is None:
+                wt = torch.empty(cs * kh * kh * cout_pad, dtype=self.dtype, device=self.device)
+                self._dgrad_w[key] = wt
+            if not (self._batched and key in self._pack_jobs):
+                self._chk(self.lib.yxh_pack_dgrad_weight(
+                    conv.weight.detach().data_ptr(), conv.out_channels, conv.in_channels, kh, kh, cb, cs, cout_pad,
+                    self.dcode, wt.data_ptr(), self.stream), "pack dgrad")
+                job = N.PackJob(conv.weight.detach().data_ptr(), None, wt.data_ptr(), None, N.PACK_DGRAD,
+                                conv.out_channels, conv.in_channels, kh, kh, cout_pad, cb, cs)
+                self._pack_jobs[key] = (job, cs * kh * kh * cout_pad, (conv.weight,))
+                self._pack_table = None
             in_h, in_w = act.h << up, act.w << up  # the conv's logical input size
             if up:  # the conv writes every element of the temporary; upsample_bwd accumulates
                 dst, acc = torch.empty(batch, in_h, in_w, cs, dtype=torch.float32, device=self.device), False
@@ -544,6 +598,7 @@ class TrainGraph:
         labels = labels.to(self.device, torch.float32).contiguous()
         self._keep = (images, labels)
         self._bn_counters = []
+        self._pack_all()
         feats = self.pafpn(self.model.backbone, images)
         out = self.head(self.model.head, feats, labels)
         if self._bn_counters:
@@ -560,6 +615,8 @@ class TrainGraph:
             fn()
         self.tape = []
         self._keep = None
+        if self.batch_pack and self._pack_table is None and self._pack_jobs:
+            self._build_pack_table()
         if self.on_backward_end is not None:
             self.on_backward_end()
         self.grads.publish(prev)

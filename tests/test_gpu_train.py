@@ -515,3 +515,63 @@ def test_sgd_step_changes_eval_plan():
     m.eval()
     y1 = m(x.cuda())
     assert not torch.equal(y0, y1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_batched_weight_repack_matches_per_conv(monkeypatch, dtype):
+    """Steps after the first repack every forward / data-gradient weight layout in ONE
+    yxh_pack_weights_batch launch: after an optimizer step, each packed buffer is
+    bit-identical to the per-conv yxh_fold_bn_pack / yxh_pack_dgrad_weight result, and the
+    step's losses equal those of a per-conv (YOLOX_AMD_BATCH_PACK=0) graph."""
+    from yolox_amd import _native as N
+    import yolox_amd.train as T
+    monkeypatch.setenv("YOLOX_AMD_TRAIN_TUNE", "0")
+    monkeypatch.setattr(T, "_TRAIN_TILES", {})
+    m, sd, x, labels, _ = _model_and_batch()
+    m = m.cuda().train()
+    opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, nesterov=True)
+
+    def step(mod):
+        ctx = torch.autocast("cuda", dtype=dtype) if dtype != torch.float32 else torch.autocast("cuda", enabled=False)
+        with ctx:
+            out = mod(x.cuda(), labels.cuda())
+        out["total_loss"].backward()
+        return out
+
+    step(m)
+    opt.step()
+    m.zero_grad(set_to_none=True)
+    out = step(m)  # batched repack of the updated weights
+    torch.cuda.synchronize()
+    g = m._train_graph
+    assert g._batched and g._pack_table is not None and g._pack_table[1] == len(g._pack_jobs) > 50
+    st = N.stream_ptr()
+    for key, (job, elems, _) in g._pack_jobs.items():
+        if key[0] == "fwd":
+            conv = next(c for c in m.modules() if id(c) == key[1])
+            got = g._fwd_w[key[1]][0]
+        else:
+            conv = next(c for c in m.modules() if id(c) == key[1])
+            got = g._dgrad_w[key]
+        want = torch.empty_like(got)
+        if job.kind == N.PACK_FWD:
+            bias = torch.empty(job.cout, dtype=torch.float32, device="cuda")
+            chk(lib().yxh_fold_bn_pack(conv.weight.data_ptr(), conv.bias.data_ptr() if conv.bias is not None else None,
+                                       None, None, None, None, 0.0, job.cout, job.cin, job.kh, job.kw, job.pad,
+                                       DT[dtype], want.data_ptr(), bias.data_ptr(), st))
+        else:
+            chk(lib().yxh_pack_dgrad_weight(conv.weight.data_ptr(), job.cout, job.cin, job.kh, job.kw, job.c_begin,
+                                            job.c_count, job.pad, DT[dtype], want.data_ptr(), st))
+        torch.cuda.synchronize()
+        assert torch.equal(got.view(torch.int16 if dtype != torch.float32 else torch.int32),
+                           want.view(torch.int16 if dtype != torch.float32 else torch.int32)), key
+    # the same step through per-conv repacks
+    m2, _, _, _, _ = _model_and_batch()
+    m2 = m2.cuda().train()
+    m2.load_state_dict(m.state_dict())
+    m2.train()
+    monkeypatch.setenv("YOLOX_AMD_BATCH_PACK", "0")
+    ref = step(m2)
+    assert not m2._train_graph.batch_pack
+    for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss", "num_fg"):
+        assert float(out[k]) == float(ref[k]), k
