@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 12
+#define YXH_ABI_VERSION 13
 
 enum yxh_status {
     YXH_OK = 0,
@@ -115,6 +115,11 @@ typedef struct {
      * dst must not alias the source (tile halos are read while other tiles write). */
     const void* pre_weight; /* [cin][cin] in dtype                                          */
     const float* pre_bias;  /* fp32 [cin]                                                    */
+    /* Optional: `weight` in the MFMA fragment-major layout of yxh_pack_frag (16-bit, cout % 16
+     * == 0, cin % 32 == 0).  The weight-stationary tiles (conv_ws / conv_ws1) then load their
+     * stationary weights as whole 1 KiB wave reads (every lane one 16-byte piece of one
+     * 128-byte line) instead of sixteen 64-byte row pieces per read; other tiles ignore it. */
+    const void* weight_frag;
 } yxh_conv_desc;
 
 #define YXH_CONV_ACCUMULATE 1
@@ -362,7 +367,8 @@ typedef struct {
     yxh_src src[2];
     yxh_src dy;
     float* dw;
-    int32_t tile, reserved;  /* tile 0: by shape; 1-4: 64x64, 128x128, 32x64, 16x64 (cout x cin,
+    int32_t tile, reserved;  /* tile 0: by shape; 17-20 (fp32 1x1 s1): k-major MFMA operands, 64x64, 128x128,
+                                128x64, 64x128; 1-4: 64x64, 128x128, 32x64, 16x64 (cout x cin,
                                 register-transposed loader); 5-10 (bf16/f16): LDS-DMA +
                                 ds_read_b64_tr_b16, 128x128 (3 / 2 buffers), 64x64 (3 / 2),
                                 128x64, 64x128 */
@@ -376,6 +382,15 @@ int yxh_conv_wgrad(const yxh_wgrad_desc* d, void* stream);
  */
 int yxh_pack_dgrad_weight(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, int32_t c_begin,
                           int32_t c_count, int32_t cout_pad, int32_t dtype, void* out, void* stream);
+
+/*
+ * yxh_pack_frag: packed conv weights [cout][taps][cin] (16-bit) -> the MFMA fragment-major
+ * layout the weight-stationary conv tiles read: 1 KiB blocks (16 output channels x 32 input
+ * channels of one tap), block (nf, tap, kb) at ((nf * taps + tap) * cin/32 + kb) KiB, lane
+ * l = 16 * q + r of a 16x16x32 MFMA operand at byte 16 * l of its block holding channel
+ * 16 nf + r, inputs 32 kb + 8 q .. + 8.  cout % 16 == 0, cin % 32 == 0.
+ */
+int yxh_pack_frag(const void* w, int32_t cout, int32_t taps, int32_t cin, int32_t dtype, void* out, void* stream);
 
 /*
  * yxh_pack_weights_batch: every weight repack of one training step in ONE launch (the

@@ -356,6 +356,21 @@ __global__ __launch_bounds__(256) void fold_bn_pack(const float* w, const float*
     }
 }
 
+// ---------------------------------------------------------------- fragment-major weights
+// [cout][taps][cin] -> 1 KiB blocks (nf, tap, kb): lane l = 16 q + r holds channel 16 nf + r,
+// inputs 32 kb + 8 q .. + 8 (yxh_pack_frag); one thread per 16-byte piece
+__global__ __launch_bounds__(256) void pack_frag(const uint4* w, int cout, int taps, int cin, uint4* out) {
+    const int kbs = cin >> 5;
+    const long long total = (long long)(cout >> 4) * taps * kbs * 64;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int l = (int)(idx & 63);
+    const long long blk = idx >> 6;
+    const int kb = (int)(blk % kbs), tap = (int)((blk / kbs) % taps), nf = (int)(blk / ((long long)kbs * taps));
+    const int n = nf * 16 + (l & 15), k = kb * 32 + (l >> 4) * 8;
+    out[idx] = w[(((long long)n * taps + tap) * cin + k) >> 3];
+}
+
 // ================================================================ host side
 namespace {
 
@@ -498,6 +513,10 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     p.res_dense = d->residual && d->res_bstride == (long long)p.ohw * d->res_cstride;
     p.pw1 = d->pre_weight;
     p.pb1 = d->pre_bias;
+    YXH_CHECK_ARG(!d->weight_frag || (dt != YXH_F32 && aligned16(d->weight_frag) && d->cout % 16 == 0 &&
+                                      d->cin % 32 == 0 && d->groups == 1),
+                  "weight_frag: 16-bit, cout %% 16 == 0, cin %% 32 == 0, groups 1");
+    p.wf = d->weight_frag;
     p.grp2 = grp2 ? 1 : 0;
     if (grp2 && d->tile == 0) return conv_ws_dispatch(dt, d->cin == 256 ? 176 - 160 : 185 - 160, p, st);
     if (grp2 && !((d->tile >> 1) > 160 && (d->tile >> 1) <= 190)) {
@@ -627,6 +646,17 @@ int spp_launch(void* buf, int dt, int B, int H, int W, int C, int cs, long long 
 #undef YXH_SPP_T
 #undef YXH_SPP
     YXH_CHECK_LAUNCH("spp launch");
+    return YXH_OK;
+}
+
+int pack_frag_launch(const void* w, int cout, int taps, int cin, int dt, void* out, hipStream_t st) {
+    YXH_CHECK_ARG(w && out && aligned16(w) && aligned16(out), "pack_frag: null / unaligned");
+    YXH_CHECK_ARG(dt == YXH_BF16 || dt == YXH_F16, "pack_frag: 16-bit weights");
+    YXH_CHECK_ARG(cout > 0 && cout % 16 == 0 && taps > 0 && cin > 0 && cin % 32 == 0, "pack_frag geometry");
+    const long long total = (long long)(cout / 16) * taps * (cin / 32) * 64;
+    hipLaunchKernelGGL(pack_frag, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const uint4*)w, cout,
+                       taps, cin, (uint4*)out);
+    YXH_CHECK_LAUNCH("pack_frag");
     return YXH_OK;
 }
 

@@ -30,7 +30,23 @@ struct ConvParams {
     const void* pw1;  // fused Bottleneck conv1 (1x1, cin -> cin) ahead of the 3x3: conv_ws only
     const float* pb1;
     int grp2;  // YXH_CONV_GROUPS2: output half g reads source channels [g*cin, (g+1)*cin)
+    const void* wf;  // weights in yxh_pack_frag's fragment-major layout, or null (conv_ws / conv_ws1)
 };
+
+// Stationary weight fragment (i: 16 output channels from n_first, tap, kb: 32-channel K block)
+// of a weight-stationary tile: one 1 KiB wave read from the fragment-major copy when present
+// (whole 128-byte lines), else 16 row pieces of 64 bytes from [cout][taps][cin].
+template <typename T>
+__device__ __forceinline__ uint4 ws_weight(const ConvParams& p, int n_first, int tap, int taps, int cin, int kb,
+                                           int lane) {
+    const int frow = lane & 15, fq = lane >> 4;
+    if (p.wf) {
+        const int nf = min(n_first, p.cout - 16) >> 4;
+        return ((const uint4*)p.wf)[((long long)(nf * taps + tap) * (cin >> 5) + kb) * 64 + lane];
+    }
+    const int n = min(n_first + frow, p.cout - 1);
+    return *(const uint4*)((const T*)p.w + ((long long)n * taps + tap) * cin + kb * 32 + fq * 8);
+}
 
 // ---------------------------------------------------------------- MFMA step
 // One 64-byte K slab: lane l holds row (l & 15), 16-byte chunk (l >> 4) of both

@@ -94,18 +94,13 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 
     // ---- stationary weights: a[i][tap][c] = 16 channels x 32 K of fragment i
     uint4 a[FR][9][WCB];
-    {
-        const T* w = (const T*)p.w;
 #pragma unroll
-        for (int i = 0; i < FR; ++i) {
-            const int n = min(n0 + wn * WTN + i * 16 + frow, cout - 1);
+    for (int i = 0; i < FR; ++i)
 #pragma unroll
-            for (int tap = 0; tap < 9; ++tap)
+        for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-                for (int c = 0; c < WCB; ++c)
-                    a[i][tap][c] = *(const uint4*)(w + ((long long)n * 9 + tap) * CIN + (wk * WCB + c) * 32 + fq * 8);
-        }
-    }
+            for (int c = 0; c < WCB; ++c)
+                a[i][tap][c] = ws_weight<T>(p, n0 + wn * WTN + i * 16, tap, 9, CIN, wk * WCB + c, lane);
     float bias[FR][4];
 #pragma unroll
     for (int i = 0; i < FR; ++i) {

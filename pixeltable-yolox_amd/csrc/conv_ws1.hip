@@ -48,15 +48,10 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
     const int c1 = CIN - c0;
 
     uint4 a[FR][WCB];
-    {
-        const T* w = (const T*)p.w;
 #pragma unroll
-        for (int i = 0; i < FR; ++i) {
-            const int n = min(n0 + wn * WTN + i * 16 + frow, cout - 1);
+    for (int i = 0; i < FR; ++i)
 #pragma unroll
-            for (int c = 0; c < WCB; ++c) a[i][c] = *(const uint4*)(w + (long long)n * CIN + (wk * WCB + c) * 32 + fq * 8);
-        }
-    }
+        for (int c = 0; c < WCB; ++c) a[i][c] = ws_weight<T>(p, n0 + wn * WTN + i * 16, 0, 1, CIN, wk * WCB + c, lane);
     float bias[FR][4];
 #pragma unroll
     for (int i = 0; i < FR; ++i) {

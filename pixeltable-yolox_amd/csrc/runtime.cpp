@@ -30,6 +30,7 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st);
 int focus_pack_launch(const void* img, int layout, int idt, int B, int H, int W, void* dst, int odt,
                       hipStream_t st);
 int spp_launch(void* buf, int dt, int B, int H, int W, int C, int cs, long long bs, hipStream_t st);
+int pack_frag_launch(const void* w, int cout, int taps, int cin, int dt, void* out, hipStream_t st);
 int fold_launch(const float* w, const float* cb, const float* g, const float* beta, const float* mean,
                 const float* var, float eps, int cout, int cin_g, int kh, int kw, int cin_pad, int dt, void* wo,
                 float* bo, hipStream_t st);
@@ -129,6 +130,10 @@ int yxh_stem_pack(const float* conv_w, const float* bn_gamma, const float* bn_be
 int yxh_spp_maxpool(void* buf, int32_t dtype, int32_t batch, int32_t h, int32_t w, int32_t c, int32_t cstride,
                     int64_t bstride, void* stream) {
     return spp_launch(buf, dtype, batch, h, w, c, cstride, bstride, (hipStream_t)stream);
+}
+
+int yxh_pack_frag(const void* w, int32_t cout, int32_t taps, int32_t cin, int32_t dtype, void* out, void* stream) {
+    return pack_frag_launch(w, cout, taps, cin, dtype, out, (hipStream_t)stream);
 }
 
 int yxh_fold_bn_pack(const float* conv_w, const float* conv_bias, const float* bn_gamma, const float* bn_beta,

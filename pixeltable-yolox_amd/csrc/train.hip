@@ -941,6 +941,136 @@ __global__ __launch_bounds__(256) void conv_wgrad2(WgradParams p) {
         }
 }
 
+// ------------------------------------------------------------------ fp32 1x1 weight gradient
+// dW[n][c] += sum over pixels p of dY[p][n] * X[p][c] for 1x1 s1 convs in fp32 (the CSP /
+// SPP / PAFPN / head-stem 1x1 BaseConvs and the head preds).  Both operands are pixel-major,
+// which is exactly the k-major operand form of v_mfma_f32_16x16x4_f32 (lane l: A[l % 16][l / 16]
+// = dY[p0 + l / 16][n0 + l % 16], B likewise from X): no transposes.  A block owns a TN x TC
+// tile of dW over a range of KP-pixel stages (split-K over pixels); per stage both [KP][TN] and
+// [KP][TC] slabs are staged through LDS by 16-byte register loads (rows padded by 16 floats:
+// the four 16-lane row groups of a ds_read_b32 hit distinct banks), double-buffered so the next
+// stage's loads fly under this stage's MFMAs; the block's partial dW goes out with hardware
+// fp32 atomics (dW pre-zeroed, as for conv_wgrad).
+template <int TN, int TC, int WN, int WC, int KP>
+__global__ __launch_bounds__(256) void wgrad1_f32(WgradParams p) {
+    static_assert(WN * WC == 4, "4 waves");
+    constexpr int WTN = TN / WN, WTC = TC / WC, FN = WTN / 16, FC = WTC / 16;
+    constexpr int TNP = TN + 16, TCP = TC + 16;
+    constexpr int ASZ = KP * TNP, BSZ = KP * TCP;
+    constexpr int ACH = KP * TN / 4, BCH = KP * TC / 4, AL = (ACH + 255) / 256, BL = (BCH + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float lds[2][ASZ + BSZ];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wn = wave % WN, wc = wave / WN;
+    const int n0 = blockIdx.y * TN, c0 = blockIdx.z * TC;
+    const int st0 = blockIdx.x * p.sps, st1 = min(p.nst, st0 + p.sps);
+    if (st0 >= st1) return;  // block-uniform
+    const int M = p.M, ohw = p.ohw, ow = p.out_w, cout = p.cout, cin = p.cin;
+    const float* dy = (const float*)p.dy;
+    const bool dy_dense = p.dybs == (long long)ohw * p.dycs;
+
+    float4 ra[AL], rb[BL];
+    auto gload = [&](int st) {
+        const int pb = st * KP;
+#pragma unroll
+        for (int i = 0; i < AL; ++i) {
+            const int q = tid + 256 * i;
+            const int row = q / (TN / 4), col = q - row * (TN / 4);
+            const int m = pb + row, n = n0 + col * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q < ACH && m < M && n < cout) {
+                long long off;
+                if (dy_dense) {
+                    off = (long long)m * p.dycs;
+                } else {
+                    const int b = m / ohw;
+                    off = (long long)b * p.dybs + (long long)(m - b * ohw) * p.dycs;
+                }
+                v = *(const float4*)(dy + off + n);
+            }
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BL; ++i) {
+            const int q = tid + 256 * i;
+            const int row = q / (TC / 4), col = q - row * (TC / 4);
+            const int m = pb + row, c = c0 + col * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q < BCH && m < M && c < cin) {
+                const int s = (p.nsrc > 1 && c >= p.src0_ch) ? 1 : 0;
+                const int cc = s ? c - p.src0_ch : c;
+                const int b = m / ohw, pix = m - b * ohw;
+                int spix = pix;
+                if (p.sup[s]) {
+                    const int y = pix / ow, x = pix - y * ow;
+                    spix = (y >> 1) * p.sw[s] + (x >> 1);
+                }
+                v = *(const float4*)((const float*)p.sptr[s] + (long long)b * p.sbs[s] + (long long)spix * p.scs[s] + cc);
+            }
+            rb[i] = v;
+        }
+    };
+    auto lstore = [&](int buf) {
+        float* A = lds[buf];
+        float* Bm = lds[buf] + ASZ;
+#pragma unroll
+        for (int i = 0; i < AL; ++i) {
+            const int q = tid + 256 * i;
+            const int row = q / (TN / 4), col = q - row * (TN / 4);
+            if (q < ACH) *(float4*)(A + row * TNP + col * 4) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BL; ++i) {
+            const int q = tid + 256 * i;
+            const int row = q / (TC / 4), col = q - row * (TC / 4);
+            if (q < BCH) *(float4*)(Bm + row * TCP + col * 4) = rb[i];
+        }
+    };
+
+    f32x4 acc[FN][FC];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int kr = lane >> 4, kc = lane & 15;
+    gload(st0);
+    lstore(0);
+    __syncthreads();
+    int buf = 0;
+    for (int st = st0; st < st1; ++st) {
+        const bool more = st + 1 < st1;
+        if (more) gload(st + 1);
+        const float* A = lds[buf] + wn * WTN + kc;
+        const float* Bm = lds[buf] + ASZ + wc * WTC + kc;
+#pragma unroll
+        for (int kk = 0; kk < KP / 4; ++kk) {
+            float a[FN], b[FC];
+#pragma unroll
+            for (int i = 0; i < FN; ++i) a[i] = A[(4 * kk + kr) * TNP + 16 * i];
+#pragma unroll
+            for (int j = 0; j < FC; ++j) b[j] = Bm[(4 * kk + kr) * TCP + 16 * j];
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FC; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) lstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    // D[m][n] of fragment (i, j): lane holds rows 4 (lane / 16) + r, column lane % 16
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+            const int c = c0 + wc * WTC + 16 * j + kc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n0 + wn * WTN + 16 * i + 4 * kr + r;
+                if (n < cout && c < p.cin_store) unsafeAtomicAdd(p.dw + (long long)n * p.cin_store + c, acc[i][j][r]);
+            }
+        }
+}
+
 // dgrad weights: w [cout][cin][kh][kw] fp32 -> [c_count][kh][kw][cout_pad] of T, taps
 // flipped (ky -> kh-1-ky), input channels [c_begin, c_begin + c_count).
 template <typename T>
@@ -1318,6 +1448,31 @@ int launch_wgrad2_t(WgradParams p, hipStream_t st) {
     }
 }
 
+template <int TN, int TC, int WN, int WC, int KP>
+int launch_wgrad1_f32(WgradParams p, hipStream_t st) {
+    if (p.kh != 1 || p.kw != 1 || p.stride != 1 || p.pad != 0) {
+        set_error("wgrad tiles 17-20 (fp32 1x1) need a 1x1 s1 p0 conv");
+        return YXH_EUNSUPPORTED;
+    }
+    if ((p.nsrc > 1 && p.src0_ch % 4) || p.dycs % 4 || p.dybs % 4) {
+        set_error("wgrad tiles 17-20: 16-byte channel chunks");
+        return YXH_EUNSUPPORTED;
+    }
+    const int ntn = (p.cout + TN - 1) / TN, ntc = (p.cin + TC - 1) / TC;
+    p.nst = (int)(((long long)p.M + KP - 1) / KP);
+    const long long tiles = (long long)ntn * ntc;
+    long long splits = (512 + tiles - 1) / tiles;  // about two blocks per CU
+    const long long max_splits = (p.nst + 3) / 4;  // >= 4 stages per split
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    p.sps = (int)((p.nst + splits - 1) / splits);
+    splits = (p.nst + p.sps - 1) / p.sps;
+    YXH_CHECK_ARG(ntn < 65536 && ntc < 65536, "wgrad grid");
+    hipLaunchKernelGGL((wgrad1_f32<TN, TC, WN, WC, KP>), dim3((unsigned)splits, ntn, ntc), dim3(256), 0, st, p);
+    YXH_CHECK_LAUNCH("wgrad1_f32");
+    return YXH_OK;
+}
+
 template <typename T>
 int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
     // default: 64 x 64 (cout x cin), 2 x 2 waves; 4 slabs (bf16: 128 pixels) per stage
@@ -1350,6 +1505,18 @@ int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
                     case 14: return s2 ? launch_wgrad9_t<2, 32, 16, 2, 1, 4>(p, st) : launch_wgrad9_t<1, 32, 16, 2, 1, 8>(p, st);
                     case 15: return s2 ? launch_wgrad9_t<2, 32, 32, 2, 2, 2>(p, st) : launch_wgrad9_t<1, 32, 32, 2, 2, 4>(p, st);
                     default: return s2 ? launch_wgrad9_t<2, 64, 16, 4, 1, 4>(p, st) : launch_wgrad9_t<1, 64, 16, 4, 1, 8>(p, st);
+                }
+            }
+        case 17: case 18: case 19: case 20:
+            if constexpr (sizeof(T) != 4) {
+                set_error("wgrad tiles 17-20 (1x1, k-major MFMA operands) are built for fp32 only");
+                return YXH_EUNSUPPORTED;
+            } else {
+                switch (tile) {
+                    case 17: return launch_wgrad1_f32<64, 64, 2, 2, 32>(p, st);
+                    case 18: return launch_wgrad1_f32<128, 128, 2, 2, 16>(p, st);
+                    case 19: return launch_wgrad1_f32<128, 64, 2, 2, 32>(p, st);
+                    default: return launch_wgrad1_f32<64, 128, 2, 2, 32>(p, st);
                 }
             }
         default: set_error("wgrad tile %d", tile); return YXH_EINVAL;

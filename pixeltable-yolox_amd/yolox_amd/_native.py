@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -47,7 +47,8 @@ class ConvDesc(C.Structure):
                 ("dst_dtype", C.c_int32), ("res_bstride", C.c_int64), ("dst", C.c_void_p),
                 ("dst_cstride", C.c_int32), ("act", C.c_int32), ("dst_bstride", C.c_int64),
                 ("decode_stride", C.c_float), ("decode_coff", C.c_int32), ("tile", C.c_int32),
-                ("flags", C.c_int32), ("reserved0", C.c_int32), ("pre_weight", C.c_void_p), ("pre_bias", C.c_void_p)]
+                ("flags", C.c_int32), ("reserved0", C.c_int32), ("pre_weight", C.c_void_p), ("pre_bias", C.c_void_p),
+                ("weight_frag", C.c_void_p)]
 
 
 CONV_ACCUMULATE = 1
@@ -205,6 +206,7 @@ def lib():
             "yxh_conv_wgrad": ([C.POINTER(WgradDesc), vp], C.c_int),
             "yxh_pack_dgrad_weight": ([vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp], C.c_int),
             "yxh_pack_weights_batch": ([vp, i32, i32, i32, vp], C.c_int),
+            "yxh_pack_frag": ([vp, i32, i32, i32, i32, vp, vp], C.c_int),
             "yxh_spp_bwd": ([i32, i32, C.POINTER(Src), i32, vp, vp, vp], C.c_int),
             "yxh_upsample_bwd": ([vp, i32, i32, i32, i32, vp, vp], C.c_int),
             "yxh_head_decode_train": ([vp, i32, i32, i32, vp, vp, i32, vp, vp], C.c_int),
@@ -242,7 +244,7 @@ EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_co
             "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_s2", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_augment_batch", "yxh_sizeof_aug_image", "yxh_postprocess_workspace_bytes", "yxh_set_nms_mask_budget",
             "yxh_postprocess", "yxh_postprocess_ev", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes", "yxh_graph_create_dag",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
-            "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_pack_weights_batch", "yxh_spp_bwd",
+            "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_pack_weights_batch", "yxh_pack_frag", "yxh_spp_bwd",
             "yxh_upsample_bwd", "yxh_head_decode_train", "yxh_yolox_loss_bwd", "yxh_opt_chunk_elems",
             "yxh_sgd_ema_step", "yxh_amp_found_inf", "yxh_amp_update_scale", "yxh_coco_eval", "yxh_coco_iou"]
 

@@ -87,6 +87,7 @@ class WeightSpec:
     stem: bool = False  # fused Focus+stem layout [round16(cout)][6][32] (yxh_stem_pack)
     w_off: int = -1  # bytes into weight arena
     b_off: int = -1  # bytes into bias arena
+    f_off: int = -1  # bytes into the fragment-major copy (yxh_pack_frag), -1 = none
 
 
 @dataclass(eq=False)
@@ -107,6 +108,8 @@ class OpRec:
 # process on one box (tools/ab_fuse.py) the two-launch form is 1.8 % faster (2.001 vs 2.038 ms per
 # yolox_s bs32 forward) -- the fused kernel's 1x1-on-the-halo phase is not overlapped with MFMAs
 _FUSE_BOTTLENECK = os.environ.get("YOLOX_AMD_FUSE_BOTTLENECK", "0") == "1"
+# fragment-major weight copies for the weight-stationary tiles (YOLOX_AMD_WFRAG=0: row layout only)
+_WFRAG = os.environ.get("YOLOX_AMD_WFRAG", "1") != "0"
 
 
 class PlanCtx:
@@ -508,6 +511,19 @@ class Plan:
                 woff += _align(s.cout * s.kh * s.kw * s.cin_pad * ctx.esize)
                 boff += _align(s.cout * 4)
         self.warena = torch.empty(max(woff, 1), dtype=torch.uint8, device=self.device)
+        # fragment-major copies of the 16-bit conv weights the weight-stationary tiles
+        # (conv_ws / conv_ws1) load as whole 1 KiB wave reads (yxh_conv_desc.weight_frag)
+        foff = 0
+        if dtype != torch.float32 and _WFRAG:
+            for rec in ctx.ops:
+                a = rec.args
+                if rec.kind != N.OP_CONV or a["dst_f32"] or a["groups"] != 1:
+                    continue
+                sp: WeightSpec = a["spec"]
+                if sp.f_off < 0 and not sp.stem and sp.cout % 16 == 0 and sp.cin_pad % 32 == 0:
+                    sp.f_off = foff
+                    foff += _align(sp.cout * sp.kh * sp.kw * sp.cin_pad * ctx.esize)
+        self.farena = torch.empty(max(foff, 1), dtype=torch.uint8, device=self.device)
         self.barena = torch.empty(max(boff, 1), dtype=torch.uint8, device=self.device)
         self.output = torch.empty(batch, anchors if stage != "features" else 0, 5 + self.num_classes,
                                   dtype=torch.float32, device=self.device)
@@ -619,6 +635,7 @@ class Plan:
                 d.weight = self.warena.data_ptr() + spec.w_off
                 d.bias = self.barena.data_ptr() + spec.b_off
                 d.flags = N.CONV_GROUPS2 if a.get("grouped2") else 0
+                d.weight_frag = self.farena.data_ptr() + spec.f_off if spec.f_off >= 0 else None
                 pre = a.get("pre_spec")
                 if pre is not None:
                     d.pre_weight = self.warena.data_ptr() + pre.w_off
@@ -687,6 +704,9 @@ class Plan:
                     conv.out_channels, conv.in_channels // conv.groups, s.kh, s.kw, s.cin_pad, dt, wout, bout,
                     stream), "fold_bn_pack")
                 row += conv.out_channels
+            if s.f_off >= 0:
+                N.check(self.lib.yxh_pack_frag(self.warena.data_ptr() + s.w_off, s.cout, s.kh * s.kw, s.cin_pad, dt,
+                                               self.farena.data_ptr() + s.f_off, stream), "pack_frag")
         torch.cuda.current_stream(self.device).synchronize()  # `keep` tensors die after this
         del keep
         self._param_sig = sig

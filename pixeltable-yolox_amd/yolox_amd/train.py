@@ -133,7 +133,7 @@ class GradBuffer:
 CONV_TUNE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
                    for k in (0, 1)]
 CONV_TUNE_TILES_F32 = CONV_TUNE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)]
-WGRAD_TUNE_TILES = list(range(1, 11)) + (list(range(11, 17)))
+WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 21))
 _TRAIN_TILES: dict = {}
 
 

@@ -75,7 +75,7 @@ def ref_conv(x, conv, bn, act):
 
 
 def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_coff=0, out_c=None, tile=0, flags=0,
-             pre=None, groups2=False):
+             pre=None, groups2=False, frag=False):
     """srcs: list of (nhwc tensor [B,h,w,C], coff, ch, upsample)."""
     n = N()
     B = srcs[0][0].shape[0]
@@ -98,6 +98,11 @@ def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_cof
         sd.channels, sd.cstride, sd.bstride = ch, t.shape[3], t.shape[1] * t.shape[2] * t.shape[3]
         sd.h, sd.w, sd.upsample = t.shape[1], t.shape[2], up
     d.weight, d.bias = w.data_ptr(), b.data_ptr()
+    if frag:  # the fragment-major copy (yxh_pack_frag) the weight-stationary tiles read
+        wf = torch.empty_like(w)
+        n.check(n.lib().yxh_pack_frag(w.data_ptr(), cout, k * k, cin // 2 if groups2 else cin, n.DTYPE_CODE[dtype],
+                                      wf.data_ptr(), n.stream_ptr()), "pack_frag")
+        d.weight_frag = wf.data_ptr()
     if residual is not None:
         t, coff = residual
         d.residual = t.data_ptr() + coff * t.element_size()
@@ -710,8 +715,25 @@ def test_conv_ws_3x3(dtype, geom):
             assert "input channels" in str(e), e
             continue
         close(y.permute(0, 3, 1, 2), want, dtype)
+        if cout % 16 == 0:  # fragment-major weights: the same values, bit for bit
+            yf = run_conv([(wide, 16, cin, 0)], conv, bn, dtype, tile=2 * tid, frag=True)
+            assert torch.equal(yf, y), tid
         ran += 1
     assert ran >= 1
+
+
+def test_pack_frag_layout():
+    """yxh_pack_frag: block (nf, tap, kb) of 1 KiB, lane l = 16 q + r holds channel 16 nf + r,
+    inputs 32 kb + 8 q .. + 8 -- against the same permutation done in torch."""
+    n = N()
+    cout, taps, cin = 48, 9, 64
+    w = torch.randn(cout, taps, cin).to(torch.bfloat16).to(DEV)
+    out = torch.empty_like(w)
+    n.check(n.lib().yxh_pack_frag(w.data_ptr(), cout, taps, cin, n.BF16, out.data_ptr(), n.stream_ptr()), "pack_frag")
+    want = w.view(cout // 16, 16, taps, cin // 32, 4, 8).permute(0, 2, 3, 4, 1, 5).reshape(-1)
+    assert torch.equal(out.view(-1), want)
+    with pytest.raises(ValueError):
+        n.check(n.lib().yxh_pack_frag(w.data_ptr(), 40, taps, cin, n.BF16, out.data_ptr(), n.stream_ptr()))
 
 
 @pytest.mark.parametrize("ch,H,W,B", [(32, 37, 45, 2), (64, 40, 24, 3), (128, 20, 22, 4), (64, 80, 80, 4)])
@@ -779,6 +801,9 @@ def test_conv_ws1_1x1(dtype, geom):
             continue
         close(y[..., 8:8 + cout].permute(0, 3, 1, 2), want, dtype)
         assert not y[..., :8].any() and not y[..., 8 + cout:].any()
+        y = y.clone()
+        yf = run_conv(bufs, conv, bn, dtype, out=out, out_coff=8, tile=2 * tid, frag=True)
+        assert torch.equal(yf, y), tid
         ran += 1
     assert ran >= 1
 
@@ -800,6 +825,8 @@ def test_conv_ws_two_groups(cin, H, W, B):
             assert "input channels" in str(e), e
             continue
         close(y.permute(0, 3, 1, 2), want, dtype)
+        yf = run_conv([(X, 0, 2 * cin, 0)], conv, bn, dtype, tile=2 * tid, groups2=True, frag=True)
+        assert torch.equal(yf, y), tid
         ran += 1
     assert ran >= 1
     with pytest.raises(NotImplementedError):  # the other kernel families refuse the two-group form

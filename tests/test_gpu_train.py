@@ -268,6 +268,47 @@ def test_conv_wgrad9_fp32_tiles(tile, cin0, cin1, up1, cout, k, s, H, B):
     assert rel(dw, wr.grad) < 1e-4
 
 
+WG1_CASES = [  # cin0, cin1, up1, cout, H, W, B, dy channels (>= cout, a strided dy view when larger)
+    (64, 0, 0, 64, 16, 20, 2, 64), (64, 64, 1, 128, 8, 12, 2, 128), (256, 0, 0, 192, 23, 17, 2, 192),
+    (48, 48, 0, 64, 10, 14, 3, 64), (128, 0, 0, 85, 6, 10, 2, 88), (512, 0, 0, 256, 5, 5, 4, 264),
+    (32, 0, 0, 32, 160, 160, 1, 32),
+]
+
+
+@pytest.mark.parametrize("tile", [17, 18, 19, 20])
+@pytest.mark.parametrize("cin0,cin1,up1,cout,H,W,B,dyc", WG1_CASES)
+def test_conv_wgrad1_fp32_tiles(tile, cin0, cin1, up1, cout, H, W, B, dyc):
+    """fp32 1x1 weight gradient on k-major MFMA operands (tiles 17-20) against torch autograd:
+    pixel tails of the KP-pixel stages, cout / cin tails of the tile (the head preds' 85 rows of
+    an 88-channel dy), two sources with the second upsampled, a wide dy read as a strided view."""
+    g = torch.Generator().manual_seed(cin0 * 3 + cout + H + tile)
+    x0 = torch.randn(B, H, W, cin0, generator=g)
+    x1 = torch.randn(B, H >> up1, W >> up1, cin1, generator=g) if cin1 else None
+    dy = torch.randn(B, H, W, dyc, generator=g)
+    srcs = [src(x0.cuda())]
+    if cin1:
+        srcs.append(src(x1.cuda(), up=up1))
+    dw = wgrad(torch.float32, srcs, src(dy.cuda()), cout, cin0 + cin1, 1, 1, 0, (H, W), (H, W), B, tile=tile)
+    torch.cuda.synchronize()
+    xin = x0.permute(0, 3, 1, 2)
+    if cin1:
+        x1n = x1.permute(0, 3, 1, 2)
+        if up1:
+            x1n = F.interpolate(x1n, scale_factor=2, mode="nearest")
+        xin = torch.cat([xin, x1n], 1)
+    wr = torch.zeros(cout, cin0 + cin1, 1, 1, requires_grad=True)
+    F.conv2d(xin, wr).backward(dy[..., :cout].permute(0, 3, 1, 2))
+    assert rel(dw, wr.grad) < 1e-5
+
+
+def test_conv_wgrad1_fp32_rejects_3x3():
+    """tiles 17-20 are 1x1 only: a 3x3 descriptor is refused (NotImplementedError)."""
+    x = torch.randn(1, 8, 8, 32).cuda()
+    dy = torch.randn(1, 8, 8, 32).cuda()
+    with pytest.raises(NotImplementedError):
+        wgrad(torch.float32, [src(x)], src(dy), 32, 32, 3, 1, 1, (8, 8), (8, 8), 1, tile=17)
+
+
 def test_wgrad_cin_store_and_strided_dy():
     """Focus stem: 16 packed channels, gradient of the 12 real ones; dy read through a
     strided view (the head's [B, A, 8] pred-gradient rows)."""

@@ -25,8 +25,11 @@ for spec in sys.argv[1:]:
     y = torch.empty(Bmax, Ho, Ho, Nc, device=dev, dtype=torch.bfloat16)
     w = (torch.randn(Nc, k, k, K, device=dev) / (k * k * K) ** 0.5).to(torch.bfloat16)
     b = torch.randn(Nc, device=dev) * 0.1
+    wf = torch.empty_like(w)
+    N.check(L.yxh_pack_frag(w.data_ptr(), Nc, k * k, K, N.BF16, wf.data_ptr(), st), "pack_frag")
     row = []
-    for B in BATCHES:
+    ref = None
+    for B, frag in [(b_, f_) for b_ in BATCHES for f_ in (0, 1)]:
         d = N.ConvDesc()
         d.dtype, d.batch = N.BF16, B
         d.in_h, d.in_w, d.out_h, d.out_w = H, H, Ho, Ho
@@ -36,10 +39,16 @@ for spec in sys.argv[1:]:
         d.weight, d.bias = w.data_ptr(), b.data_ptr()
         d.dst, d.dst_dtype, d.dst_cstride, d.dst_bstride = y.data_ptr(), N.BF16, Nc, Ho * Ho * Nc
         d.act, d.tile = N.ACT_SILU, 2 * tid
+        d.weight_frag = wf.data_ptr() if frag else None
+        y.zero_()
         if L.yxh_conv2d(C.byref(d), st) != N.OK:
             row.append(f"B{B}: n/a")
             continue
         torch.cuda.synchronize()
+        if not frag:
+            ref = y[:B].clone()
+        elif not torch.equal(ref, y[:B]):
+            row.append("FRAG MISMATCH")
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(30):
@@ -47,5 +56,5 @@ for spec in sys.argv[1:]:
         e.record()
         e.synchronize()
         t = s.elapsed_time(e) / 30 * 1e3
-        row.append(f"B{B}: {t:.1f}")
+        row.append(f"B{B}{'f' if frag else ''}: {t:.1f}")
     print(f"k{k}s{S} {H} {K}->{Nc} id {tid}: " + "  ".join(row), flush=True)
