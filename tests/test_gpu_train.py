@@ -285,10 +285,11 @@ def test_conv_wgrad1_fp32_tiles(tile, cin0, cin1, up1, cout, H, W, B, dyc):
     x0 = torch.randn(B, H, W, cin0, generator=g)
     x1 = torch.randn(B, H >> up1, W >> up1, cin1, generator=g) if cin1 else None
     dy = torch.randn(B, H, W, dyc, generator=g)
-    srcs = [src(x0.cuda())]
+    keep = [x0.cuda(), dy.cuda()] + ([x1.cuda()] if cin1 else [])  # the Src structs hold raw pointers
+    srcs = [src(keep[0])]
     if cin1:
-        srcs.append(src(x1.cuda(), up=up1))
-    dw = wgrad(torch.float32, srcs, src(dy.cuda()), cout, cin0 + cin1, 1, 1, 0, (H, W), (H, W), B, tile=tile)
+        srcs.append(src(keep[2], up=up1))
+    dw = wgrad(torch.float32, srcs, src(keep[1]), cout, cin0 + cin1, 1, 1, 0, (H, W), (H, W), B, tile=tile)
     torch.cuda.synchronize()
     xin = x0.permute(0, 3, 1, 2)
     if cin1:
@@ -305,7 +306,7 @@ def test_conv_wgrad1_fp32_rejects_3x3():
     """tiles 17-20 are 1x1 only: a 3x3 descriptor is refused (NotImplementedError)."""
     x = torch.randn(1, 8, 8, 32).cuda()
     dy = torch.randn(1, 8, 8, 32).cuda()
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(NotImplementedError):  # x / dy stay referenced for the raw Src pointers
         wgrad(torch.float32, [src(x)], src(dy), 32, 32, 3, 1, 1, (8, 8), (8, 8), 1, tile=17)
 
 
