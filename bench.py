@@ -330,6 +330,10 @@ def main_train(args, world, rank):
     dt_max = max_over_ranks(dt, world)
     gpu_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     loss = float(out["total_loss"].detach())
+    from yolox_amd import train as _T
+    if _T._LAUNCH_LOG is not None and rank == 0:  # diagnostic: conv / wgrad launches of every step
+        with open(os.environ["YOLOX_AMD_TRAIN_LOG"], "w") as f:
+            json.dump({"steps": args.warmup + args.steps, "launches": _T._LAUNCH_LOG}, f)
     if rank != 0:
         if world > 1:
             import torch.distributed as dist

@@ -560,17 +560,20 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
                           (tile > 32 && tile <= 32 + kNumRowTiles) || (tile > 64 && tile <= 64 + kNumPwTiles) ||
                           (tile > 80 && tile <= 80 + kNumPwrTiles) || (tile > 96 && tile <= 96 + kNumPwfTiles) ||
                           (tile > 112 && tile <= 112 + kNumR3Tiles) || (tile > 160 && tile <= 160 + kNumWsTiles) ||
-                          (tile > 200 && tile <= 200 + kNumWs1Tiles),
+                          (tile > 200 && tile <= 200 + kNumWs1Tiles) || (tile > 210 && tile <= 210 + kNumPw1fTiles) ||
+                          (tile > 214 && tile <= 214 + kNumDgradS2Tiles),
                       "tile %d", d->tile);
         YXH_CHECK_ARG(want_ks == 1 || ks == 2, "2-slab staging not possible for this conv");
         ks = want_ks;
     }
     const int kstage = 4 * ks * epc;
     p.ncb = (d->cin + kstage - 1) / kstage;
+    if (tile > 214) return dgrad_s2f_dispatch(dt, tile - 214, p, st);
     if (dilated && tile > 16) {
         set_error("dilated (upsample == 2) sources run on the register-staged kernel only (tile ids 1-9)");
         return YXH_EUNSUPPORTED;
     }
+    if (tile > 210) return conv_pw1f_dispatch(dt, tile - 210, p, st);
     if (tile > 200) return conv_ws1_dispatch(dt, tile - 200, p, st);
     if (tile > 160) return conv_ws_dispatch(dt, tile - 160, p, st);
     if (tile > 112) return conv_r3_dispatch(dt, tile - 112, p, st);

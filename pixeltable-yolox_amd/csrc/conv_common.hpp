@@ -289,5 +289,11 @@ constexpr int kNumWsTiles = 36;  // 31..36: fused Bottleneck (pre_weight)
 // Weight-stationary persistent 1x1 conv over dense sources (conv_ws1.hip): tile ids 201..200+kNumWs1Tiles
 int conv_ws1_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumWs1Tiles = 10;
+// fp32 1x1 GEMM for the training path, k-minor MFMA operands (conv_pw1f.hip): tile ids 211..210+kNumPw1fTiles
+int conv_pw1f_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
+constexpr int kNumPw1fTiles = 4;
+// fp32 data gradient of a 3x3 s2 conv by output parity class (conv_pw1f.hip): tile ids 215..216
+int dgrad_s2f_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
+constexpr int kNumDgradS2Tiles = 2;
 
 }  // namespace yxh

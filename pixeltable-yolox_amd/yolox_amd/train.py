@@ -132,9 +132,11 @@ class GradBuffer:
 # tiles 1-10.  YOLOX_AMD_TRAIN_TUNE=0 keeps the by-shape defaults.
 CONV_TUNE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
                    for k in (0, 1)]
-CONV_TUNE_TILES_F32 = CONV_TUNE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)]
+CONV_TUNE_TILES_F32 = CONV_TUNE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)] + [2 * i for i in range(211, 217)]
 WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 21))
 _TRAIN_TILES: dict = {}
+# diagnostic (tools/train_shapes.py): every conv / wgrad launch of the training step, in order
+_LAUNCH_LOG: Optional[list] = [] if os.environ.get("YOLOX_AMD_TRAIN_LOG") else None
 
 
 def _src_key(s: N.Src) -> tuple:
@@ -168,6 +170,7 @@ class TrainGraph:
         # data-gradient input slice, recording each as a yxh_pack_job; later steps repack
         # everything in ONE yxh_pack_weights_batch launch at the start of the forward
         self._dgrad_w: dict = {}
+        self._dgrad_ptrs: set = set()  # data pointers of the dgrad weight buffers (launch log only)
         self._pack_jobs: dict = {}  # key -> (PackJob, (weight, bias) tensors it reads)
         self._pack_table = None     # (device job table, njobs, total blocks, signature)
         self._batched = False       # this step's repacks were done by the batch launch
@@ -262,6 +265,9 @@ class TrainGraph:
         d.tile = self._tile(key, d, self.lib.yxh_conv2d, "dst", batch * dst_bs * (4 if dst_f32 else self.esize),
                             CONV_TUNE_TILES_F32 if self.dtype == torch.float32 else CONV_TUNE_TILES)
         self._chk(self.lib.yxh_conv2d(C.byref(d), self.stream), "conv")
+        if _LAUNCH_LOG is not None:
+            _LAUNCH_LOG.append(("dgrad" if weight in self._dgrad_ptrs else "conv", k, stride, cin, cout, in_h, in_w,
+                                out_h, out_w, batch, d.tile, len(srcs), int(srcs[0].upsample), int(accumulate)))
 
     def _wgrad(self, srcs: list, cin: int, cin_store: int, cout: int, k: int, stride: int, pad: int, dy: N.Src,
                dw: torch.Tensor, in_h: int, in_w: int, out_h: int, out_w: int, batch: int) -> None:
@@ -278,6 +284,9 @@ class TrainGraph:
                _src_key(dy)) + tuple(_src_key(q) for q in srcs)
         d.tile = self._tile(key, d, self.lib.yxh_conv_wgrad, "dw", cout * cin_store * k * k * 4, WGRAD_TUNE_TILES)
         self._chk(self.lib.yxh_conv_wgrad(C.byref(d), self.stream), "wgrad")
+        if _LAUNCH_LOG is not None:
+            _LAUNCH_LOG.append(("wgrad", k, stride, cin, cout, in_h, in_w, out_h, out_w, batch, d.tile, len(srcs),
+                                int(srcs[0].upsample), 0))
 
     def _tile(self, key: tuple, d, fn, out_field: str, out_bytes: int, candidates: list, reps: int = 3) -> int:
         """The cached tile for this shape, or the fastest candidate timed now (writing to
@@ -331,6 +340,7 @@ class TrainGraph:
             if wt is None:
                 wt = torch.empty(cs * kh * kh * cout_pad, dtype=self.dtype, device=self.device)
                 self._dgrad_w[key] = wt
+                self._dgrad_ptrs.add(wt.data_ptr())
             if not (self._batched and key in self._pack_jobs):
                 self._chk(self.lib.yxh_pack_dgrad_weight(
                     conv.weight.detach().data_ptr(), conv.out_channels, conv.in_channels, kh, kh, cb, cs, cout_pad,

@@ -736,6 +736,42 @@ def test_pack_frag_layout():
         n.check(n.lib().yxh_pack_frag(w.data_ptr(), 40, taps, cin, n.BF16, out.data_ptr(), n.stream_ptr()))
 
 
+PW1F_GEOMS = [  # sources (channels, upsample), cout, H, W (output), batch
+    ([(64, 0)], 64, 20, 24, 2), ([(128, 0)], 85, 8, 10, 2), ([(48, 0), (48, 0)], 64, 10, 14, 3),
+    ([(64, 1), (64, 0)], 128, 8, 12, 2), ([(512, 0)], 256, 5, 7, 4), ([(32, 0)], 32, 40, 40, 2)]
+
+
+@pytest.mark.parametrize("geom", PW1F_GEOMS)
+def test_conv_pw1f_fp32(geom):
+    """conv_pw1f (ids 211-214): fp32 1x1 GEMM of the training path vs torch fp32 -- one or two
+    sources (the first nearest-x2 upsampled), cout tails (the head preds' 85), a channel-slice
+    destination, and YXH_CONV_ACCUMULATE (data gradients add into the input gradient)."""
+    srcs, cout, H, W, B = geom
+    cin = sum(c for c, _ in srcs)
+    conv, bn = make_conv(cin, cout, 1, 1, seed=cin + cout)
+    g = torch.Generator().manual_seed(H * W + cin)
+    parts, bufs = [], []
+    for c, up in srcs:
+        x = torch.randn(B, c, H >> up, W >> up, generator=g)
+        parts.append(F.interpolate(x, scale_factor=2, mode="nearest") if up else x)
+        bufs.append((nhwc(x, torch.float32), 0, c, up))
+    want = ref_conv(torch.cat(parts, 1), conv, bn, "silu")
+    ran = 0
+    cpad = (cout + 3) // 4 * 4 + 8  # 16-byte pixel rows (the kernel's store granule)
+    for tid in range(211, 215):
+        out = torch.zeros(B, H, W, cpad, dtype=torch.float32, device=DEV)
+        y = run_conv(bufs, conv, bn, torch.float32, out=out, out_coff=4, tile=2 * tid)
+        close(y[..., 4:4 + cout].permute(0, 3, 1, 2), want, torch.float32)
+        assert not y[..., :4].any() and not y[..., 4 + cout:].any()
+        out.fill_(0.25)  # accumulate onto it (no activation: a data gradient)
+        y = run_conv(bufs, conv, bn, torch.float32, act="none", out=out, out_coff=4, tile=2 * tid,
+                     flags=N().CONV_ACCUMULATE)
+        close(y[..., 4:4 + cout].permute(0, 3, 1, 2) - 0.25, ref_conv(torch.cat(parts, 1), conv, bn, "none"),
+              torch.float32)
+        ran += 1
+    assert ran == 4
+
+
 @pytest.mark.parametrize("ch,H,W,B", [(32, 37, 45, 2), (64, 40, 24, 3), (128, 20, 22, 4), (64, 80, 80, 4)])
 @pytest.mark.parametrize("shortcut", [True, False])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])

@@ -310,6 +310,45 @@ def test_conv_wgrad1_fp32_rejects_3x3():
         wgrad(torch.float32, [src(x)], src(dy), 32, 32, 3, 1, 1, (8, 8), (8, 8), 1, tile=17)
 
 
+@pytest.mark.parametrize("tile", [215, 216])
+@pytest.mark.parametrize("cin,cout,H,W,B", [(32, 64, 16, 20, 2), (64, 128, 10, 8, 3), (128, 256, 8, 8, 2),
+                                           (96, 40, 12, 6, 2)])
+def test_dgrad_stride2_parity_classes(tile, cin, cout, H, W, B):
+    """fp32 data gradient of a 3x3 s2 p1 conv by output parity class (tiles 215-216: 1, 2, 2, 4 taps
+    per class instead of nine taps over a zero-dilated dy) vs torch autograd, accumulating onto an
+    existing gradient into a channel slice of a wider buffer; the dilated register-staged tile
+    agrees."""
+    from yolox_amd import _native as N
+    from yolox_amd.train import dense_src
+    g = torch.Generator().manual_seed(cin + cout + H + tile)
+    oh, ow = H // 2, W // 2
+    dy = torch.randn(B, oh, ow, cout, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * 0.1
+    dyd, wtd = dy.cuda(), wt.cuda()
+    pk = torch.empty(cin * 9 * cout, device="cuda")
+    chk(lib().yxh_pack_dgrad_weight(wtd.data_ptr(), cout, cin, 3, 3, 0, cin, cout, 0, pk.data_ptr(), stream()))
+    zb = torch.zeros(cin, device="cuda")
+    outs = []
+    for t in (tile, 2):
+        dx = torch.full((B, H, W, cin + 8), 0.5, device="cuda")
+        d = N.ConvDesc()
+        d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w = 0, B, H, W, H, W
+        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.groups, d.nsrc = cout, cin, 3, 3, 1, 1, 1, 1
+        d.src[0] = dense_src(dyd, up=2)
+        d.weight, d.bias, d.dst, d.dst_dtype = pk.data_ptr(), zb.data_ptr(), dx.data_ptr() + 4 * 4, 0
+        d.dst_cstride, d.dst_bstride, d.act, d.flags = cin + 8, H * W * (cin + 8), 0, N.CONV_ACCUMULATE
+        d.tile = 2 * t
+        chk(lib().yxh_conv2d(C.byref(d), stream()))
+        torch.cuda.synchronize()
+        outs.append(dx.cpu())
+    got, dil = outs
+    assert (got[..., :4] == 0.5).all() and (got[..., 4 + cin:] == 0.5).all()
+    x = torch.zeros(B, cin, H, W, requires_grad=True)
+    F.conv2d(x, wt, stride=2, padding=1).backward(dy.permute(0, 3, 1, 2))
+    assert rel(got[..., 4:4 + cin] - 0.5, x.grad.permute(0, 2, 3, 1)) < 1e-5
+    assert rel(got[..., 4:4 + cin], dil[..., 4:4 + cin]) < 1e-5
+
+
 def test_wgrad_cin_store_and_strided_dy():
     """Focus stem: 16 packed channels, gradient of the 12 real ones; dy read through a
     strided view (the head's [B, A, 8] pred-gradient rows)."""
