@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 13
+#define YXH_ABI_VERSION 14
 
 enum yxh_status {
     YXH_OK = 0,
@@ -367,11 +367,16 @@ typedef struct {
     yxh_src src[2];
     yxh_src dy;
     float* dw;
-    int32_t tile, reserved;  /* tile 0: by shape; 17-20 (fp32 1x1 s1): k-major MFMA operands, 64x64, 128x128,
+    int32_t tile, reserved;  /* tile 0: by shape; 17-20 (fp32, any kernel / stride): k-major MFMA operands,
+                                one tap per block, 64x64, 128x128,
                                 128x64, 64x128; 1-4: 64x64, 128x128, 32x64, 16x64 (cout x cin,
                                 register-transposed loader); 5-10 (bf16/f16): LDS-DMA +
                                 ds_read_b64_tr_b16, 128x128 (3 / 2 buffers), 64x64 (3 / 2),
                                 128x64, 64x128 */
+    /* fp32 tiles 17-20: optional scratch for per-split partial gradients; with it the splits are
+     * summed by a second launch in a fixed order (deterministic, no atomics) */
+    float* workspace;
+    int64_t workspace_bytes;
 } yxh_wgrad_desc;
 int yxh_conv_wgrad(const yxh_wgrad_desc* d, void* stream);
 

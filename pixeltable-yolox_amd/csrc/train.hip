@@ -358,6 +358,8 @@ struct WgradParams {
     int sps, nst;  // stages per split, total pixel stages
     int ntc;       // channel tiles per tap
     int dych;      // channels of the dy view (loads past them read the zero chunk)
+    float* ws;     // fp32 tiles 17-20: per-split partial dW (yxh_wgrad_desc.workspace), or null
+    long long ws_elems;
 };
 
 __device__ __attribute__((aligned(16))) uint4 g_wg_zero[4];
@@ -941,18 +943,19 @@ __global__ __launch_bounds__(256) void conv_wgrad2(WgradParams p) {
         }
 }
 
-// ------------------------------------------------------------------ fp32 1x1 weight gradient
-// dW[n][c] += sum over pixels p of dY[p][n] * X[p][c] for 1x1 s1 convs in fp32 (the CSP /
-// SPP / PAFPN / head-stem 1x1 BaseConvs and the head preds).  Both operands are pixel-major,
-// which is exactly the k-major operand form of v_mfma_f32_16x16x4_f32 (lane l: A[l % 16][l / 16]
-// = dY[p0 + l / 16][n0 + l % 16], B likewise from X): no transposes.  A block owns a TN x TC
-// tile of dW over a range of KP-pixel stages (split-K over pixels); per stage both [KP][TN] and
-// [KP][TC] slabs are staged through LDS by 16-byte register loads (rows padded by 16 floats:
-// the four 16-lane row groups of a ds_read_b32 hit distinct banks), double-buffered so the next
-// stage's loads fly under this stage's MFMAs; the block's partial dW goes out with hardware
-// fp32 atomics (dW pre-zeroed, as for conv_wgrad).
+// ------------------------------------------------------------------ fp32 weight gradient
+// dW[n][c][tap] += sum over output pixels p of dY[p][n] * X[in(p, tap)][c] for fp32 convs (any
+// kh x kw, stride, pad; the 1x1 and 3x3 BaseConvs of the training step).  Both operands are
+// pixel-major, which is exactly the k-major operand form of v_mfma_f32_16x16x4_f32 (lane l:
+// A[l % 16][l / 16] = dY[p0 + l / 16][n0 + l % 16], B likewise from X at the tap's input pixel,
+// zero outside the image): no transposes.  A block owns a TN x TC tile of ONE tap over a range of
+// KP-pixel stages (split-K over pixels); per stage both slabs are staged through LDS by 16-byte
+// register loads (rows padded by 16 floats: the four 16-lane row groups of a ds_read_b32 hit
+// distinct banks), double-buffered.  With a workspace each split stores its partial dW plainly
+// and wgrad_reduce sums the splits in a fixed order (deterministic, no cross-XCD atomics);
+// without one the partials go out as fp32 atomics (dW pre-zeroed, as for conv_wgrad).
 template <int TN, int TC, int WN, int WC, int KP>
-__global__ __launch_bounds__(256) void wgrad1_f32(WgradParams p) {
+__global__ __launch_bounds__(256) void wgrad_f32(WgradParams p) {
     static_assert(WN * WC == 4, "4 waves");
     constexpr int WTN = TN / WN, WTC = TC / WC, FN = WTN / 16, FC = WTC / 16;
     constexpr int TNP = TN + 16, TCP = TC + 16;
@@ -961,9 +964,11 @@ __global__ __launch_bounds__(256) void wgrad1_f32(WgradParams p) {
     __shared__ __attribute__((aligned(16))) float lds[2][ASZ + BSZ];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wn = wave % WN, wc = wave / WN;
-    const int n0 = blockIdx.y * TN, c0 = blockIdx.z * TC;
+    const int taps = p.kh * p.kw;
+    const int tap = (int)blockIdx.z % taps, ct = (int)blockIdx.z / taps;
+    const int ty = tap / p.kw, tx = tap - ty * p.kw;
+    const int n0 = blockIdx.y * TN, c0 = ct * TC;
     const int st0 = blockIdx.x * p.sps, st1 = min(p.nst, st0 + p.sps);
-    if (st0 >= st1) return;  // block-uniform
     const int M = p.M, ohw = p.ohw, ow = p.out_w, cout = p.cout, cin = p.cin;
     const float* dy = (const float*)p.dy;
     const bool dy_dense = p.dybs == (long long)ohw * p.dycs;
@@ -996,15 +1001,15 @@ __global__ __launch_bounds__(256) void wgrad1_f32(WgradParams p) {
             const int m = pb + row, c = c0 + col * 4;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (q < BCH && m < M && c < cin) {
-                const int s = (p.nsrc > 1 && c >= p.src0_ch) ? 1 : 0;
-                const int cc = s ? c - p.src0_ch : c;
                 const int b = m / ohw, pix = m - b * ohw;
-                int spix = pix;
-                if (p.sup[s]) {
-                    const int y = pix / ow, x = pix - y * ow;
-                    spix = (y >> 1) * p.sw[s] + (x >> 1);
+                const int oy = pix / ow, ox = pix - oy * ow;
+                const int iy = oy * p.stride + ty - p.pad, ix = ox * p.stride + tx - p.pad;
+                if ((unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w) {
+                    const int s = (p.nsrc > 1 && c >= p.src0_ch) ? 1 : 0;
+                    const int cc = s ? c - p.src0_ch : c;
+                    const int spix = p.sup[s] ? (iy >> 1) * p.sw[s] + (ix >> 1) : iy * p.sw[s] + ix;
+                    v = *(const float4*)((const float*)p.sptr[s] + (long long)b * p.sbs[s] + (long long)spix * p.scs[s] + cc);
                 }
-                v = *(const float4*)((const float*)p.sptr[s] + (long long)b * p.sbs[s] + (long long)spix * p.scs[s] + cc);
             }
             rb[i] = v;
         }
@@ -1032,9 +1037,11 @@ __global__ __launch_bounds__(256) void wgrad1_f32(WgradParams p) {
 #pragma unroll
         for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int kr = lane >> 4, kc = lane & 15;
-    gload(st0);
-    lstore(0);
-    __syncthreads();
+    if (st0 < st1) {
+        gload(st0);
+        lstore(0);
+        __syncthreads();
+    }
     int buf = 0;
     for (int st = st0; st < st1; ++st) {
         const bool more = st + 1 < st1;
@@ -1058,6 +1065,7 @@ __global__ __launch_bounds__(256) void wgrad1_f32(WgradParams p) {
         buf ^= 1;
     }
     // D[m][n] of fragment (i, j): lane holds rows 4 (lane / 16) + r, column lane % 16
+    float* out = p.ws ? p.ws + (long long)blockIdx.x * p.cout * p.cin_store * taps : p.dw;
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -1066,9 +1074,21 @@ __global__ __launch_bounds__(256) void wgrad1_f32(WgradParams p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int n = n0 + wn * WTN + 16 * i + 4 * kr + r;
-                if (n < cout && c < p.cin_store) unsafeAtomicAdd(p.dw + (long long)n * p.cin_store + c, acc[i][j][r]);
+                if (n >= cout || c >= p.cin_store) continue;
+                float* d = out + ((long long)n * p.cin_store + c) * taps + tap;
+                if (p.ws) *d = acc[i][j][r];
+                else unsafeAtomicAdd(d, acc[i][j][r]);
             }
         }
+}
+
+// dW[i] += sum over the splits of ws[split][i], in split order (deterministic)
+__global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, int splits, long long ne, float* dw) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= ne) return;
+    float s = 0.0f;
+    for (int k = 0; k < splits; ++k) s += ws[(long long)k * ne + i];
+    dw[i] += s;
 }
 
 // dgrad weights: w [cout][cin][kh][kw] fp32 -> [c_count][kh][kw][cout_pad] of T, taps
@@ -1449,27 +1469,32 @@ int launch_wgrad2_t(WgradParams p, hipStream_t st) {
 }
 
 template <int TN, int TC, int WN, int WC, int KP>
-int launch_wgrad1_f32(WgradParams p, hipStream_t st) {
-    if (p.kh != 1 || p.kw != 1 || p.stride != 1 || p.pad != 0) {
-        set_error("wgrad tiles 17-20 (fp32 1x1) need a 1x1 s1 p0 conv");
-        return YXH_EUNSUPPORTED;
-    }
-    if ((p.nsrc > 1 && p.src0_ch % 4) || p.dycs % 4 || p.dybs % 4) {
+int launch_wgrad_f32(WgradParams p, hipStream_t st) {
+    if ((p.nsrc > 1 && p.src0_ch % 4) || p.dycs % 4 || p.dybs % 4 || p.cin % 4) {
         set_error("wgrad tiles 17-20: 16-byte channel chunks");
         return YXH_EUNSUPPORTED;
     }
+    const int taps = p.kh * p.kw;
     const int ntn = (p.cout + TN - 1) / TN, ntc = (p.cin + TC - 1) / TC;
     p.nst = (int)(((long long)p.M + KP - 1) / KP);
-    const long long tiles = (long long)ntn * ntc;
-    long long splits = (512 + tiles - 1) / tiles;  // about two blocks per CU
+    const long long tiles = (long long)ntn * ntc * taps;
+    long long splits = (768 + tiles - 1) / tiles;  // about three blocks per CU
     const long long max_splits = (p.nst + 3) / 4;  // >= 4 stages per split
     if (splits > max_splits) splits = max_splits;
+    const long long ne = (long long)p.cout * p.cin_store * taps;
+    if (p.ws && splits > p.ws_elems / ne) splits = p.ws_elems / ne;  // the workspace holds every split
     if (splits < 1) splits = 1;
     p.sps = (int)((p.nst + splits - 1) / splits);
     splits = (p.nst + p.sps - 1) / p.sps;
-    YXH_CHECK_ARG(ntn < 65536 && ntc < 65536, "wgrad grid");
-    hipLaunchKernelGGL((wgrad1_f32<TN, TC, WN, WC, KP>), dim3((unsigned)splits, ntn, ntc), dim3(256), 0, st, p);
-    YXH_CHECK_LAUNCH("wgrad1_f32");
+    if (p.ws && splits * ne > p.ws_elems) p.ws = nullptr;  // too small even for one split: atomics
+    YXH_CHECK_ARG(ntn < 65536 && ntc * taps < 65536, "wgrad grid");
+    hipLaunchKernelGGL((wgrad_f32<TN, TC, WN, WC, KP>), dim3((unsigned)splits, ntn, ntc * taps), dim3(256), 0, st, p);
+    YXH_CHECK_LAUNCH("wgrad_f32");
+    if (p.ws) {
+        hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, (const float*)p.ws,
+                           (int)splits, ne, p.dw);
+        YXH_CHECK_LAUNCH("wgrad_reduce");
+    }
     return YXH_OK;
 }
 
@@ -1509,14 +1534,14 @@ int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
             }
         case 17: case 18: case 19: case 20:
             if constexpr (sizeof(T) != 4) {
-                set_error("wgrad tiles 17-20 (1x1, k-major MFMA operands) are built for fp32 only");
+                set_error("wgrad tiles 17-20 (k-major MFMA operands) are built for fp32 only");
                 return YXH_EUNSUPPORTED;
             } else {
                 switch (tile) {
-                    case 17: return launch_wgrad1_f32<64, 64, 2, 2, 32>(p, st);
-                    case 18: return launch_wgrad1_f32<128, 128, 2, 2, 16>(p, st);
-                    case 19: return launch_wgrad1_f32<128, 64, 2, 2, 32>(p, st);
-                    default: return launch_wgrad1_f32<64, 128, 2, 2, 32>(p, st);
+                    case 17: return launch_wgrad_f32<64, 64, 2, 2, 32>(p, st);
+                    case 18: return launch_wgrad_f32<128, 128, 2, 2, 16>(p, st);
+                    case 19: return launch_wgrad_f32<128, 64, 2, 2, 32>(p, st);
+                    default: return launch_wgrad_f32<64, 128, 2, 2, 32>(p, st);
                 }
             }
         default: set_error("wgrad tile %d", tile); return YXH_EINVAL;
@@ -1577,6 +1602,9 @@ int conv_wgrad_launch(const yxh_wgrad_desc* d, hipStream_t st) {
     p.dw = d->dw;
     p.cin_store = d->cin_store;
     p.dych = g.channels;
+    YXH_CHECK_ARG(!d->workspace || a16(d->workspace), "wgrad workspace alignment");
+    p.ws = (float*)d->workspace;
+    p.ws_elems = d->workspace ? d->workspace_bytes / 4 : 0;
     if (dt == YXH_BF16) return wgrad_tile<bf16>(d->tile, p, st);
     if (dt == YXH_F16) return wgrad_tile<f16>(d->tile, p, st);
     return wgrad_tile<float>(d->tile, p, st);

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -83,7 +83,8 @@ class WgradDesc(C.Structure):
                 ("out_h", C.c_int32), ("out_w", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32),
                 ("kh", C.c_int32), ("kw", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32),
                 ("nsrc", C.c_int32), ("cin_store", C.c_int32), ("src", Src * 2), ("dy", Src),
-                ("dw", C.c_void_p), ("tile", C.c_int32), ("reserved", C.c_int32)]
+                ("dw", C.c_void_p), ("tile", C.c_int32), ("reserved", C.c_int32), ("workspace", C.c_void_p),
+                ("workspace_bytes", C.c_int64)]
 
 
 class FocusDesc(C.Structure):

@@ -166,6 +166,8 @@ class TrainGraph:
         self.grad_total = torch.ones((), dtype=torch.float32, device=self.device)
         self.tune = os.environ.get("YOLOX_AMD_TRAIN_TUNE", "1") != "0"
         self._scratch = torch.empty(0, dtype=torch.uint8, device=self.device)
+        # per-split partial weight gradients of the fp32 wgrad tiles (summed in a fixed order)
+        self.wg_ws = torch.empty(64 << 20, dtype=torch.uint8, device=self.device)
         # weight repacks: the first step launches one pack per conv (forward layout) and per
         # data-gradient input slice, recording each as a yxh_pack_job; later steps repack
         # everything in ONE yxh_pack_weights_batch launch at the start of the forward
@@ -280,6 +282,7 @@ class TrainGraph:
             d.src[j] = s
         d.dy = dy
         d.dw = dw.data_ptr()
+        d.workspace, d.workspace_bytes = self.wg_ws.data_ptr(), self.wg_ws.numel()
         key = ("wgrad", self.dcode, batch, in_h, in_w, out_h, out_w, cin, cin_store, cout, k, stride, pad,
                _src_key(dy)) + tuple(_src_key(q) for q in srcs)
         d.tile = self._tile(key, d, self.lib.yxh_conv_wgrad, "dw", cout * cin_store * k * k * 4, WGRAD_TUNE_TILES)

@@ -120,7 +120,7 @@ def test_bn_act_bwd(dtype, B, H, W, Cc, act):
 
 
 # ----------------------------------------------------------------- conv gradients
-def wgrad(dtype, srcs, dy, cout, cin, k, s, p, in_hw, out_hw, B, cin_store=None, tile=0):
+def wgrad(dtype, srcs, dy, cout, cin, k, s, p, in_hw, out_hw, B, cin_store=None, tile=0, ws_bytes=0):
     from yolox_amd import _native as N
     d = N.WgradDesc()
     d.dtype, d.batch = DT[dtype], B
@@ -134,7 +134,11 @@ def wgrad(dtype, srcs, dy, cout, cin, k, s, p, in_hw, out_hw, B, cin_store=None,
     dw = torch.zeros(cout, cin_store or cin, k, k, device="cuda")
     d.dw = dw.data_ptr()
     d.tile = tile
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device="cuda") if ws_bytes else None
+    if ws is not None:
+        d.workspace, d.workspace_bytes = ws.data_ptr(), ws_bytes
     chk(lib().yxh_conv_wgrad(C.byref(d), stream()))
+    torch.cuda.synchronize()
     return dw
 
 
@@ -268,85 +272,54 @@ def test_conv_wgrad9_fp32_tiles(tile, cin0, cin1, up1, cout, k, s, H, B):
     assert rel(dw, wr.grad) < 1e-4
 
 
-WG1_CASES = [  # cin0, cin1, up1, cout, H, W, B, dy channels (>= cout, a strided dy view when larger)
-    (64, 0, 0, 64, 16, 20, 2, 64), (64, 64, 1, 128, 8, 12, 2, 128), (256, 0, 0, 192, 23, 17, 2, 192),
-    (48, 48, 0, 64, 10, 14, 3, 64), (128, 0, 0, 85, 6, 10, 2, 88), (512, 0, 0, 256, 5, 5, 4, 264),
-    (32, 0, 0, 32, 160, 160, 1, 32),
+WGF_CASES = [  # cin0, cin1, up1, cout, k, s, H, W, B, dy channels (>= cout: a strided dy view when larger)
+    (64, 0, 0, 64, 1, 1, 16, 20, 2, 64), (64, 64, 1, 128, 1, 1, 8, 12, 2, 128), (256, 0, 0, 192, 1, 1, 23, 17, 2, 192),
+    (48, 48, 0, 64, 1, 1, 10, 14, 3, 64), (128, 0, 0, 85, 1, 1, 6, 10, 2, 88), (512, 0, 0, 256, 1, 1, 5, 5, 4, 264),
+    (32, 0, 0, 32, 1, 1, 160, 160, 1, 32), (64, 0, 0, 64, 3, 1, 20, 16, 2, 64), (128, 0, 0, 128, 3, 1, 9, 11, 2, 128),
+    (32, 0, 0, 64, 3, 2, 20, 18, 2, 64), (96, 32, 0, 136, 3, 2, 17, 15, 2, 136), (16, 0, 0, 32, 3, 1, 24, 20, 1, 32),
 ]
 
 
+@pytest.mark.parametrize("ws", [0, 8 << 20, 4096])
 @pytest.mark.parametrize("tile", [17, 18, 19, 20])
-@pytest.mark.parametrize("cin0,cin1,up1,cout,H,W,B,dyc", WG1_CASES)
-def test_conv_wgrad1_fp32_tiles(tile, cin0, cin1, up1, cout, H, W, B, dyc):
-    """fp32 1x1 weight gradient on k-major MFMA operands (tiles 17-20) against torch autograd:
-    pixel tails of the KP-pixel stages, cout / cin tails of the tile (the head preds' 85 rows of
-    an 88-channel dy), two sources with the second upsampled, a wide dy read as a strided view."""
-    g = torch.Generator().manual_seed(cin0 * 3 + cout + H + tile)
+@pytest.mark.parametrize("cin0,cin1,up1,cout,k,s,H,W,B,dyc", WGF_CASES)
+def test_conv_wgrad_fp32_kmajor_tiles(ws, tile, cin0, cin1, up1, cout, k, s, H, W, B, dyc):
+    """fp32 weight gradient on k-major MFMA operands (tiles 17-20, one tap per block) against torch
+    autograd: 1x1 and 3x3 (stride 1 / 2, zero padding), pixel tails of the KP-pixel stages, cout /
+    cin tails (the head preds' 85 rows of an 88-channel dy), two sources with the second upsampled,
+    a wide dy read as a strided view; per-split partials through a workspace (summed in a fixed
+    order), a workspace too small for them (falls back to atomics) and none (atomics)."""
+    g = torch.Generator().manual_seed(cin0 * 3 + cout + H + tile + k)
+    p = (k - 1) // 2
+    oh, ow = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
     x0 = torch.randn(B, H, W, cin0, generator=g)
     x1 = torch.randn(B, H >> up1, W >> up1, cin1, generator=g) if cin1 else None
-    dy = torch.randn(B, H, W, dyc, generator=g)
+    dy = torch.randn(B, oh, ow, dyc, generator=g)
     keep = [x0.cuda(), dy.cuda()] + ([x1.cuda()] if cin1 else [])  # the Src structs hold raw pointers
     srcs = [src(keep[0])]
     if cin1:
         srcs.append(src(keep[2], up=up1))
-    dw = wgrad(torch.float32, srcs, src(keep[1]), cout, cin0 + cin1, 1, 1, 0, (H, W), (H, W), B, tile=tile)
-    torch.cuda.synchronize()
+    dw = wgrad(torch.float32, srcs, src(keep[1]), cout, cin0 + cin1, k, s, p, (H, W), (oh, ow), B, tile=tile,
+               ws_bytes=ws)
     xin = x0.permute(0, 3, 1, 2)
     if cin1:
         x1n = x1.permute(0, 3, 1, 2)
         if up1:
             x1n = F.interpolate(x1n, scale_factor=2, mode="nearest")
         xin = torch.cat([xin, x1n], 1)
-    wr = torch.zeros(cout, cin0 + cin1, 1, 1, requires_grad=True)
-    F.conv2d(xin, wr).backward(dy[..., :cout].permute(0, 3, 1, 2))
+    wr = torch.zeros(cout, cin0 + cin1, k, k, requires_grad=True)
+    F.conv2d(xin, wr, stride=s, padding=p).backward(dy[..., :cout].permute(0, 3, 1, 2))
     assert rel(dw, wr.grad) < 1e-5
 
 
-def test_conv_wgrad1_fp32_rejects_3x3():
-    """tiles 17-20 are 1x1 only: a 3x3 descriptor is refused (NotImplementedError)."""
-    x = torch.randn(1, 8, 8, 32).cuda()
-    dy = torch.randn(1, 8, 8, 32).cuda()
-    with pytest.raises(NotImplementedError):  # x / dy stay referenced for the raw Src pointers
-        wgrad(torch.float32, [src(x)], src(dy), 32, 32, 3, 1, 1, (8, 8), (8, 8), 1, tile=17)
-
-
-@pytest.mark.parametrize("tile", [215, 216])
-@pytest.mark.parametrize("cin,cout,H,W,B", [(32, 64, 16, 20, 2), (64, 128, 10, 8, 3), (128, 256, 8, 8, 2),
-                                           (96, 40, 12, 6, 2)])
-def test_dgrad_stride2_parity_classes(tile, cin, cout, H, W, B):
-    """fp32 data gradient of a 3x3 s2 p1 conv by output parity class (tiles 215-216: 1, 2, 2, 4 taps
-    per class instead of nine taps over a zero-dilated dy) vs torch autograd, accumulating onto an
-    existing gradient into a channel slice of a wider buffer; the dilated register-staged tile
-    agrees."""
-    from yolox_amd import _native as N
-    from yolox_amd.train import dense_src
-    g = torch.Generator().manual_seed(cin + cout + H + tile)
-    oh, ow = H // 2, W // 2
-    dy = torch.randn(B, oh, ow, cout, generator=g)
-    wt = torch.randn(cout, cin, 3, 3, generator=g) * 0.1
-    dyd, wtd = dy.cuda(), wt.cuda()
-    pk = torch.empty(cin * 9 * cout, device="cuda")
-    chk(lib().yxh_pack_dgrad_weight(wtd.data_ptr(), cout, cin, 3, 3, 0, cin, cout, 0, pk.data_ptr(), stream()))
-    zb = torch.zeros(cin, device="cuda")
-    outs = []
-    for t in (tile, 2):
-        dx = torch.full((B, H, W, cin + 8), 0.5, device="cuda")
-        d = N.ConvDesc()
-        d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w = 0, B, H, W, H, W
-        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.groups, d.nsrc = cout, cin, 3, 3, 1, 1, 1, 1
-        d.src[0] = dense_src(dyd, up=2)
-        d.weight, d.bias, d.dst, d.dst_dtype = pk.data_ptr(), zb.data_ptr(), dx.data_ptr() + 4 * 4, 0
-        d.dst_cstride, d.dst_bstride, d.act, d.flags = cin + 8, H * W * (cin + 8), 0, N.CONV_ACCUMULATE
-        d.tile = 2 * t
-        chk(lib().yxh_conv2d(C.byref(d), stream()))
-        torch.cuda.synchronize()
-        outs.append(dx.cpu())
-    got, dil = outs
-    assert (got[..., :4] == 0.5).all() and (got[..., 4 + cin:] == 0.5).all()
-    x = torch.zeros(B, cin, H, W, requires_grad=True)
-    F.conv2d(x, wt, stride=2, padding=1).backward(dy.permute(0, 3, 1, 2))
-    assert rel(got[..., 4:4 + cin] - 0.5, x.grad.permute(0, 2, 3, 1)) < 1e-5
-    assert rel(got[..., 4:4 + cin], dil[..., 4:4 + cin]) < 1e-5
+def test_conv_wgrad_fp32_workspace_is_deterministic():
+    """With a workspace the split partials are summed in a fixed order: two runs agree bit for bit."""
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(4, 40, 40, 128, generator=g).cuda()
+    dy = torch.randn(4, 40, 40, 128, generator=g).cuda()
+    a = wgrad(torch.float32, [src(x)], src(dy), 128, 128, 3, 1, 1, (40, 40), (40, 40), 4, tile=17, ws_bytes=32 << 20)
+    b = wgrad(torch.float32, [src(x)], src(dy), 128, 128, 3, 1, 1, (40, 40), (40, 40), 4, tile=17, ws_bytes=32 << 20)
+    assert torch.equal(a, b)
 
 
 def test_wgrad_cin_store_and_strided_dy():
