@@ -320,9 +320,12 @@ def main_train(args, world, rank):
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_s = 0.0  # time the host spends issuing a step (ctypes launches + tensor bookkeeping)
     for k in range(args.steps):
         evs[k][0].record(stream)
+        h0 = time.perf_counter()
         out = step()
+        host_s += time.perf_counter() - h0
         evs[k][1].record(stream)
     torch.cuda.synchronize()
     barrier(world)
@@ -368,6 +371,7 @@ def main_train(args, world, rank):
                      "frac": round(achieved / peak, 4), "traffic": None,
                      "algorithmic_flops_per_launch": flops, "step_gpu_ms": round(gpu_ms, 3)},
         "last_loss": round(loss, 4),
+        "host_issue_ms_per_step": round(host_s / args.steps * 1e3, 3),
     }
     if not args.no_cpu_baseline and world == 1:
         result["cpu_baseline"] = cpu_baseline_train(args, args.cpu_seconds)

@@ -1082,6 +1082,130 @@ __global__ __launch_bounds__(256) void wgrad_f32(WgradParams p) {
         }
 }
 
+// fp32 3x3 weight gradient with all nine taps per block: a stage is a row segment of KP output
+// pixels (image b, row oy, columns ox0 .. ox0 + KP); dY[KP][TN] and the three input rows it
+// reads, X[3][(KP - 1) s + 3][TC] (zero outside the image), are staged once, and every tap's
+// B operand is a shifted view of the X rows: dY and X are read once per stage instead of once
+// per tap.  acc[9][FN][FC] stays in registers for the block's pixel range; partials as wgrad_f32.
+template <int TN, int TC, int S, int KP>
+__global__ __launch_bounds__(256) void wgrad9t_f32(WgradParams p, int nseg) {
+    constexpr int WN = 2, WC = 2;
+    constexpr int WTN = TN / WN, WTC = TC / WC, FN = WTN / 16, FC = WTC / 16;
+    constexpr int XW = (KP - 1) * S + 3, TNP = TN + 16, TCP = TC + 16;
+    constexpr int ASZ = KP * TNP, BSZ = 3 * XW * TCP;
+    constexpr int ACH = KP * TN / 4, BCH = 3 * XW * TC / 4, AL = (ACH + 255) / 256, BL = (BCH + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float lds[2][ASZ + BSZ];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wn = wave % WN, wc = wave / WN;
+    const int n0 = blockIdx.y * TN, c0 = blockIdx.z * TC;
+    const int st0 = blockIdx.x * p.sps, st1 = min(p.nst, st0 + p.sps);
+    const int oh = p.out_h, ow = p.out_w, cout = p.cout, cin = p.cin;
+    const float* dy = (const float*)p.dy;
+
+    float4 ra[AL], rb[BL];
+    auto gload = [&](int st) {
+        const int seg = st % nseg, r = st / nseg;
+        const int b = r / oh, oy = r - b * oh, ox0 = seg * KP;
+#pragma unroll
+        for (int i = 0; i < AL; ++i) {
+            const int q = tid + 256 * i;
+            const int row = q / (TN / 4), col = q - row * (TN / 4);
+            const int ox = ox0 + row, n = n0 + col * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q < ACH && ox < ow && n < cout)
+                v = *(const float4*)(dy + (long long)b * p.dybs + (long long)(oy * ow + ox) * p.dycs + n);
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BL; ++i) {
+            const int q = tid + 256 * i;
+            const int row = q / (TC / 4), col = q - row * (TC / 4);  // row = ty * XW + xx
+            const int ty = row / XW, xx = row - ty * XW;
+            const int iy = oy * S + ty - 1, ix = ox0 * S + xx - 1, c = c0 + col * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q < BCH && c < cin && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w) {
+                const int s = (p.nsrc > 1 && c >= p.src0_ch) ? 1 : 0;
+                const int cc = s ? c - p.src0_ch : c;
+                const int spix = p.sup[s] ? (iy >> 1) * p.sw[s] + (ix >> 1) : iy * p.sw[s] + ix;
+                v = *(const float4*)((const float*)p.sptr[s] + (long long)b * p.sbs[s] + (long long)spix * p.scs[s] + cc);
+            }
+            rb[i] = v;
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < AL; ++i) {
+            const int q = tid + 256 * i;
+            if (q < ACH) *(float4*)(lds[buf] + (q / (TN / 4)) * TNP + (q % (TN / 4)) * 4) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BL; ++i) {
+            const int q = tid + 256 * i;
+            if (q < BCH) *(float4*)(lds[buf] + ASZ + (q / (TC / 4)) * TCP + (q % (TC / 4)) * 4) = rb[i];
+        }
+    };
+
+    f32x4 acc[9][FN][FC];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FC; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int kr = lane >> 4, kc = lane & 15;
+    if (st0 < st1) {
+        gload(st0);
+        lstore(0);
+        __syncthreads();
+    }
+    int buf = 0;
+    for (int st = st0; st < st1; ++st) {
+        const bool more = st + 1 < st1;
+        if (more) gload(st + 1);
+        const float* A = lds[buf] + wn * WTN + kc;
+        const float* Bm = lds[buf] + ASZ + wc * WTC + kc;
+#pragma unroll
+        for (int kk = 0; kk < KP / 4; ++kk) {
+            float a[FN];
+#pragma unroll
+            for (int i = 0; i < FN; ++i) a[i] = A[(4 * kk + kr) * TNP + 16 * i];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int xrow = (t / 3) * XW + (4 * kk + kr) * S + (t % 3);
+                float b[FC];
+#pragma unroll
+                for (int j = 0; j < FC; ++j) b[j] = Bm[xrow * TCP + 16 * j];
+#pragma unroll
+                for (int i = 0; i < FN; ++i)
+#pragma unroll
+                    for (int j = 0; j < FC; ++j)
+                        acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[t][i][j], 0, 0, 0);
+            }
+        }
+        if (more) lstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    float* out = p.ws ? p.ws + (long long)blockIdx.x * p.cout * p.cin_store * 9 : p.dw;
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+            const int c = c0 + wc * WTC + 16 * j + kc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n0 + wn * WTN + 16 * i + 4 * kr + r;
+                if (n >= cout || c >= p.cin_store) continue;
+                float* d = out + ((long long)n * p.cin_store + c) * 9;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    if (p.ws) d[t] = acc[t][i][j][r];
+                    else unsafeAtomicAdd(d + t, acc[t][i][j][r]);
+                }
+            }
+        }
+}
+
 // dW[i] += sum over the splits of ws[split][i], in split order (deterministic)
 __global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, int splits, long long ne, float* dw) {
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -1478,11 +1602,14 @@ int launch_wgrad_f32(WgradParams p, hipStream_t st) {
     const int ntn = (p.cout + TN - 1) / TN, ntc = (p.cin + TC - 1) / TC;
     p.nst = (int)(((long long)p.M + KP - 1) / KP);
     const long long tiles = (long long)ntn * ntc * taps;
-    long long splits = (768 + tiles - 1) / tiles;  // about three blocks per CU
+    long long splits = (512 + tiles - 1) / tiles;  // about two blocks per CU
     const long long max_splits = (p.nst + 3) / 4;  // >= 4 stages per split
     if (splits > max_splits) splits = max_splits;
     const long long ne = (long long)p.cout * p.cin_store * taps;
-    if (p.ws && splits > p.ws_elems / ne) splits = p.ws_elems / ne;  // the workspace holds every split
+    // the workspace holds every split; partials beyond 16 MiB cost more to write and sum than
+    // the extra blocks gain
+    const long long cap = std::min<long long>(p.ws_elems, 4LL << 20) / ne;
+    if (p.ws && splits > cap) splits = cap;
     if (splits < 1) splits = 1;
     p.sps = (int)((p.nst + splits - 1) / splits);
     splits = (p.nst + p.sps - 1) / p.sps;
@@ -1490,6 +1617,41 @@ int launch_wgrad_f32(WgradParams p, hipStream_t st) {
     YXH_CHECK_ARG(ntn < 65536 && ntc * taps < 65536, "wgrad grid");
     hipLaunchKernelGGL((wgrad_f32<TN, TC, WN, WC, KP>), dim3((unsigned)splits, ntn, ntc * taps), dim3(256), 0, st, p);
     YXH_CHECK_LAUNCH("wgrad_f32");
+    if (p.ws) {
+        hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, (const float*)p.ws,
+                           (int)splits, ne, p.dw);
+        YXH_CHECK_LAUNCH("wgrad_reduce");
+    }
+    return YXH_OK;
+}
+
+template <int TN, int TC, int S, int KP>
+int launch_wgrad9t_f32(WgradParams p, hipStream_t st) {
+    if (p.kh != 3 || p.kw != 3 || p.stride != S || p.pad != 1) {
+        set_error("wgrad tiles 21-24 (fp32, nine taps per block) need a 3x3 pad-1 conv of stride %d", S);
+        return YXH_EUNSUPPORTED;
+    }
+    if ((p.nsrc > 1 && p.src0_ch % 4) || p.dycs % 4 || p.dybs % 4 || p.cin % 4) {
+        set_error("wgrad tiles 21-24: 16-byte channel chunks");
+        return YXH_EUNSUPPORTED;
+    }
+    const int nseg = (p.out_w + KP - 1) / KP;
+    const int ntn = (p.cout + TN - 1) / TN, ntc = (p.cin + TC - 1) / TC;
+    p.nst = p.B * p.out_h * nseg;
+    const long long tiles = (long long)ntn * ntc;
+    long long splits = (512 + tiles - 1) / tiles;
+    const long long max_splits = (p.nst + 3) / 4;
+    if (splits > max_splits) splits = max_splits;
+    const long long ne = (long long)p.cout * p.cin_store * 9;
+    const long long cap = std::min<long long>(p.ws_elems, 4LL << 20) / ne;
+    if (p.ws && splits > cap) splits = cap;
+    if (splits < 1) splits = 1;
+    p.sps = (int)((p.nst + splits - 1) / splits);
+    splits = (p.nst + p.sps - 1) / p.sps;
+    if (p.ws && splits * ne > p.ws_elems) p.ws = nullptr;
+    YXH_CHECK_ARG(ntn < 65536 && ntc < 65536, "wgrad grid");
+    hipLaunchKernelGGL((wgrad9t_f32<TN, TC, S, KP>), dim3((unsigned)splits, ntn, ntc), dim3(256), 0, st, p, nseg);
+    YXH_CHECK_LAUNCH("wgrad9t_f32");
     if (p.ws) {
         hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, (const float*)p.ws,
                            (int)splits, ne, p.dw);
@@ -1542,6 +1704,19 @@ int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
                     case 18: return launch_wgrad_f32<128, 128, 2, 2, 16>(p, st);
                     case 19: return launch_wgrad_f32<128, 64, 2, 2, 32>(p, st);
                     default: return launch_wgrad_f32<64, 128, 2, 2, 32>(p, st);
+                }
+            }
+        case 21: case 22: case 23: case 24:
+            if constexpr (sizeof(T) != 4) {
+                set_error("wgrad tiles 21-24 (nine taps per block, k-major operands) are built for fp32 only");
+                return YXH_EUNSUPPORTED;
+            } else {
+                const bool s2 = p.stride == 2;
+                switch (tile) {
+                    case 21: return s2 ? launch_wgrad9t_f32<64, 64, 2, 16>(p, st) : launch_wgrad9t_f32<64, 64, 1, 16>(p, st);
+                    case 22: return s2 ? launch_wgrad9t_f32<64, 64, 2, 8>(p, st) : launch_wgrad9t_f32<64, 64, 1, 32>(p, st);
+                    case 23: return s2 ? launch_wgrad9t_f32<32, 64, 2, 16>(p, st) : launch_wgrad9t_f32<32, 64, 1, 16>(p, st);
+                    default: return s2 ? launch_wgrad9t_f32<64, 32, 2, 16>(p, st) : launch_wgrad9t_f32<64, 32, 1, 16>(p, st);
                 }
             }
         default: set_error("wgrad tile %d", tile); return YXH_EINVAL;

@@ -130,10 +130,14 @@ class GradBuffer:
 # families, plus the conv_r3h tiles on fp32 (tile codes as engine.TILE_CANDIDATES); weight
 # gradients: yxh_wgrad_desc
 # tiles 1-10.  YOLOX_AMD_TRAIN_TUNE=0 keeps the by-shape defaults.
-CONV_TUNE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
-                   for k in (0, 1)]
-CONV_TUNE_TILES_F32 = CONV_TUNE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)] + [2 * i for i in range(211, 217)]
-WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 21))
+_BASE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52)) for k in (0, 1)]
+# 16-bit (autocast) steps also try the inference path's 16-bit kernels for the forward convs: dense
+# 1x1 conv_pwf (97-104), weight-stationary 3x3 conv_ws (161-190) and 1x1 conv_ws1 (201-210); they
+# refuse the fp32-accumulating data-gradient form, which stays on the tiles above
+CONV_TUNE_TILES = _BASE_TILES + ([] if os.environ.get("YOLOX_AMD_TRAIN_TILES16") == "base" else
+                                 [2 * i for i in list(range(97, 105)) + list(range(161, 191)) + list(range(201, 211))])
+CONV_TUNE_TILES_F32 = _BASE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)] + [2 * i for i in range(211, 217)]
+WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 25))
 _TRAIN_TILES: dict = {}
 # diagnostic (tools/train_shapes.py): every conv / wgrad launch of the training step, in order
 _LAUNCH_LOG: Optional[list] = [] if os.environ.get("YOLOX_AMD_TRAIN_LOG") else None
