@@ -540,8 +540,11 @@ __global__ __launch_bounds__(256) void conv_wgrad(WgradParams p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int n = n0 + wr * WTN + i * 16 + fq * 4 + r;
-                if (n < p.cout)
-                    atomicAdd(p.dw + (((long long)n * p.cin_store + c) * p.kh + ky) * p.kw + kx, acc[i][j][r]);
+                if (n < p.cout) {
+                    const long long e = (((long long)n * p.cin_store + c) * p.kh + ky) * p.kw + kx;
+                    if (p.ws) p.ws[(long long)blockIdx.x * p.cout * p.cin_store * p.kh * p.kw + e] = acc[i][j][r];
+                    else atomicAdd(p.dw + e, acc[i][j][r]);
+                }
             }
         }
 }
@@ -692,15 +695,47 @@ __global__ __launch_bounds__(64 * WN * WC) void conv_wgrad9(WgradParams p, int t
             for (int r = 0; r < 4; ++r) {
                 const int n = n0 + wn * WTN + i * 16 + fq * 4 + r;
                 if (n >= p.cout) continue;
-                float* d = p.dw + ((long long)n * p.cin_store + c) * 9;
+                const long long e = ((long long)n * p.cin_store + c) * 9;
+                if (p.ws) {
+                    float* d = p.ws + (long long)blockIdx.x * p.cout * p.cin_store * 9 + e;
 #pragma unroll
-                for (int t = 0; t < 9; ++t) atomicAdd(d + t, acc[t][i][j][r]);
+                    for (int t = 0; t < 9; ++t) d[t] = acc[t][i][j][r];
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) atomicAdd(p.dw + e + t, acc[t][i][j][r]);
+                }
             }
         }
 }
 
+__global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, int splits, long long ne, float* dw);
+
+// Per-split partials (yxh_wgrad_desc.workspace): the split count a launcher wants, capped so every
+// split's partial dW fits the workspace and 16 MiB (beyond that writing and summing the partials
+// costs more than the extra blocks gain); p.ws is cleared when not even one split fits (atomics).
+static long long ws_cap_splits(WgradParams& p, long long splits) {
+    if (!p.ws) return splits;
+    const long long ne = (long long)p.cout * p.cin_store * p.kh * p.kw;
+    const long long cap = std::min<long long>(p.ws_elems, 4LL << 20) / ne;
+    if (cap < 1) {
+        p.ws = nullptr;
+        return splits;
+    }
+    return std::min(splits, cap);
+}
+
+// dW += the splits' partials, summed in split order (deterministic)
+static int ws_reduce(const WgradParams& p, long long splits, hipStream_t st) {
+    if (!p.ws) return YXH_OK;
+    const long long ne = (long long)p.cout * p.cin_store * p.kh * p.kw;
+    hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, (const float*)p.ws,
+                       (int)splits, ne, p.dw);
+    YXH_CHECK_LAUNCH("wgrad_reduce");
+    return YXH_OK;
+}
+
 template <int S, int TN, int TC, int WN, int WC, int TY>
-int launch_wgrad9_t(const WgradParams& p, hipStream_t st) {
+int launch_wgrad9_t(WgradParams p, hipStream_t st) {
     if (p.kh != 3 || p.kw != 3 || p.pad != 1 || p.stride != S || p.nsrc != 1 || p.sup[0] || p.sw[0] != p.in_w) {
         set_error("wgrad tiles 11-16 (all nine taps per block) need a 3x3 pad-1 stride-%d conv over one plain source", S);
         return YXH_EUNSUPPORTED;
@@ -716,13 +751,14 @@ int launch_wgrad9_t(const WgradParams& p, hipStream_t st) {
     // about two blocks per CU over the grid, at least two pixel tiles per block
     long long splits = (512 + (long long)ntn * ntc - 1) / ((long long)ntn * ntc);
     if (splits > (T + 1) / 2) splits = (T + 1) / 2;
+    splits = ws_cap_splits(p, splits);
     if (splits < 1) splits = 1;
     const int tpb = (int)((T + splits - 1) / splits);
     splits = (T + tpb - 1) / tpb;
     hipLaunchKernelGGL((conv_wgrad9<S, TN, TC, WN, WC, TY>), dim3((unsigned)splits, ntn, ntc), dim3(64 * WN * WC), 0,
                        st, p, tiles_x, tiles_y, tpb);
     YXH_CHECK_LAUNCH("conv_wgrad9");
-    return YXH_OK;
+    return ws_reduce(p, splits, st);
 }
 
 // ------------------------------------------------------------------ weight gradient, LDS-DMA + transposed reads
@@ -937,8 +973,11 @@ __global__ __launch_bounds__(256) void conv_wgrad2(WgradParams p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int n = n0 + wr * WTN + i * 16 + (lane >> 4) * 4 + r;
-                if (n < p.cout)
-                    atomicAdd(p.dw + (((long long)n * p.cin_store + c) * p.kh + ky) * p.kw + kx, acc[i][j][r]);
+                if (n < p.cout) {
+                    const long long e = (((long long)n * p.cin_store + c) * p.kh + ky) * p.kw + kx;
+                    if (p.ws) p.ws[(long long)blockIdx.x * p.cout * p.cin_store * p.kh * p.kw + e] = acc[i][j][r];
+                    else atomicAdd(p.dw + e, acc[i][j][r]);
+                }
             }
         }
 }
@@ -1554,6 +1593,7 @@ int launch_wgrad_t(WgradParams p, hipStream_t st) {
     long long splits = (512 + tiles - 1) / tiles;
     const long long max_splits = (p.nst + 7) / 8;
     if (splits > max_splits) splits = max_splits;
+    splits = ws_cap_splits(p, splits);
     if (splits < 1) splits = 1;
     p.sps = (int)((p.nst + splits - 1) / splits);
     splits = (p.nst + p.sps - 1) / p.sps;
@@ -1561,7 +1601,7 @@ int launch_wgrad_t(WgradParams p, hipStream_t st) {
     hipLaunchKernelGGL((conv_wgrad<T, TN, TM, WR, WC, KS>), dim3((unsigned)splits, ntn, ntap * p.ntc), dim3(256), 0,
                        st, p);
     YXH_CHECK_LAUNCH("conv_wgrad");
-    return YXH_OK;
+    return ws_reduce(p, splits, st);
 }
 
 template <typename T, int TN, int TM, int NBUF>
@@ -1581,6 +1621,7 @@ int launch_wgrad2_t(WgradParams p, hipStream_t st) {
         long long splits = (256LL * (occ < 1 ? 1 : occ) + tiles - 1) / tiles;  // about one wave of blocks
         const long long max_splits = (p.nst + 3) / 4;                           // >= 4 stages per split
         if (splits > max_splits) splits = max_splits;
+        splits = ws_cap_splits(p, splits);
         if (splits < 1) splits = 1;
         p.sps = (int)((p.nst + splits - 1) / splits);
         splits = (p.nst + p.sps - 1) / p.sps;
@@ -1588,7 +1629,7 @@ int launch_wgrad2_t(WgradParams p, hipStream_t st) {
         hipLaunchKernelGGL((conv_wgrad2<T, TN, TM, NBUF>), dim3((unsigned)splits, ntn, ntap * p.ntc), dim3(256), 0,
                            st, p);
         YXH_CHECK_LAUNCH("conv_wgrad2");
-        return YXH_OK;
+        return ws_reduce(p, splits, st);
     }
 }
 
@@ -1605,24 +1646,14 @@ int launch_wgrad_f32(WgradParams p, hipStream_t st) {
     long long splits = (512 + tiles - 1) / tiles;  // about two blocks per CU
     const long long max_splits = (p.nst + 3) / 4;  // >= 4 stages per split
     if (splits > max_splits) splits = max_splits;
-    const long long ne = (long long)p.cout * p.cin_store * taps;
-    // the workspace holds every split; partials beyond 16 MiB cost more to write and sum than
-    // the extra blocks gain
-    const long long cap = std::min<long long>(p.ws_elems, 4LL << 20) / ne;
-    if (p.ws && splits > cap) splits = cap;
+    splits = ws_cap_splits(p, splits);
     if (splits < 1) splits = 1;
     p.sps = (int)((p.nst + splits - 1) / splits);
     splits = (p.nst + p.sps - 1) / p.sps;
-    if (p.ws && splits * ne > p.ws_elems) p.ws = nullptr;  // too small even for one split: atomics
     YXH_CHECK_ARG(ntn < 65536 && ntc * taps < 65536, "wgrad grid");
     hipLaunchKernelGGL((wgrad_f32<TN, TC, WN, WC, KP>), dim3((unsigned)splits, ntn, ntc * taps), dim3(256), 0, st, p);
     YXH_CHECK_LAUNCH("wgrad_f32");
-    if (p.ws) {
-        hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, (const float*)p.ws,
-                           (int)splits, ne, p.dw);
-        YXH_CHECK_LAUNCH("wgrad_reduce");
-    }
-    return YXH_OK;
+    return ws_reduce(p, splits, st);
 }
 
 template <int TN, int TC, int S, int KP>
@@ -1642,22 +1673,14 @@ int launch_wgrad9t_f32(WgradParams p, hipStream_t st) {
     long long splits = (512 + tiles - 1) / tiles;
     const long long max_splits = (p.nst + 3) / 4;
     if (splits > max_splits) splits = max_splits;
-    const long long ne = (long long)p.cout * p.cin_store * 9;
-    const long long cap = std::min<long long>(p.ws_elems, 4LL << 20) / ne;
-    if (p.ws && splits > cap) splits = cap;
+    splits = ws_cap_splits(p, splits);
     if (splits < 1) splits = 1;
     p.sps = (int)((p.nst + splits - 1) / splits);
     splits = (p.nst + p.sps - 1) / p.sps;
-    if (p.ws && splits * ne > p.ws_elems) p.ws = nullptr;
     YXH_CHECK_ARG(ntn < 65536 && ntc < 65536, "wgrad grid");
     hipLaunchKernelGGL((wgrad9t_f32<TN, TC, S, KP>), dim3((unsigned)splits, ntn, ntc), dim3(256), 0, st, p, nseg);
     YXH_CHECK_LAUNCH("wgrad9t_f32");
-    if (p.ws) {
-        hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, (const float*)p.ws,
-                           (int)splits, ne, p.dw);
-        YXH_CHECK_LAUNCH("wgrad_reduce");
-    }
-    return YXH_OK;
+    return ws_reduce(p, splits, st);
 }
 
 template <typename T>

@@ -172,6 +172,10 @@ class TrainGraph:
         self._scratch = torch.empty(0, dtype=torch.uint8, device=self.device)
         # per-split partial weight gradients of the fp32 wgrad tiles (summed in a fixed order)
         self.wg_ws = torch.empty(64 << 20, dtype=torch.uint8, device=self.device)
+        # weight gradients run on a side stream beside the data-gradient chain (YOLOX_AMD_WGRAD_STREAM=0: inline)
+        self._wside = (torch.cuda.Stream(self.device) if os.environ.get("YOLOX_AMD_WGRAD_STREAM", "1") != "0"
+                       and self.device.type == "cuda" else None)
+        self._scratch_side = torch.empty(0, dtype=torch.uint8, device=self.device)
         # weight repacks: the first step launches one pack per conv (forward layout) and per
         # data-gradient input slice, recording each as a yxh_pack_job; later steps repack
         # everything in ONE yxh_pack_weights_batch launch at the start of the forward
@@ -295,6 +299,20 @@ class TrainGraph:
             _LAUNCH_LOG.append(("wgrad", k, stride, cin, cout, in_h, in_w, out_h, out_w, batch, d.tile, len(srcs),
                                 int(srcs[0].upsample), 0))
 
+    def _side_wgrad(self, launch: Callable[[], None], dy: torch.Tensor, param: nn.Parameter) -> None:
+        """A conv's weight gradient on the side stream: it needs only dy and the forward's input
+        (both final by now) and nothing on the main stream reads dW before the backward ends, so
+        it overlaps the data-gradient chain (the critical path) instead of sitting in it."""
+        if self._wside is None:
+            launch()
+            self._ready(param)
+            return
+        self._wside.wait_stream(torch.cuda.current_stream(self.device))  # dy written, dW zeroed
+        with torch.cuda.stream(self._wside):
+            launch()
+            self._ready(param)  # DP: the bucket's event is recorded on this stream
+        dy.record_stream(self._wside)
+
     def _tile(self, key: tuple, d, fn, out_field: str, out_bytes: int, candidates: list, reps: int = 3) -> int:
         """The cached tile for this shape, or the fastest candidate timed now (writing to
         scratch instead of ``out_field``); 0 (by shape) when tuning is off."""
@@ -303,11 +321,17 @@ class TrainGraph:
             return t
         if not self.tune:
             return 0
-        if self._scratch.numel() < out_bytes:
-            self._scratch = torch.empty(out_bytes, dtype=torch.uint8, device=self.device)
-        real = getattr(d, out_field)
-        setattr(d, out_field, self._scratch.data_ptr())
         stream = torch.cuda.current_stream(self.device)
+        side = self._wside is not None and stream == self._wside  # each stream tunes into its own sink
+        scratch = self._scratch_side if side else self._scratch
+        if scratch.numel() < out_bytes:
+            scratch = torch.empty(out_bytes, dtype=torch.uint8, device=self.device)
+            if side:
+                self._scratch_side = scratch
+            else:
+                self._scratch = scratch
+        real = getattr(d, out_field)
+        setattr(d, out_field, scratch.data_ptr())
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st, ref = self.stream, C.byref(d)
         best = (float("inf"), 0)
@@ -421,9 +445,8 @@ class TrainGraph:
                     residual.grad = out.grad
                 else:
                     residual.grad.add_(out.grad)
-            self._wgrad(srcs, cin, cin_store, cout, k, s, p, dense_src(dy), gb.of(conv.weight), in_h, in_w, oh, ow,
-                        B)
-            self._ready(conv.weight)
+            self._side_wgrad(lambda: self._wgrad(srcs, cin, cin_store, cout, k, s, p, dense_src(dy), gb.of(conv.weight),
+                                                 in_h, in_w, oh, ow, B), dy, conv.weight)
             off, ins = 0, []
             for a, up in inputs:
                 ins.append((a, up, off))
@@ -630,6 +653,8 @@ class TrainGraph:
         prev = self.grads.begin()
         for fn in reversed(self.tape):
             fn()
+        if self._wside is not None:  # every weight gradient is in before the reducer / optimizer
+            torch.cuda.current_stream(self.device).wait_stream(self._wside)
         self.tape = []
         self._keep = None
         if self.batch_pack and self._pack_table is None and self._pack_jobs:

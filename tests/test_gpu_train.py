@@ -210,10 +210,11 @@ WG_TILE_CASES = [  # cin0, cin1, up1, cout, k, s, H, B
 ]
 
 
+@pytest.mark.parametrize("ws", [0, 16 << 20])
 @pytest.mark.parametrize("tile", [1, 2, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("cin0,cin1,up1,cout,k,s,H,B", WG_TILE_CASES)
-def test_conv_wgrad_tiles(tile, dtype, cin0, cin1, up1, cout, k, s, H, B):
+def test_conv_wgrad_tiles(ws, tile, dtype, cin0, cin1, up1, cout, k, s, H, B):
     """every weight-gradient tile (register-transposed 1-4, LDS-DMA + ds_read_b64_tr_b16
     5-10) against torch autograd: ragged pixel counts (stage tails), cout / cin not
     multiples of the tile, two sources with an upsampled second one, stride 2."""
@@ -230,7 +231,7 @@ def test_conv_wgrad_tiles(tile, dtype, cin0, cin1, up1, cout, k, s, H, B):
     if cin1:
         x1d = x1.cuda()
         srcs.append(src(x1d, up=up1))
-    dw = wgrad(dtype, srcs, src(dyd), cout, cin0 + cin1, k, s, p, (H, W), (oh, ow), B, tile=tile)
+    dw = wgrad(dtype, srcs, src(dyd), cout, cin0 + cin1, k, s, p, (H, W), (oh, ow), B, tile=tile, ws_bytes=ws)
     torch.cuda.synchronize()
     xin = x0.float().permute(0, 3, 1, 2)
     if cin1:
@@ -243,9 +244,10 @@ def test_conv_wgrad_tiles(tile, dtype, cin0, cin1, up1, cout, k, s, H, B):
     assert rel(dw, wr.grad) < 1e-4  # fp32 accumulation of exact products: order-only differences
 
 
+@pytest.mark.parametrize("ws", [0, 16 << 20])
 @pytest.mark.parametrize("tile", [11, 12, 13, 14, 15, 16])
 @pytest.mark.parametrize("cin0,cin1,up1,cout,k,s,H,B", WG_TILE_CASES + [(16, 0, 0, 32, 3, 1, 40, 2)])
-def test_conv_wgrad9_fp32_tiles(tile, cin0, cin1, up1, cout, k, s, H, B):
+def test_conv_wgrad9_fp32_tiles(ws, tile, cin0, cin1, up1, cout, k, s, H, B):
     """fp32 all-nine-taps weight gradient (tiles 11-16) against torch autograd: partial
     pixel tiles at the image edges, cout / cin tails, stride 2; other geometries are
     rejected (NotImplementedError) and run on tiles 1-4."""
@@ -261,7 +263,8 @@ def test_conv_wgrad9_fp32_tiles(tile, cin0, cin1, up1, cout, k, s, H, B):
     if cin1:
         srcs.append(src(torch.randn(B, H >> up1, W >> up1, cin1, generator=g).cuda(), up=up1))
     try:
-        dw = wgrad(torch.float32, srcs, src(dyd), cout, cin0 + cin1, k, s, p, (H, W), (oh, ow), B, tile=tile)
+        dw = wgrad(torch.float32, srcs, src(dyd), cout, cin0 + cin1, k, s, p, (H, W), (oh, ow), B, tile=tile,
+                   ws_bytes=ws)
     except NotImplementedError as e:
         assert k != 3 or cin1, e
         return
