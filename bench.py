@@ -3,7 +3,7 @@
 configs[1]: batch 32 per GPU, synthetic uniform [0,255] images, seeded weights).
 
 One step = one batch through the hot path: the captured hipGraph of the whole
-forward (Focus -> CSPDarknet -> PAFPN -> decoupled head with fused decode, 82
+forward (Focus -> CSPDarknet -> PAFPN -> decoupled head with fused decode, 63
 kernels) followed by device post-processing (filter, sort, bitmask NMS) at the
 processor defaults (conf 0.5, nms 0.65); a batch's NMS runs on a side stream beside the
 next batch's forward, which waits only for the NMS filter pass (the one reader of the

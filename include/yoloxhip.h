@@ -107,7 +107,8 @@ typedef struct {
                             kernel, id 65-70 the persistent streaming 1x1 kernel;
                             chosen by the planner's on-device autotune                   */
     int32_t flags;       /* YXH_CONV_ACCUMULATE: f32 dst += result (gradient accumulation) */
-    int32_t reserved0;
+    int32_t grid_cap;    /* 0, or the CUs the persistent tiles (conv_ws / conv_ws1 / conv_pwf) may occupy: a
+                            graph lane running beside another lane's work leaves it the rest of the chip */
     /* Fused Bottleneck (network_blocks.py:77-99): when pre_weight is set, the source is the
      * Bottleneck input x and the 3x3 conv reads t = act(pre_weight . x + pre_bias) (its
      * conv1, a 1x1 cin -> cin, BatchNorm folded), computed per pixel tile on the halo in LDS

@@ -517,6 +517,8 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
                                       d->cin % 32 == 0 && d->groups == 1),
                   "weight_frag: 16-bit, cout %% 16 == 0, cin %% 32 == 0, groups 1");
     p.wf = d->weight_frag;
+    YXH_CHECK_ARG(d->grid_cap >= 0, "grid_cap %d", d->grid_cap);
+    p.cus = d->grid_cap > 0 && d->grid_cap < 256 ? d->grid_cap : 256;
     p.grp2 = grp2 ? 1 : 0;
     if (grp2 && d->tile == 0) return conv_ws_dispatch(dt, d->cin == 256 ? 176 - 160 : 185 - 160, p, st);
     if (grp2 && !((d->tile >> 1) > 160 && (d->tile >> 1) <= 190)) {

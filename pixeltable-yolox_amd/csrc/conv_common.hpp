@@ -31,6 +31,7 @@ struct ConvParams {
     const float* pb1;
     int grp2;  // YXH_CONV_GROUPS2: output half g reads source channels [g*cin, (g+1)*cin)
     const void* wf;  // weights in yxh_pack_frag's fragment-major layout, or null (conv_ws / conv_ws1)
+    int cus;         // CUs the persistent grids may occupy (yxh_conv_desc.grid_cap; 256 = all)
 };
 
 // Stationary weight fragment (i: 16 output channels from n_first, tap, kb: 32-channel K block)

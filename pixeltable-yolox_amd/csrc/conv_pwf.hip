@@ -288,8 +288,12 @@ static int launch_pwf(const ConvParams& p, hipStream_t st) {
     }
     const int ntn = (p.cout + TN - 1) / TN, ntm = (p.M + TM - 1) / TM;
     long long blocks = (long long)ntn * ntm;
+    if (PER_CU == 0 && p.cus < 256) {  // one block per tile: cap the grid as a persistent one would be
+        const long long cap = std::max<long long>(ntn, (long long)p.cus * 2 / ntn * ntn);
+        if (blocks > cap) blocks = cap;
+    }
     if (PER_CU > 0) {
-        long long cap = 256LL * PER_CU / ntn * ntn;  // whole channel-tile groups
+        long long cap = (long long)p.cus * PER_CU / ntn * ntn;  // whole channel-tile groups
         if (cap < ntn) cap = ntn;
         if (blocks > cap) blocks = cap;
     }

@@ -434,7 +434,7 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
         set_error("conv_ws: too many tiles");
         return YXH_EINVAL;
     }
-    const int nwork = (int)std::min<long long>(ntiles, std::max(1, 256 * BPC / ntn));
+    const int nwork = (int)std::min<long long>(ntiles, std::max(1, p.cus * BPC / ntn));
     hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM, BPC, F1>), dim3((unsigned)(nwork * ntn)),
                        dim3(64 * WN * WK * WM), 0, st, p, tiles_x, tiles_y, (int)ntiles, ntn, nwork);
     YXH_CHECK_LAUNCH("conv_ws launch");

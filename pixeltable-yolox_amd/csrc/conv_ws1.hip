@@ -247,7 +247,7 @@ static int launch_ws1(const ConvParams& p, hipStream_t st) {
     }
     const long long ntiles = (M + TM - 1) / TM;
     const int ntn = (p.cout + TN - 1) / TN;
-    const int nwork = (int)std::min<long long>(ntiles, std::max(1, 256 * BPC / ntn));
+    const int nwork = (int)std::min<long long>(ntiles, std::max(1, p.cus * BPC / ntn));
     hipLaunchKernelGGL((conv_ws1<T, CIN, TM, TN, WN, WK, WM, BPC>), dim3((unsigned)(nwork * ntn)),
                        dim3(64 * WN * WK * WM), 0, st, p, (int)ntiles, ntn, nwork, ps, l0, l1);
     YXH_CHECK_LAUNCH("conv_ws1 launch");

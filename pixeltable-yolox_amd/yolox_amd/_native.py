@@ -47,7 +47,7 @@ class ConvDesc(C.Structure):
                 ("dst_dtype", C.c_int32), ("res_bstride", C.c_int64), ("dst", C.c_void_p),
                 ("dst_cstride", C.c_int32), ("act", C.c_int32), ("dst_bstride", C.c_int64),
                 ("decode_stride", C.c_float), ("decode_coff", C.c_int32), ("tile", C.c_int32),
-                ("flags", C.c_int32), ("reserved0", C.c_int32), ("pre_weight", C.c_void_p), ("pre_bias", C.c_void_p),
+                ("flags", C.c_int32), ("grid_cap", C.c_int32), ("pre_weight", C.c_void_p), ("pre_bias", C.c_void_p),
                 ("weight_frag", C.c_void_p)]
 
 

@@ -347,6 +347,15 @@ class OutBuffer:
 # (yoloxhip.h yxh_conv_desc.tile)
 TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
                    + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 197)] + [2 * i for i in range(201, 211)]
+# 16-bit plans: the families that win on MI355X (profiles/r03/final/tune_r3fa_*.json: yolox_s picks only
+# conv_pwf / conv_ws / conv_ws1; yolox_l fp16 also conv_igemm and conv_r3 once or twice); the LDS-DMA
+# conv_glds, row-tiled conv_rows and the round-1 pointwise kernels never do and are tried only with
+# YOLOX_AMD_TUNE_ALL_FAMILIES=1 (fp32 plans always try every family)
+TILE_CANDIDATES_16 = [t for t in TILE_CANDIDATES if (t >> 1) < 17 or (t >> 1) > 96]
+_TUNE_ALL_FAMILIES = os.environ.get("YOLOX_AMD_TUNE_ALL_FAMILIES", "0") == "1"
+# CUs a graph lane's persistent conv grids may occupy ("lane:cus,..."; yxh_conv_desc.grid_cap): a head
+# level forked early (YOLOX_AMD_GRAPH=streams) leaves the rest of the chip to the neck it runs beside
+_LANE_CUS = {int(k): int(v) for k, v in (e.split(":") for e in os.environ.get("YOLOX_AMD_LANE_CUS", "").split(",") if e)}
 _TUNE_CACHE: dict = {}
 _TUNE_ALL = os.environ.get("YOLOX_AMD_TUNE_ALL", "0") == "1"  # print every variant's time
 
@@ -635,6 +644,7 @@ class Plan:
                 d.weight = self.warena.data_ptr() + spec.w_off
                 d.bias = self.barena.data_ptr() + spec.b_off
                 d.flags = N.CONV_GROUPS2 if a.get("grouped2") else 0
+                d.grid_cap = _LANE_CUS.get(rec.lane, 0)
                 d.weight_frag = self.farena.data_ptr() + spec.f_off if spec.f_off >= 0 else None
                 pre = a.get("pre_spec")
                 if pre is not None:
@@ -997,7 +1007,8 @@ class Plan:
                 continue
             best = (float("inf"), 0)
             ptr = C.pointer(op)
-            for tile in TILE_CANDIDATES:
+            cands = (TILE_CANDIDATES if self.dtype == torch.float32 or _TUNE_ALL_FAMILIES else TILE_CANDIDATES_16)
+            for tile in cands:
                 op.u.conv.tile = tile
                 if L.yxh_run_ops(ptr, 1, st) != N.OK:  # variant not applicable
                     continue
