@@ -996,6 +996,9 @@ class Plan:
         stream = torch.cuda.current_stream(self.device)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         chosen = {}
+        # YOLOX_AMD_TUNE_COLD=1: time each candidate after streaming 64 MiB through the L2s
+        flush = (torch.zeros(16 << 20, dtype=torch.float32, device=self.device)
+                 if os.environ.get("YOLOX_AMD_TUNE_COLD", "0") == "1" else None)
         for i, rec in enumerate(self.ctx.ops):
             if rec.kind != N.OP_CONV or rec.args["groups"] != 1:
                 continue
@@ -1012,12 +1015,22 @@ class Plan:
                 op.u.conv.tile = tile
                 if L.yxh_run_ops(ptr, 1, st) != N.OK:  # variant not applicable
                     continue
-                ev0.record(stream)
-                for _ in range(reps):
-                    L.yxh_run_ops(ptr, 1, st)
-                ev1.record(stream)
-                ev1.synchronize()
-                t = ev0.elapsed_time(ev1) / reps
+                if flush is None:
+                    ev0.record(stream)
+                    for _ in range(reps):
+                        L.yxh_run_ops(ptr, 1, st)
+                    ev1.record(stream)
+                    ev1.synchronize()
+                    t = ev0.elapsed_time(ev1) / reps
+                else:  # each rep after evicting the XCD L2s, as in the forward (weights come from HBM / MALL)
+                    t = 0.0
+                    for _ in range(reps):
+                        flush.add_(1)
+                        ev0.record(stream)
+                        L.yxh_run_ops(ptr, 1, st)
+                        ev1.record(stream)
+                        ev1.synchronize()
+                        t += ev0.elapsed_time(ev1) / reps
                 if _TUNE_ALL:
                     print(f"  op {i} tile {tile >> 1} slabs {(tile & 1) + 1}: {t * 1e3:.1f} us", file=sys.stderr)
                 if t < best[0]:
