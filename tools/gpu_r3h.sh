@@ -15,3 +15,8 @@ for CFG in "streams:" "streams:1:128" "streams:1:160" "streams:1:96" "lanes:1:12
       > gpurun_out/bench_${TAG}_${G}_${C}.json 2>&1 || exit 1
   grep -o '"value": [0-9.]*\|"forward_ms": [0-9.]*' gpurun_out/bench_${TAG}_${G}_${C}.json | tr '\n' ' '; echo " $G cus=$C"
 done
+# cold-cache autotune (weights evicted from the XCD L2s before every timed candidate launch)
+TC=gpurun_out/tune_${TAG}_cold.json
+YOLOX_AMD_TUNE_COLD=1 timeout -k 10 400 python bench.py --no-cpu-baseline --tune-file $TC \
+    > gpurun_out/bench_${TAG}_cold.json 2>&1 || exit 1
+grep -o '"value": [0-9.]*\|"forward_ms": [0-9.]*' gpurun_out/bench_${TAG}_cold.json | tr '\n' ' '; echo " lanes cold-tuned"
