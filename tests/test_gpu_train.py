@@ -662,4 +662,3 @@ def test_batched_weight_repack_matches_per_conv(monkeypatch, dtype):
     assert not m2._train_graph.batch_pack
     for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss", "num_fg"):
         assert float(out[k]) == float(ref[k]), k
-
