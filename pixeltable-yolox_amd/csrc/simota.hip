@@ -92,6 +92,20 @@ __device__ __forceinline__ float iou_cxcywh(const float* a, const float* b) {
 
 // One thread per anchor: the 80 class-logit reads of different anchors are independent,
 // so thousands are in flight instead of one image's block walking them chunk by chunk.
+// Per-step initialisation of the assignment outputs and the match counters (one launch;
+// replaces five memset nodes, so a captured training step has only kernel nodes here).
+__global__ __launch_bounds__(256) void sim_init(int BA, int B, int* nmatch, uint8_t* fg, int* matched, float* piou,
+                                                int* num_fg) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < BA) {
+        nmatch[i] = 0;
+        fg[i] = 0;
+        matched[i] = -1;
+        piou[i] = 0.f;
+    }
+    if (i < B) num_fg[i] = 0;
+}
+
 __global__ __launch_bounds__(256) void sim_flags(const float* preds, const float* labels, int A, int C, int L,
                                                  SimGeom geo, SimWork w) {
     const int b = blockIdx.y, a = blockIdx.x * 256 + threadIdx.x;
@@ -496,13 +510,10 @@ int yolox_loss(const float* preds, const float* origin, const float* labels, int
     w.partial = (float*)take(sizeof(float) * 4 * (size_t)B * nblk);
     w.s1a = (float*)take(sizeof(float) * (size_t)B * A);
     w.flag = (uint8_t*)take((size_t)B * A);
-    int rc = 0;
-    rc |= check_hip(hipMemsetAsync(w.nmatch, 0, sizeof(int) * (size_t)B * A, st), "memset");
-    rc |= check_hip(hipMemsetAsync(fg, 0, (size_t)B * A, st), "memset");
-    rc |= check_hip(hipMemsetAsync(matched, 0xff, sizeof(int) * (size_t)B * A, st), "memset");
-    rc |= check_hip(hipMemsetAsync(piou, 0, sizeof(float) * (size_t)B * A, st), "memset");
-    rc |= check_hip(hipMemsetAsync(num_fg, 0, sizeof(int) * B, st), "memset");
-    if (rc) return YXH_EHIP;
+    YXH_CHECK_ARG((long long)B * A < (1LL << 31), "B*A too large");
+    const int BA = B * A;
+    hipLaunchKernelGGL(sim_init, dim3((BA + 255) / 256), dim3(256), 0, st, BA, B, w.nmatch, fg, matched, piou, num_fg);
+    YXH_CHECK_LAUNCH("sim_init");
     hipLaunchKernelGGL(sim_flags, dim3((A + 255) / 256, B), dim3(256), 0, st, preds, labels, A, C, L, geo, w);
     YXH_CHECK_LAUNCH("sim_flags");
     hipLaunchKernelGGL(sim_candidates, dim3(B), dim3(1024), 0, st, A, w);

@@ -28,15 +28,48 @@ import torch.distributed as dist
 import torch.nn as nn
 
 
+class _CudaOps:
+    """The stream operations GradReducer issues (tests substitute a recording fake)."""
+
+    def current(self, device):
+        return torch.cuda.current_stream(device)
+
+    def new_stream(self, device):
+        return torch.cuda.Stream(device)
+
+    def record(self, stream):
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev
+
+    def wait(self, stream, ev) -> None:
+        stream.wait_event(ev)
+
+    def all_reduce(self, t: torch.Tensor, stream, group):
+        with torch.cuda.stream(stream):
+            return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
+
+    def scale(self, t: torch.Tensor, v: float) -> None:
+        t.mul_(v)
+
+
 class GradReducer:
     """Bucketed all-reduce over a flat gradient buffer.
 
     flat: 1-D fp32 tensor; params_in_order: the parameters laid out in ``flat`` (each a
     contiguous slice, in order); offsets: id(param) -> element offset.
+
+    Ordering: a parameter is reported ready from the stream that wrote its gradient (the
+    compute stream for BN / head parameters, the weight-gradient side stream for conv
+    weights, yolox_amd.train).  Each ``ready`` records an event on the CURRENT stream for
+    the parameter's bucket (one live event per (bucket, stream): a later record on the same
+    stream covers the earlier writes), and a bucket's all-reduce waits on every one of them,
+    so it never reads a gradient another stream is still writing -- wherever the bucket
+    boundaries fall.
     """
 
     def __init__(self, flat: torch.Tensor, params_in_order, offsets: dict, bucket_mb: float = 8.0,
-                 group=None, world: Optional[int] = None):
+                 group=None, world: Optional[int] = None, ops=None):
         self.flat = flat
         self.group = group
         self.world = world if world is not None else dist.get_world_size(group)
@@ -60,8 +93,8 @@ class GradReducer:
             self.buckets.append((start, cur))
             sizes.append(n_in)
         self.sizes = sizes
-        self.cuda = flat.is_cuda
-        self.side = torch.cuda.Stream(flat.device) if self.cuda else None
+        self.ops = ops if ops is not None else (_CudaOps() if flat.is_cuda else None)
+        self.side = self.ops.new_stream(flat.device) if self.ops is not None else None
         self.reset()
 
     def reset(self) -> None:
@@ -69,11 +102,15 @@ class GradReducer:
         self.next = 0
         self.works: list = []
         self.launch_order: list[int] = []
+        self.events: list[dict] = [{} for _ in self.buckets]  # bucket -> {stream: latest event}
 
     def ready(self, p: nn.Parameter) -> None:
         k = self.bucket_of.get(id(p))
         if k is None:
             return
+        if self.ops is not None:
+            s = self.ops.current(self.flat.device)
+            self.events[k][s] = self.ops.record(s)
         self.pending[k] -= 1
         while self.next < len(self.buckets) and self.pending[self.next] <= 0:
             self._launch(self.next)
@@ -82,12 +119,13 @@ class GradReducer:
     def _launch(self, k: int) -> None:
         s, e = self.buckets[k]
         t = self.flat[s:e]
-        if self.cuda:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.flat.device))
-            with torch.cuda.stream(self.side):
-                self.side.wait_event(ev)
-                w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if self.ops is not None:
+            if not self.events[k]:  # finish() of a bucket nobody reported: order after the caller
+                cur = self.ops.current(self.flat.device)
+                self.events[k][cur] = self.ops.record(cur)
+            for ev in self.events[k].values():
+                self.ops.wait(self.side, ev)
+            w = self.ops.all_reduce(t, self.side, self.group)
         else:
             w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.works.append(w)
@@ -101,7 +139,10 @@ class GradReducer:
         for w in self.works:
             w.wait()  # NCCL: the current stream waits on RCCL's stream; gloo: blocks
         if self.world > 1:
-            self.flat.mul_(1.0 / self.world)
+            if self.ops is not None:
+                self.ops.scale(self.flat, 1.0 / self.world)
+            else:
+                self.flat.mul_(1.0 / self.world)
 
 
 class DistributedDataParallel(nn.Module):

@@ -152,7 +152,7 @@ class FusedStep:
         # in-place writes behind torch's back: bump versions (eager plans) and the modules'
         # weights epochs (captured plans) so eval plans repack
         torch.autograd.graph.increment_version(self.params)
-        for m in (self.model, getattr(self.ema, "ema", None)):
+        for m in (getattr(self.model, "module", self.model), getattr(self.ema, "ema", None)):
             if hasattr(m, "weights_changed"):
                 m.weights_changed()
         if self.ema is not None:

@@ -38,6 +38,7 @@ from .models.network import (BaseConv, Bottleneck, CspDarknet, CspLayer, DWConv,
                              YoloPafpn, YoloxHead)
 
 MAX_CHANNELS = 4096  # reduction workspace sizing (yolox_x: 1280)
+WGRAD_WS_BYTES = 16 << 20  # = the launcher's cap on per-split partials (4 Mi floats)
 
 
 class Act:
@@ -170,11 +171,17 @@ class TrainGraph:
         self.grad_total = torch.ones((), dtype=torch.float32, device=self.device)
         self.tune = os.environ.get("YOLOX_AMD_TRAIN_TUNE", "1") != "0"
         self._scratch = torch.empty(0, dtype=torch.uint8, device=self.device)
-        # per-split partial weight gradients of the fp32 wgrad tiles (summed in a fixed order)
-        self.wg_ws = torch.empty(64 << 20, dtype=torch.uint8, device=self.device)
         # weight gradients run on a side stream beside the data-gradient chain (YOLOX_AMD_WGRAD_STREAM=0: inline)
         self._wside = (torch.cuda.Stream(self.device) if os.environ.get("YOLOX_AMD_WGRAD_STREAM", "1") != "0"
                        and self.device.type == "cuda" else None)
+        # per-split partial weight gradients of the fp32 wgrad tiles (summed in a fixed order); the
+        # launcher uses at most 16 MiB of partials (csrc/train.hip ws_cap_splits; a weight too large
+        # for one split falls back to fp32 atomics).  One workspace per stream that issues
+        # weight gradients (head preds: main stream; BaseConvs: the side stream), so work in
+        # flight on one stream never shares partials with the other.
+        self.wg_ws = torch.empty(WGRAD_WS_BYTES, dtype=torch.uint8, device=self.device)
+        self.wg_ws_side = (torch.empty(WGRAD_WS_BYTES, dtype=torch.uint8, device=self.device)
+                           if self._wside is not None else self.wg_ws)
         self._scratch_side = torch.empty(0, dtype=torch.uint8, device=self.device)
         self._wpending: list = []
         self.wgrad_group = max(1, int(os.environ.get("YOLOX_AMD_WGRAD_GROUP", "1")))
@@ -292,7 +299,9 @@ class TrainGraph:
             d.src[j] = s
         d.dy = dy
         d.dw = dw.data_ptr()
-        d.workspace, d.workspace_bytes = self.wg_ws.data_ptr(), self.wg_ws.numel()
+        side = self._wside is not None and torch.cuda.current_stream(self.device) == self._wside
+        wsb = self.wg_ws_side if side else self.wg_ws
+        d.workspace, d.workspace_bytes = wsb.data_ptr(), wsb.numel()
         key = ("wgrad", self.dcode, batch, in_h, in_w, out_h, out_w, cin, cin_store, cout, k, stride, pad,
                _src_key(dy)) + tuple(_src_key(q) for q in srcs)
         d.tile = self._tile(key, d, self.lib.yxh_conv_wgrad, "dw", cout * cin_store * k * k * 4, WGRAD_TUNE_TILES)

@@ -63,6 +63,14 @@ class ModelEMA:
             e, s = self._pairs
             torch._foreach_mul_(e, d)
             torch._foreach_add_(e, [t.detach() for t in s], alpha=1.0 - d)
+        _weights_changed(self.ema)
+
+
+def _weights_changed(model: nn.Module) -> None:
+    """Advance the weights epoch a replayed inference plan checks (engine.Plan.replay)."""
+    m = model.module if hasattr(model, "module") else model
+    if hasattr(m, "weights_changed"):
+        m.weights_changed()
 
 
 def train_one_iter(model: nn.Module, optimizer, images: torch.Tensor, targets: torch.Tensor,
@@ -85,12 +93,14 @@ def train_one_iter(model: nn.Module, optimizer, images: torch.Tensor, targets: t
             return outputs
         scaler.step(optimizer)
         scaler.update()
+        _weights_changed(model)
     else:
         loss.backward()
         if fused is not None:
             fused.step()  # SGD + EMA in one pass
             return outputs
         optimizer.step()
+        _weights_changed(model)
     if ema is not None:
         ema.update(model)
     return outputs
@@ -246,7 +256,7 @@ class Trainer:
         self.data_type = torch.float16 if args.fp16 else torch.float32
         self.input_size = tuple(config.input_size)
         self.start_epoch = 0
-        self.history: list = []  # (progress, input_size, loss) per iteration
+        self.last = None  # (progress, input_size, detached loss) of the latest iteration only
 
     def train(self) -> None:
         self.before_train()
@@ -315,11 +325,11 @@ class Trainer:
         lr = self.lr_scheduler.update_lr(self.progress_in_iter + 1)
         for param_group in self.optimizer.param_groups:
             param_group["lr"] = lr
-        self.history.append((self.progress_in_iter, self.input_size, loss))
+        self.last = (self.progress_in_iter, self.input_size, loss.detach())
 
     def after_iter(self) -> None:
         if self.rank == 0 and (self.iter + 1) % self.exp.print_interval == 0:
-            _, size, loss = self.history[-1]
+            _, size, loss = self.last
             print(f"epoch: {self.epoch + 1}/{self.max_epoch}, iter: {self.iter + 1}/{self.max_iter}, "
                   f"total_loss: {float(loss):.3f}, lr: {self.optimizer.param_groups[0]['lr']:.3e}, size: {size[0]}",
                   flush=True)
