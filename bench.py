@@ -309,10 +309,20 @@ def main_train(args, world, rank):
     from yolox_amd.optim import FusedStep
     fused = FusedStep(model, opt, ema)  # SGD + EMA (+ GradScaler under fp16) on the device
 
+    cap = None
+
     def step():
-        return train_one_iter(net, opt, imgs, labels, amp_dtype=amp, scaler=scaler, ema=ema, fused=fused)
+        return train_one_iter(net, opt, imgs, labels, amp_dtype=amp, scaler=scaler, ema=ema, fused=fused,
+                              captured=cap)
 
     for _ in range(args.warmup):
+        out = step()
+    # one process, YOLOX_AMD_TRAIN_GRAPH=1: the forward + reverse pass replays as hipGraph segments
+    if world == 1 and args.warmup >= 1 and os.environ.get("YOLOX_AMD_TRAIN_GRAPH", "0") == "1":
+        from yolox_amd.train import CapturedTrainStep
+        opt.zero_grad(set_to_none=True)
+        cap = CapturedTrainStep(model, imgs, labels, dtype=amp or torch.float32,
+                                grad_scale=scaler._scale if scaler is not None else None)
         out = step()
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
@@ -365,7 +375,8 @@ def main_train(args, world, rank):
                                + (f" (BASELINE configs[{idx}])" if idx is not None else " (not a BASELINE config)"),
                    "baseline_config_index": idx,
                    "batch_per_gpu": B, "global_batch": B * world, "image_size": S,
-                   "parallelism": f"dp{world} (bucketed RCCL all-reduce overlapped with the reverse pass)"},
+                   "parallelism": f"dp{world} (bucketed RCCL all-reduce overlapped with the reverse pass)",
+                   "issue": "hipGraph replay" if cap is not None else "eager"},
         "roofline": {"kernel": "whole step (conv fwd/dgrad/wgrad dominate; HIP events around each step)",
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": None,

@@ -131,6 +131,8 @@ __global__ void amp_update(float* scale, int32_t* tracker, const float* found_in
     }
 }
 
+__global__ void zero_flag(float* f) { *f = 0.f; }
+
 }  // namespace yxh
 
 int yxh_opt_chunk_elems(void) { return yxh::kOptChunk; }
@@ -141,7 +143,9 @@ int yxh_amp_found_inf(const yxh_opt_seg* segs, const int32_t* chunks, int32_t nc
         yxh::set_error("amp_found_inf: null table / output");
         return YXH_EINVAL;
     }
-    int rc = yxh::check_hip(hipMemsetAsync(found_inf, 0, sizeof(float), (hipStream_t)stream), "zero found_inf");
+    // a kernel, not hipMemsetAsync: memset nodes in a captured step broke later replays (train.py)
+    hipLaunchKernelGGL(yxh::zero_flag, dim3(1), dim3(1), 0, (hipStream_t)stream, found_inf);
+    int rc = yxh::check_hip(hipGetLastError(), "zero found_inf");
     if (rc || nchunks == 0) return rc;
     hipLaunchKernelGGL(yxh::amp_found_inf, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, segs, chunks,
                        found_inf);

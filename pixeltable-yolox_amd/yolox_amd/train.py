@@ -184,6 +184,7 @@ class TrainGraph:
                            if self._wside is not None else self.wg_ws)
         self._scratch_side = torch.empty(0, dtype=torch.uint8, device=self.device)
         self._wpending: list = []
+        self._segcap = None  # CapturedTrainStep's segment recorder while it captures
         self.wgrad_group = max(1, int(os.environ.get("YOLOX_AMD_WGRAD_GROUP", "1")))
         # weight repacks: the first step launches one pack per conv (forward layout) and per
         # data-gradient input slice, recording each as a yxh_pack_job; later steps repack
@@ -324,8 +325,12 @@ class TrainGraph:
 
     def _flush_wgrad(self) -> None:
         """Issue the pending weight gradients on the side stream behind ONE fork from the main
-        stream (YOLOX_AMD_WGRAD_GROUP convs per fork, default 1)."""
+        stream (YOLOX_AMD_WGRAD_GROUP convs per fork: fewer cross-stream edges in a captured step)."""
         if not self._wpending:
+            return
+        if self._segcap is not None:  # CapturedTrainStep: a side-stream graph segment of its own
+            self._segcap.side(self._wpending)
+            self._wpending = []
             return
         self._wside.wait_stream(torch.cuda.current_stream(self.device))  # dy written, dW zeroed
         with torch.cuda.stream(self._wside):
@@ -678,7 +683,8 @@ class TrainGraph:
             fn()
         if self._wside is not None:  # every weight gradient is in before the reducer / optimizer
             self._flush_wgrad()
-            torch.cuda.current_stream(self.device).wait_stream(self._wside)
+            if self._segcap is None:
+                torch.cuda.current_stream(self.device).wait_stream(self._wside)
         self.tape = []
         self._keep = None
         if self.batch_pack and self._pack_table is None and self._pack_jobs:
@@ -686,6 +692,137 @@ class TrainGraph:
         if self.on_backward_end is not None:
             self.on_backward_end()
         self.grads.publish(prev)
+
+
+class CapturedTrainStep:
+    """One training forward + reverse pass captured as hipGraph segments (torch.cuda.CUDAGraph
+    objects sharing one memory pool: the main stream's work between two weight-gradient forks,
+    and each fork's weight gradients for the side stream) and replayed for every batch of the
+    same shape: the step's ~850 launches cost the host a few graph launches and events instead
+    of the ctypes issue of every kernel (bench.py reports the eager ``host_issue_ms_per_step``).
+
+    Each call copies the batch into the static input buffers and replays; the loss dict, the
+    SimOTA assignment and the flat gradient buffer are rewritten in place, and ``param.grad``
+    views are (re)published, as after ``optimizer.zero_grad(set_to_none=True)`` +
+    ``loss.backward()`` (trainer.py:104-112).  The weight repacks, the BN running statistics
+    and ``num_batches_tracked`` are inside the graph and read the fp32 master weights through
+    their fixed storage, so in-place optimizer steps between replays are seen.  ``grad_scale``
+    (a one-element fp32 device tensor, e.g. ``GradScaler._scale``) is read by every replay.
+
+    Requirements: the step ran eagerly once for this shape (tiles tuned, the repack table
+    recorded), one process (the data-parallel reducer's per-bucket hooks stay eager), and the
+    parameters keep their storage (``model.to`` / re-created tensors need a new capture)."""
+
+    def __init__(self, model, images: torch.Tensor, targets: torch.Tensor, dtype: Optional[torch.dtype] = None,
+                 grad_scale: Optional[torch.Tensor] = None):
+        g = getattr(model, "_train_graph", None)
+        dtype = dtype or compute_dtype_from_autocast()
+        if g is None or g.dtype != dtype or g.device != model.device:
+            raise RuntimeError("CapturedTrainStep: run one eager training step of this shape first")
+        if g.on_param_ready is not None or g.on_backward_end is not None:
+            raise RuntimeError("CapturedTrainStep: data-parallel reducer hooks are not captured")
+        if g.batch_pack and g._pack_table is None:
+            raise RuntimeError("CapturedTrainStep: the repack table is not recorded yet (run an eager step)")
+        self.model, self.g, self.dev = model, g, model.device
+        self.images = images.to(model.device).clone()
+        self.targets = targets.to(model.device).clone()
+        self.grad_scale = grad_scale
+        if grad_scale is None:
+            g.grad_total.fill_(1.0)
+        for p in g.grads.params:  # the graph overwrites the gradients (no carry-over of held ones)
+            p.grad = None
+        # segments: the main stream's work between two weight-gradient forks is one graph, each
+        # fork's weight gradients another, replayed on the side stream behind an event -- the
+        # concurrency of the eager step.  (One multi-stream capture lets the runtime re-assign
+        # nodes to its own queues, which serialised the weight gradients with the data-gradient
+        # chain on MI355X: profiles/r03/train_graph.txt.)
+        self.pool = None  # the first segment's private pool, shared by the later segments (CUDAGraph.pool())
+        self.plan: list = []  # ("main" | "side", CUDAGraph)
+        self._keep: list = []  # conv-output gradients read by side segments: alive for the whole step
+        self.main = torch.cuda.Stream(self.dev)
+        self.side_stream = g._wside
+        self._dbg = os.environ.get("YOLOX_AMD_CAP_DEBUG", "")
+        if "torch" in self._dbg:  # diagnostic: one torch.cuda.graph capture (side stream forked inside it)
+            self.single = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.single):
+                self.out = g.forward(self.images, self.targets)
+                g.backward(grad_scale)
+            return
+        self.single = None
+        torch.cuda.synchronize(self.dev)
+        if "gc" in self._dbg:
+            import gc
+            gc.collect()
+            torch.cuda.empty_cache()
+        with torch.cuda.stream(self.main):
+            self._begin()
+            g._segcap = self if self.side_stream is not None else None
+            try:
+                self.out = g.forward(self.images, self.targets)
+                g.backward(grad_scale)  # begin(): p.grad is None here, nothing to carry over
+            finally:
+                g._segcap = None
+                self._end()
+        self.events = [torch.cuda.Event() for _ in self.plan]
+
+    def _begin(self) -> None:
+        self._cur = torch.cuda.CUDAGraph()
+        self._cur.capture_begin(pool=self.pool, capture_error_mode="global" if "global" in self._dbg else "thread_local")
+
+    def _end(self) -> None:
+        self._cur.capture_end()
+        if self.pool is None:
+            self.pool = self._cur.pool()
+        self.plan.append(("main", self._cur))
+        self._cur = None
+
+    def side(self, pending: list) -> None:
+        """TrainGraph._flush_wgrad while capturing: close the main segment, capture the
+        pending weight gradients as a side segment, open the next main segment."""
+        self._end()
+        gs = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(self.side_stream):
+            gs.capture_begin(pool=self.pool, capture_error_mode="thread_local")
+            for launch, dy, _ in pending:
+                launch()
+                self._keep.append(dy)
+            gs.capture_end()
+        self.plan.append(("side", gs))
+        self._begin()
+
+    def _replay(self) -> None:
+        caller = torch.cuda.current_stream(self.dev)
+        self.main.wait_stream(caller)
+        fork = None
+        with torch.cuda.stream(self.main):
+            for (kind, gr), ev in zip(self.plan, self.events):
+                if kind == "main":
+                    gr.replay()
+                    fork = ev
+                    ev.record(self.main)
+                else:
+                    self.side_stream.wait_event(fork)
+                    with torch.cuda.stream(self.side_stream):
+                        gr.replay()
+            if self.side_stream is not None:
+                self.main.wait_stream(self.side_stream)
+        caller.wait_stream(self.main)
+
+    def __call__(self, images: torch.Tensor, targets: torch.Tensor) -> dict:
+        if images.shape != self.images.shape or targets.shape != self.targets.shape:
+            raise ValueError("CapturedTrainStep: batch shape differs from the captured one")
+        if images.data_ptr() != self.images.data_ptr():
+            self.images.copy_(images, non_blocking=True)
+        if targets.data_ptr() != self.targets.data_ptr():
+            self.targets.copy_(targets, non_blocking=True)
+        if self.single is not None:
+            self.single.replay()
+        else:
+            self._replay()
+        self.g.grads.publish(None)
+        if hasattr(self.model, "weights_changed"):  # BN running statistics were updated in place
+            self.model.weights_changed()
+        return dict(self.out)
 
 
 class _LossFn(torch.autograd.Function):

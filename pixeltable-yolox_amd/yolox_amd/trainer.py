@@ -75,13 +75,22 @@ def _weights_changed(model: nn.Module) -> None:
 
 def train_one_iter(model: nn.Module, optimizer, images: torch.Tensor, targets: torch.Tensor,
                    amp_dtype: Optional[torch.dtype] = None, scaler=None, ema: Optional[ModelEMA] = None,
-                   fused=None) -> dict:
+                   fused=None, captured=None) -> dict:
     """trainer.py:96-129 (minus data loading / logging / LR schedule).
 
     ``fused`` (yolox_amd.optim.FusedStep over the same optimizer and EMA) replaces
     ``optimizer.step()`` + ``ema.update(model)`` with one HIP pass; with a GradScaler
     (--fp16) it also takes over ``scaler.step`` / ``scaler.update`` (inf check, unscale,
-    skip, scale update on the device, no host sync)."""
+    skip, scale update on the device, no host sync).
+
+    ``captured`` (yolox_amd.train.CapturedTrainStep of this batch shape, its grad_scale the
+    scaler's scale under fp16) replaces the forward + ``backward()`` with one graph replay."""
+    if captured is not None:
+        if fused is None:
+            raise ValueError("train_one_iter(captured=...) needs the fused optimizer step")
+        outputs = captured(images, targets)
+        fused.step(scaler)
+        return outputs
     with torch.autocast("cuda", dtype=amp_dtype or torch.float16, enabled=amp_dtype is not None):
         outputs = model(images, targets)
     loss = outputs["total_loss"]

@@ -662,3 +662,54 @@ def test_batched_weight_repack_matches_per_conv(monkeypatch, dtype):
     assert not m2._train_graph.batch_pack
     for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss", "num_fg"):
         assert float(out[k]) == float(ref[k]), k
+
+
+@pytest.mark.parametrize("opt_kind", ["sgd", "fused"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_captured_train_step_matches_eager(monkeypatch, dtype, opt_kind):
+    """CapturedTrainStep (the forward + reverse pass as hipGraph segments: main-stream graphs
+    between weight-gradient forks, side-stream graphs behind events) gives the eager step's
+    losses, parameter gradients and BN running statistics bit for bit, over three optimizer
+    steps (torch SGD or the fused HIP SGD step) between replays; the replay repacks the
+    updated master weights, and another model's eager step runs between two replays
+    (allocating and freeing from the caching allocator).  Round 3's version of this test
+    failed on the second replay: the five hipMemsetAsync nodes SimOTA's setup captured broke
+    every replay after the first (replaced by the sim_init kernel, tools/cap_probe.py)."""
+    from yolox_amd.optim import FusedStep
+    import yolox_amd.train as T
+    monkeypatch.setenv("YOLOX_AMD_TRAIN_TUNE", "0")
+    monkeypatch.setattr(T, "_TRAIN_TILES", {})
+    m1, sd, x, labels, _ = _model_and_batch()
+    m2, _, _, _, _ = _model_and_batch()
+    xs, ls = x.cuda(), labels.cuda()
+    ctx = ((lambda: torch.autocast("cuda", dtype=dtype)) if dtype != torch.float32
+           else (lambda: torch.autocast("cuda", enabled=False)))
+    mods = []
+    for m in (m1, m2):
+        m = m.cuda().train()
+        opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, nesterov=True)
+        step = FusedStep(m, opt, None).step if opt_kind == "fused" else opt.step
+        with ctx():
+            m(xs, ls)["total_loss"].backward()  # eager warm-up (tiles, repack table)
+        step()
+        mods.append((m, opt, step))
+    (m1, o1, s1), (m2, o2, s2) = mods
+    with ctx():
+        cap = T.CapturedTrainStep(m2, xs, ls)
+    for it in range(3):
+        o1.zero_grad(set_to_none=True)
+        with ctx():
+            ref = m1(xs, ls)
+        ref["total_loss"].backward()
+        got = cap(xs, ls)
+        torch.cuda.synchronize()
+        for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss", "num_fg"):
+            assert float(got[k]) == float(ref[k]), (it, k)
+        p1, p2 = dict(m1.named_parameters()), dict(m2.named_parameters())
+        for name in p1:
+            assert torch.equal(p1[name].grad, p2[name].grad), (it, name)
+        b1, b2 = dict(m1.named_buffers()), dict(m2.named_buffers())
+        for name in b1:
+            assert torch.equal(b1[name], b2[name]), (it, name)
+        s1()
+        s2()
