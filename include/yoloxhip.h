@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 14
+#define YXH_ABI_VERSION 15
 
 enum yxh_status {
     YXH_OK = 0,
@@ -183,6 +183,24 @@ typedef struct {
     int32_t dst_cstride;
     int32_t reserved;
     int64_t dst_bstride;
+    /* ABI 15, optional CSP form (w3 != NULL): dark2's CspLayer conv1 | conv2 and its first
+     * Bottleneck conv1 (network_blocks.py:176-178, 95-96) in the same launch.  The stride-2 map
+     * is then NOT stored (dst unused):
+     *   dst3 <- SiLU(w3 . map + b3), w3 [c2][c2] (conv1 rows then conv2 rows), whole 16-byte
+     *           aligned rows of dst3_cstride elements;
+     *   dst4 <- SiLU(w4 . dst3[:, :c2/2] + b4), w4 [c2/2][c2/2] (optional: w4 NULL skips it). */
+    const void* w3;
+    const float* b3;
+    void* dst3;
+    int32_t dst3_cstride;
+    int32_t reserved3;
+    int64_t dst3_bstride;
+    const void* w4;
+    const float* b4;
+    void* dst4;
+    int32_t dst4_cstride;
+    int32_t reserved4;
+    int64_t dst4_bstride;
 } yxh_stem2_desc;
 int yxh_stem_s2(const yxh_stem2_desc* d, void* stream);
 int yxh_stem_conv(const yxh_stem_desc* d, void* stream);

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -108,7 +108,11 @@ class Stem2Desc(C.Structure):
     _fields_ = [("img", C.c_void_p), ("layout", C.c_int32), ("img_dtype", C.c_int32), ("batch", C.c_int32),
                 ("h", C.c_int32), ("w", C.c_int32), ("dtype", C.c_int32), ("c1", C.c_int32), ("c2", C.c_int32),
                 ("act", C.c_int32), ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p),
-                ("dst", C.c_void_p), ("dst_cstride", C.c_int32), ("reserved", C.c_int32), ("dst_bstride", C.c_int64)]
+                ("dst", C.c_void_p), ("dst_cstride", C.c_int32), ("reserved", C.c_int32), ("dst_bstride", C.c_int64),
+                ("w3", C.c_void_p), ("b3", C.c_void_p), ("dst3", C.c_void_p), ("dst3_cstride", C.c_int32),
+                ("reserved3", C.c_int32), ("dst3_bstride", C.c_int64), ("w4", C.c_void_p), ("b4", C.c_void_p),
+                ("dst4", C.c_void_p), ("dst4_cstride", C.c_int32), ("reserved4", C.c_int32),
+                ("dst4_bstride", C.c_int64)]
 
 
 class AugImage(C.Structure):

@@ -108,13 +108,15 @@ class OpRec:
 # process on one box (tools/ab_fuse.py) the two-launch form is 1.8 % faster (2.001 vs 2.038 ms per
 # yolox_s bs32 forward) -- the fused kernel's 1x1-on-the-halo phase is not overlapped with MFMAs
 _FUSE_BOTTLENECK = os.environ.get("YOLOX_AMD_FUSE_BOTTLENECK", "0") == "1"
+# 1x1 convs folded into the launch that produces their input (YOLOX_AMD_CSP_FUSION=0: separate launches)
+_CSP_FUSION = os.environ.get("YOLOX_AMD_CSP_FUSION", "1") != "0"
 # fragment-major weight copies for the weight-stationary tiles (YOLOX_AMD_WFRAG=0: row layout only)
 _WFRAG = os.environ.get("YOLOX_AMD_WFRAG", "1") != "0"
 
 
 class PlanCtx:
     def __init__(self, batch: int, dtype: torch.dtype, device: torch.device, fuse_stem: bool = True,
-                 fuse_bottleneck: bool = _FUSE_BOTTLENECK, fuse_stem_s2: bool = True):
+                 fuse_bottleneck: bool = _FUSE_BOTTLENECK, fuse_stem_s2: bool = True, csp_fusion: Optional[bool] = None):
         if dtype not in (torch.float32, torch.bfloat16, torch.float16):
             raise ValueError(f"compute dtype {dtype} not supported (float32, bfloat16, float16)")
         self.batch = batch
@@ -125,6 +127,8 @@ class PlanCtx:
         self.device = device
         self.fuse_stem = fuse_stem
         self.fuse_stem_s2 = fuse_stem_s2  # Focus stem + dark2[0] as one yxh_stem_s2 launch
+        # 1x1 convs folded into a neighbouring launch (stem_s2's CSP form; YOLOX_AMD_CSP_FUSION=0: off)
+        self.csp_fusion = (_CSP_FUSION if csp_fusion is None else csp_fusion) and dtype != torch.float32
         # the image the plan reads (set by Plan): the fused stem + stride-2 conv needs NHWC
         self.input_layout = N.NHWC
         self.input_dtype = torch.uint8
@@ -179,19 +183,50 @@ class PlanCtx:
     def stem_s2(self, stem, conv, img: ImageRef) -> View:
         """Focus + stem BaseConv + dark2[0] (darknet.py:112-123) as ONE launch: the stem map
         exists only per tile in LDS (csrc/stem_s2.hip)."""
+        return self._stem_s2(stem, conv, img)[0]
+
+    def stem_s2_csp_fusable(self, csp) -> bool:
+        """dark2's CspLayer conv1 | conv2 (1x1 64 -> 2 x 32) and its first Bottleneck's conv1
+        (1x1 32 -> 32) can ride in the stem_s2 launch (yxh_stem2_desc.w3 / w4)."""
+        if not (self.csp_fusion and not self.fuse_bottleneck and hasattr(csp, "conv1") and len(csp.m) >= 1):
+            return False
+        b0 = csp.m[0]
+        k1, k2, kb = csp.conv1.conv, csp.conv2.conv, getattr(b0.conv1, "conv", None)
+        ok = kb is not None and all(k.kernel_size == (1, 1) and k.groups == 1 and k.stride == (1, 1) for k in (k1, k2, kb))
+        return (ok and k1.in_channels == 64 and k1.out_channels == 32 and k2.out_channels == 32
+                and kb.in_channels == 32 and kb.out_channels == 32
+                and {getattr(m, "act_name", "silu") for m in (csp.conv1, csp.conv2, b0.conv1)} == {"silu"})
+
+    def stem_s2_csp(self, stem, conv, csp, img: ImageRef) -> tuple:
+        """stem_s2 + dark2's CspLayer conv1 | conv2 + its first Bottleneck conv1 as ONE launch:
+        returns (the [x_1 | x_2] concat buffer, the Bottleneck's hidden map t)."""
+        _, cat, t = self._stem_s2(stem, conv, img, csp)
+        return cat, t
+
+    def _stem_s2(self, stem, conv, img: ImageRef, csp=None) -> tuple:
         if img.h % 4 or img.w % 4:
             raise ValueError("stem_s2 needs image sides that are multiples of 4")
         oh1, ow1 = img.h // 2, img.w // 2
         oh, ow = (oh1 - 1) // 2 + 1, (ow1 - 1) // 2 + 1
         c1, c2 = stem.conv.out_channels, conv.conv.out_channels
-        out = self.buffer(oh, ow, c2)
         s1 = WeightSpec([(stem.conv, stem.bn)], c1, 12, 3, 3, 12, stem=True)
         self.weights.append(s1)
         s2 = self._weights([(conv.conv, conv.bn)], c1)
-        self.ops.append(OpRec(N.OP_STEM2, dict(dst=out.full(), h=img.h, w=img.w, spec1=s1, spec2=s2, c1=c1, c2=c2,
-                                               act=N.ACT_SILU)))
+        args = dict(h=img.h, w=img.w, spec1=s1, spec2=s2, c1=c1, c2=c2, act=N.ACT_SILU)
         self.flops += 2.0 * self.batch * oh1 * ow1 * c1 * 9 * 12 + 2.0 * self.batch * oh * ow * c2 * 9 * c1
-        return out.full()
+        if csp is None:
+            out = self.buffer(oh, ow, c2)
+            self.ops.append(OpRec(N.OP_STEM2, dict(dst=out.full(), **args)))
+            return out.full(), None, None
+        hidden = csp.conv1.conv.out_channels
+        b0 = csp.m[0]
+        cat = self.buffer(oh, ow, 2 * hidden)
+        t = self.buffer(oh, ow, hidden)
+        s3 = self._weights([(csp.conv1.conv, csp.conv1.bn), (csp.conv2.conv, csp.conv2.bn)], c2)
+        s4 = self._weights([(b0.conv1.conv, b0.conv1.bn)], hidden)
+        self.ops.append(OpRec(N.OP_STEM2, dict(dst=None, dst3=cat.full(), dst4=t.full(), spec3=s3, spec4=s4, **args)))
+        self.flops += 2.0 * self.batch * oh * ow * (2 * hidden * c2 + hidden * hidden)
+        return None, cat, t.full()
 
     def focus(self, h: int, w: int) -> View:
         packed = self.buffer(h // 2, w // 2, 16)
@@ -388,6 +423,8 @@ def op_buffers(r: OpRec) -> tuple:
     a = r.args
     if r.kind == N.OP_SPP:
         return [a["buf"]], [a["buf"]]
+    if r.kind == N.OP_STEM2 and a.get("dst") is None:
+        return [], [a["dst3"].buf, a["dst4"].buf]
     if r.kind in (N.OP_FOCUS, N.OP_STEM, N.OP_STEM2):
         return [], [a["dst"].buf]
     if r.kind == N.OP_HEAD:
@@ -448,7 +485,7 @@ class Plan:
                  input_layout: int = N.NCHW, input_dtype: torch.dtype = torch.float32, train: bool = False,
                  fuse_stem: bool = True, chunk: Optional[int] = None, fuse_bottleneck: bool = _FUSE_BOTTLENECK,
                  parallel_chunks: bool = False, fuse_stem_s2: bool = True, stage: str = "full",
-                 head_inputs: Optional[list] = None):
+                 head_inputs: Optional[list] = None, csp_fusion: Optional[bool] = None):
         """``stage``: "full" (image -> decoded rows), "features" (image -> the three PAFPN
         maps: YoloPafpn.forward) or "head" (three feature maps of ``head_inputs`` shapes
         [(C, H, W)] -> decoded rows: YoloxHead.forward)."""
@@ -471,7 +508,7 @@ class Plan:
         head = model.head
         self.num_classes = head.num_classes if head is not None else 0
         ctx = PlanCtx(chunk, dtype, self.device, fuse_stem=fuse_stem, fuse_bottleneck=fuse_bottleneck,
-                      fuse_stem_s2=fuse_stem_s2)
+                      fuse_stem_s2=fuse_stem_s2, csp_fusion=csp_fusion)
         ctx.input_layout, ctx.input_dtype = input_layout, input_dtype
         if stage == "head":
             if chunk != batch or not head_inputs or len(head_inputs) != 3:
@@ -602,8 +639,17 @@ class Plan:
                 t.w2 = self.warena.data_ptr() + a["spec2"].w_off
                 t.b2 = self.barena.data_ptr() + a["spec2"].b_off
                 v = a["dst"]
-                t.dst = self._ptr(v, c)
-                t.dst_cstride, t.dst_bstride = v.buf.c, v.buf.nelem_image
+                if v is not None:
+                    t.dst = self._ptr(v, c)
+                    t.dst_cstride, t.dst_bstride = v.buf.c, v.buf.nelem_image
+                else:  # CSP form: conv1 | conv2 -> dst3, the first Bottleneck's conv1 -> dst4
+                    t.dst = None
+                    for name, spec, view in (("3", a["spec3"], a["dst3"]), ("4", a["spec4"], a["dst4"])):
+                        setattr(t, "w" + name, self.warena.data_ptr() + spec.w_off)
+                        setattr(t, "b" + name, self.barena.data_ptr() + spec.b_off)
+                        setattr(t, "dst" + name, self._ptr(view, c))
+                        setattr(t, f"dst{name}_cstride", view.buf.c)
+                        setattr(t, f"dst{name}_bstride", view.buf.nelem_image)
                 t.img = None
                 self._input_index = i
             elif rec.kind == N.OP_HEAD:

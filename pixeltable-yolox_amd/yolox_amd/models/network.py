@@ -136,8 +136,18 @@ class CspLayer(_Planned):
         self.conv3 = BaseConv(2 * hidden, out_channels, 1, stride=1, act=act)
         self.m = nn.Sequential(*[Bottleneck(hidden, hidden, shortcut, 1.0, depthwise, act=act) for _ in range(n)])
 
-    def plan(self, ctx, srcs, out=None):
+    def plan(self, ctx, srcs, out=None, fused_head=None):
+        """``fused_head``: (the [x_1 | x_2] buffer, the first Bottleneck's hidden map) already
+        written by the launch that produced this layer's input (stem_s2's CSP form)."""
         hidden = self.conv1.conv.out_channels
+        if fused_head is not None:
+            cat, t0 = fused_head
+            x1 = cat.slice(0, hidden)
+            b0 = self.m[0]
+            b0.conv2.plan(ctx, [t0], out=x1, residual=x1 if b0.use_add else None)
+            for b in list(self.m)[1:]:
+                b.plan(ctx, x1, out=x1)
+            return self.conv3.plan(ctx, [cat.full()], out=out)
         cat = ctx.buffer(srcs[0].lh, srcs[0].lw, 2 * hidden)
         x1 = cat.slice(0, hidden)
         # conv1 | conv2 read the same input: one conv writes the whole [x_1 | x_2]
@@ -194,14 +204,24 @@ class CspDarknet(_Planned):
 
     def plan(self, ctx, packed):
         fused = ctx.stem_s2_fusable(self.stem.conv, self.dark2[0])
-        # Focus stem + dark2[0] as one launch where the geometry allows (yxh_stem_s2)
-        x = ctx.stem_s2(self.stem.conv, self.dark2[0], packed) if fused else self.stem.plan(ctx, packed)
+        csp2 = self.dark2[1]
+        head2 = None
+        # Focus stem + dark2[0] as one launch where the geometry allows (yxh_stem_s2), with
+        # dark2's CspLayer conv1 | conv2 and first Bottleneck conv1 in the same launch if they fit
+        if fused and isinstance(csp2, CspLayer) and ctx.stem_s2_csp_fusable(csp2) and len(self.dark2) == 2:
+            head2 = ctx.stem_s2_csp(self.stem.conv, self.dark2[0], csp2, packed)
+            x = None
+        else:
+            x = ctx.stem_s2(self.stem.conv, self.dark2[0], packed) if fused else self.stem.plan(ctx, packed)
         feats = []
         for stage in (self.dark2, self.dark3, self.dark4, self.dark5):
             if not (fused and stage is self.dark2):
                 x = stage[0].plan(ctx, [x])
             for blk in list(stage)[1:]:
-                x = blk.plan(ctx, [x])
+                if head2 is not None and blk is csp2:
+                    x = blk.plan(ctx, None, fused_head=head2)
+                else:
+                    x = blk.plan(ctx, [x])
             feats.append(x)
         return feats[1], feats[2], feats[3]  # dark3, dark4, dark5
 

@@ -130,8 +130,12 @@ def test_planner_topology_and_flops(name, hw, gflop, anchors):
     # ... and a 16-bit plan runs cls_convs[k][1] | reg_convs[k][1] as one two-group launch
     n_grouped = sum(1 for o in ctx.ops if o.args.get("grouped2"))
     assert n_grouped == (3 if name in ("yolox_s", "yolox_l") else n_grouped)
+    # ... and yolox_s's dark2 CspLayer conv1 | conv2 and first Bottleneck conv1 ride in the
+    # stem_s2 launch (its CSP form: two conv ops fewer)
+    n_stem_csp = sum(1 for o in ctx.ops if o.kind == 5 and o.args.get("dst") is None)
+    assert n_stem_csp == (1 if name == "yolox_s" else 0)
     assert (kinds.count(0) == n_bn_convs - n_csp - fused_head + 2 * (3 - heads) - 1 - n_fused_bneck - n_grouped
-            - s2)
+            - s2 - 2 * n_stem_csp)
 
 
 def test_planner_fused_bottleneck_ping_pong():

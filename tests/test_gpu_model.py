@@ -220,6 +220,33 @@ def test_fused_stem_s2_plan_matches_unfused_plan():
     assert torch.equal(fused.replay().clone(), a)
 
 
+@pytest.mark.parametrize("hw", [(160, 192), (640, 640)])
+def test_csp_fusion_plan_matches_split_plan(hw):
+    """Round 4: 1x1 convs folded into the launch that produces their input (stem_s2's CSP
+    form: dark2's CspLayer conv1 | conv2 + first Bottleneck conv1) vs the plan with every
+    conv its own launch.  The fused kernels round the same intermediate maps to bf16; the
+    split plan's by-shape tiles may sum K in another order (K slabs), so the bound is a few
+    bf16 ulps propagated through the network, well inside the bf16 forward bounds."""
+    from yolox_amd import _native as N
+    from yolox_amd.engine import Plan
+    from yolox_amd.weights import synthetic_images
+    m = model("yolox_s", torch.bfloat16)
+    H, W = hw
+    x = torch.from_numpy(synthetic_images(2, H, W, seed=13)).cuda()
+    fused = Plan(m, 2, H, W, torch.bfloat16, "cuda", N.NHWC, torch.uint8, csp_fusion=True)
+    split = Plan(m, 2, H, W, torch.bfloat16, "cuda", N.NHWC, torch.uint8, csp_fusion=False)
+    assert any(r.kind == N.OP_STEM2 and r.args.get("dst") is None for r in fused.ctx.ops)
+    assert len(fused.ctx.ops) < len(split.ctx.ops)
+    a = fused.run(x).clone()
+    b = split.run(x).clone()
+    torch.cuda.synchronize()
+    dp = (a[..., 4:] - b[..., 4:]).abs()
+    assert dp.max().item() < 0.05 and dp.float().quantile(0.99).item() < 0.01
+    assert (a[..., :2] - b[..., :2]).abs().max().item() < 0.5
+    fused.static_input().copy_(x)
+    assert torch.equal(fused.replay().clone(), a)
+
+
 def test_submodules_are_callable_like_the_reference(golden):
     """module.backbone(x) and module.head(feats) run standalone (reference YoloPafpn.forward,
     yolo_pafpn.py:83-116; YoloxHead.forward eval, yolo_head.py:140-211): the PAFPN maps match

@@ -973,6 +973,63 @@ def test_stem_s2_fused_vs_reference(idt, dtype, hw):
     assert err < TOL[dtype], err
 
 
+@pytest.mark.parametrize("with4", [True, False])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("hw", [(128, 128), (100, 68), (36, 260)])
+def test_stem_s2_csp_form_vs_reference(dtype, hw, with4):
+    """yxh_stem_s2's CSP form (round 4): the stride-2 map stays in LDS; dark2's CspLayer
+    conv1 | conv2 (1x1 64 -> 64, network_blocks.py:176-178) over it goes to dst3 and the first
+    Bottleneck's conv1 (1x1 32 -> 32, :95-96) over its x_1 half to dst4 -- vs the reference
+    order in fp32 with every stored map rounded to the compute dtype.  Destinations wider than
+    the written channels keep their other channels."""
+    n = N()
+    H, W = hw
+    img = torch.randint(0, 256, (2, 3, H, W)).float()
+    src = img.permute(0, 2, 3, 1).to(DEV, torch.uint8).contiguous()
+    c1, bn1 = make_conv(12, 32, 3, 1, seed=5)
+    c2, bn2 = make_conv(32, 64, 3, 2, seed=6)
+    c3, bn3 = make_conv(64, 64, 1, 1, seed=7)
+    c4, bn4 = make_conv(32, 32, 1, 1, seed=8)
+    f = lambda t: t.detach().float().contiguous().to(DEV)  # noqa: E731
+    args = [f(c1.weight), f(bn1.weight), f(bn1.bias), f(bn1.running_mean), f(bn1.running_var)]
+    w1 = torch.empty(32 * 6 * 32, dtype=dtype, device=DEV)
+    b1 = torch.empty(32, dtype=torch.float32, device=DEV)
+    n.check(n.lib().yxh_stem_pack(*[a.data_ptr() for a in args], float(bn1.eps), 32, n.DTYPE_CODE[dtype],
+                                  w1.data_ptr(), b1.data_ptr(), n.stream_ptr()), "stem pack")
+    w2, b2 = pack(c2, bn2, dtype)
+    w3, b3 = pack(c3, bn3, dtype)
+    w4, b4 = pack(c4, bn4, dtype)
+    oh, ow = (H // 2 - 1) // 2 + 1, (W // 2 - 1) // 2 + 1
+    cs3, cs4 = 72, 40
+    dst3 = torch.full((2, oh, ow, cs3), 7.0, dtype=dtype, device=DEV)
+    dst4 = torch.full((2, oh, ow, cs4), 7.0, dtype=dtype, device=DEV)
+    d = n.Stem2Desc()
+    d.img, d.layout, d.img_dtype, d.batch, d.h, d.w = src.data_ptr(), n.NHWC, n.U8, 2, H, W
+    d.dtype, d.c1, d.c2, d.act = n.DTYPE_CODE[dtype], 32, 64, n.ACT_SILU
+    d.w1, d.b1, d.w2, d.b2 = w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr()
+    d.dst = None
+    d.w3, d.b3, d.dst3, d.dst3_cstride, d.dst3_bstride = w3.data_ptr(), b3.data_ptr(), dst3.data_ptr(), cs3, oh * ow * cs3
+    if with4:
+        d.w4, d.b4, d.dst4, d.dst4_cstride, d.dst4_bstride = (w4.data_ptr(), b4.data_ptr(), dst4.data_ptr(), cs4,
+                                                              oh * ow * cs4)
+    n.check(n.lib().yxh_stem_s2(ctypes.byref(d), n.stream_ptr()), "stem_s2 csp")
+    torch.cuda.synchronize()
+    x = torch.cat([img[..., ::2, ::2], img[..., 1::2, ::2], img[..., ::2, 1::2], img[..., 1::2, 1::2]], 1)
+    s = ref_conv(x, c1, bn1, "silu").to(dtype).float()
+    y = ref_conv(s, c2, bn2, "silu").to(dtype).float()
+    z = ref_conv(y, c3, bn3, "silu")
+    got3 = dst3.float().cpu().permute(0, 3, 1, 2)
+    assert (got3[:, 64:] == 7.0).all()
+    assert (got3[:, :64] - z).abs().max().item() / z.abs().max().item() < TOL[dtype]
+    got4 = dst4.float().cpu().permute(0, 3, 1, 2)
+    if with4:
+        t = ref_conv(z.to(dtype).float()[:, :32], c4, bn4, "silu")
+        assert (got4[:, 32:] == 7.0).all()
+        assert (got4[:, :32] - t).abs().max().item() / t.abs().max().item() < TOL[dtype]
+    else:
+        assert (got4 == 7.0).all()
+
+
 def test_stem_s2_rejects_what_it_does_not_build():
     n = N()
     d = n.Stem2Desc()

@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU box: a focused test selection, then the default bench (+ optional env A/B of the bench).
+# Usage: TESTS="tests/x.py -k y" AB="ENV=0 ENV=1" bash tools/gpu_iter.sh TAG
+set -o pipefail
+TAG=${1:-it}
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+if [ -n "$TESTS" ]; then
+  eval timeout -k 10 400 python -u -m pytest $TESTS -m gpu -x -q --timeout 200 --timeout-method thread \
+      > gpurun_out/tests_$TAG.log 2>&1; rc=$?
+  tail -4 gpurun_out/tests_$TAG.log
+  [ $rc -eq 0 ] || { grep -E "^E |Error" gpurun_out/tests_$TAG.log | head -20; exit $rc; }
+fi
+for e in ${AB:-DEFAULT=1}; do
+  env $e timeout -k 10 300 python -u bench.py --no-cpu-baseline --layers > gpurun_out/bench_${TAG}_$e.json \
+      2> gpurun_out/bench_${TAG}_$e.err || { tail -5 gpurun_out/bench_${TAG}_$e.err; exit 1; }
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], 'img/s fwd', d['roofline']['forward_ms'], 'ms frac', d['roofline']['frac'])" gpurun_out/bench_${TAG}_$e.json $e
+done
