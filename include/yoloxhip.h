@@ -121,6 +121,21 @@ typedef struct {
      * stationary weights as whole 1 KiB wave reads (every lane one 16-byte piece of one
      * 128-byte line) instead of sixteen 64-byte row pieces per read; other tiles ignore it. */
     const void* weight_frag;
+    /* ABI 15, optional 1x1 post conv (network_blocks.py:180-183 CspLayer.conv3 over the concat
+     * [x_1 | x_2] after its last Bottleneck; :176-178 conv1 | conv2 after a stage's stride-2
+     * conv).  When post_weight is set the conv's output (activation and residual applied,
+     * rounded to dtype) is NOT stored to dst; a block keeps its output tile in LDS and writes
+     *   post_dst <- SiLU(post_weight . [tile | post_src] + post_bias)
+     * post_weight [post_cout][cout + post_src.channels] in dtype (the concat order), post_src
+     * an optional second operand read at the conv's output pixels (channels 0: none).
+     * conv_ws post tiles only (16-bit 3x3 whose block owns all cout channels). */
+    const void* post_weight;
+    const float* post_bias;
+    yxh_src post_src;
+    void* post_dst;
+    int32_t post_cout;
+    int32_t post_dst_cstride;
+    int64_t post_dst_bstride;
 } yxh_conv_desc;
 
 #define YXH_CONV_ACCUMULATE 1

@@ -434,7 +434,7 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     YXH_CHECK_ARG(d->cin > 0 && d->cout > 0 && d->kh > 0 && d->kw > 0 && d->stride > 0 && d->pad >= 0,
                   "bad conv geometry");
     YXH_CHECK_ARG(d->nsrc == 1 || d->nsrc == 2, "nsrc %d", d->nsrc);
-    YXH_CHECK_ARG(d->weight && d->bias && d->dst, "null weight/bias/dst");
+    YXH_CHECK_ARG(d->weight && d->bias && (d->dst || d->post_weight), "null weight/bias/dst");
     YXH_CHECK_ARG(d->dst_dtype == dt || d->dst_dtype == YXH_F32, "dst dtype %d", d->dst_dtype);
     YXH_CHECK_ARG(d->act >= YXH_ACT_NONE && d->act <= YXH_ACT_DECODE_TRAIN, "act %d", d->act);
     YXH_CHECK_ARG(d->act < YXH_ACT_DECODE || d->dst_dtype == YXH_F32, "decode needs an f32 dst");
@@ -513,6 +513,35 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     p.res_dense = d->residual && d->res_bstride == (long long)p.ohw * d->res_cstride;
     p.pw1 = d->pre_weight;
     p.pb1 = d->pre_bias;
+    if (d->post_weight) {
+        YXH_CHECK_ARG(dt != YXH_F32 && d->post_bias && d->post_dst && aligned16(d->post_weight) && d->post_cout > 0 &&
+                          d->post_cout % 16 == 0 && d->kh == 3 && d->groups == 1 && !d->pre_weight && !grp2 &&
+                          d->post_src.channels >= 0 && d->post_src.channels % 32 == 0 &&
+                          (d->post_src.channels == 0 || (d->post_src.ptr && aligned16(d->post_src.ptr) &&
+                                                         d->post_src.cstride % 8 == 0 && d->post_src.bstride % 8 == 0 &&
+                                                         !d->post_src.upsample && d->post_src.h == d->out_h &&
+                                                         d->post_src.w == d->out_w)) &&
+                          ((uintptr_t)d->post_dst % 8) == 0 && d->post_dst_cstride % 4 == 0 &&
+                          d->post_dst_bstride % 4 == 0,
+                      "post conv: 16-bit 3x3 conv (no pre_weight / groups), post_cout %% 16, post_src channels %% 32 "
+                      "at the output size (16-byte rows), 8-byte aligned post_dst rows");
+        p.pgw = d->post_weight;
+        p.pgb = d->post_bias;
+        p.pgd = d->post_dst;
+        p.pgd_cs = d->post_dst_cstride;
+        p.pgd_bs = d->post_dst_bstride;
+        p.pgs = d->post_src.channels ? d->post_src.ptr : nullptr;
+        p.pgs_cs = d->post_src.cstride;
+        p.pgs_bs = d->post_src.bstride;
+        p.pgs_ch = d->post_src.channels;
+        p.pg_cout = d->post_cout;
+        if (d->tile == 0)  // default post tile per shape
+            return conv_ws_dispatch(dt, d->stride == 2 ? 45 : d->cin == 32 ? 41 : 43, p, st);
+        if (!((d->tile >> 1) > 220 && (d->tile >> 1) <= 220 + kNumWsPostTiles)) {
+            set_error("a post conv runs on the conv_ws post tiles (ids 221-%d) only", 220 + kNumWsPostTiles);
+            return YXH_EUNSUPPORTED;
+        }
+    }
     YXH_CHECK_ARG(!d->weight_frag || (dt != YXH_F32 && aligned16(d->weight_frag) && d->cout % 16 == 0 &&
                                       d->cin % 32 == 0 && d->groups == 1),
                   "weight_frag: 16-bit, cout %% 16 == 0, cin %% 32 == 0, groups 1");
@@ -563,13 +592,15 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
                           (tile > 80 && tile <= 80 + kNumPwrTiles) || (tile > 96 && tile <= 96 + kNumPwfTiles) ||
                           (tile > 112 && tile <= 112 + kNumR3Tiles) || (tile > 160 && tile <= 160 + kNumWsTiles) ||
                           (tile > 200 && tile <= 200 + kNumWs1Tiles) || (tile > 210 && tile <= 210 + kNumPw1fTiles) ||
-                          (tile > 214 && tile <= 214 + kNumDgradS2Tiles),
+                          (tile > 214 && tile <= 214 + kNumDgradS2Tiles) ||
+                          (tile > 220 && tile <= 220 + kNumWsPostTiles),
                       "tile %d", d->tile);
         YXH_CHECK_ARG(want_ks == 1 || ks == 2, "2-slab staging not possible for this conv");
         ks = want_ks;
     }
     const int kstage = 4 * ks * epc;
     p.ncb = (d->cin + kstage - 1) / kstage;
+    if (tile > 220) return conv_ws_dispatch(dt, tile - 220 + 40, p, st);
     if (tile > 214) return dgrad_s2f_dispatch(dt, tile - 214, p, st);
     if (dilated && tile > 16) {
         set_error("dilated (upsample == 2) sources run on the register-staged kernel only (tile ids 1-9)");

@@ -32,6 +32,16 @@ struct ConvParams {
     int grp2;  // YXH_CONV_GROUPS2: output half g reads source channels [g*cin, (g+1)*cin)
     const void* wf;  // weights in yxh_pack_frag's fragment-major layout, or null (conv_ws / conv_ws1)
     int cus;         // CUs the persistent grids may occupy (yxh_conv_desc.grid_cap; 256 = all)
+    // 1x1 post conv (yxh_conv_desc.post_*): conv_ws post tiles only
+    const void* pgw;
+    const float* pgb;
+    void* pgd;
+    int pgd_cs;
+    long long pgd_bs;
+    const void* pgs;
+    int pgs_cs, pgs_ch;
+    long long pgs_bs;
+    int pg_cout;
 };
 
 // Stationary weight fragment (i: 16 output channels from n_first, tap, kb: 32-channel K block)
@@ -287,6 +297,9 @@ constexpr int kNumR3Tiles = 48;  // ids beyond the built ones report EINVAL
 // Weight-stationary persistent 3x3 conv (conv_ws.hip): tile ids 161..160+kNumWsTiles
 int conv_ws_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumWsTiles = 36;  // 31..36: fused Bottleneck (pre_weight)
+// conv_ws tiles with a 1x1 post conv (yxh_conv_desc.post_weight): tile ids 221..220+kNumWsPostTiles
+// (conv_ws_dispatch ids 41..40+kNumWsPostTiles)
+constexpr int kNumWsPostTiles = 6;
 // Weight-stationary persistent 1x1 conv over dense sources (conv_ws1.hip): tile ids 201..200+kNumWs1Tiles
 int conv_ws1_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumWs1Tiles = 10;

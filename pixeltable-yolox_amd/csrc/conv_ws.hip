@@ -44,7 +44,8 @@ constexpr int ws_hxp(int tx, int s) {
 
 }  // namespace
 
-template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC, bool F1>
+template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC, bool F1, int PGN = 0,
+          int PGC = 0>
 __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, int tiles_x, int tiles_y,
                                                                  int ntiles, int ntn, int nwork) {
     static_assert(sizeof(T) == 2, "16-bit operands");
@@ -62,13 +63,27 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     // residual tile staging (stride-1 variants: the Bottleneck's shortcut): TM pixels x TN
     // channels by LDS-DMA with the halo, one 16-byte pad slot per pixel row, a ring of three
     // (the epilogue of tile k-1 runs during tile k while tile k+1 lands)
-    constexpr int RS = TN / 8 + 1, RSLOTS = S == 1 ? TM * RS : 0;
+    // Post conv (PGN > 0, yxh_conv_desc.post_weight): the tile's output Y stays in LDS in the
+    // residual slot layout (a ring of two slots, the residual DMA'd in and Y written over it
+    // in place) and Z = SiLU(W2 . [Y | X2] + b2) of PGN channels leaves instead, X2 = PGC
+    // channels of post_src DMA'd per tile (ring of two)
+    constexpr bool PG = PGN > 0;
+    constexpr int RS = TN / 8 + 1, RSLOTS = (S == 1 || PG) ? TM * RS : 0;
     constexpr int RLOADS = (RSLOTS + 63) / 64, GR = (RLOADS + NW - 1) / NW, RTB = RLOADS * 1024;
+    constexpr int NRING = PG ? 2 : 3;
+    constexpr int XS = PGC / 8 + 1, XSLOTS = PG && PGC > 0 ? TM * XS : 0;
+    constexpr int XLOADS = (XSLOTS + 63) / 64, GX = (XLOADS + NW - 1) / NW, XTB = XLOADS * 1024;
+    constexpr int K2 = TN + PGC, KB2 = K2 / 32;
+    constexpr int WN2 = PG ? (NW < PGN / 16 ? NW : PGN / 16) : 1, WM2 = NW / WN2;
+    constexpr int NF2 = PG ? PGN / 16 / WN2 : 1, PF2 = TM / 16 / WM2;
+    static_assert(!PG || (WK == 1 && !F1 && TN % 32 == 0 && PGC % 32 == 0 && PGN % (16 * WN2) == 0 &&
+                          NW % WN2 == 0 && (TM / 16) % WM2 == 0), "post-conv tile");
     // fused Bottleneck (F1): t = act(W1 . x + b1) of the halo tile, computed into one more
     // halo-shaped LDS image that the 3x3 then reads; wave w computes t channels
     // 32 (w % NG) .. +32 of every R-th 16-pixel halo fragment
     constexpr int NG = CIN / 32, R1 = NW / NG, NPA = (HY * HXP + 15) / 16;
-    constexpr int TOFF = 2 * HBYTES + RBYTES + 3 * RTB;
+    constexpr int XOFF = 2 * HBYTES + RBYTES + NRING * RTB;
+    constexpr int TOFF = XOFF + 2 * XTB;
     constexpr int SMEM = TOFF + (F1 ? HBYTES : 0);
     static_assert(!F1 || (S == 1 && NW % NG == 0), "fused Bottleneck tile");
     constexpr int FCO = (FC + WK - 1) / WK;  // pixel fragments this wave finishes
@@ -121,6 +136,23 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
                 a1[i][cb] = *(const uint4*)(w1 + (g * 32 + i * 16 + frow) * CIN + cb * 32 + fq * 8);
 #pragma unroll
             for (int r = 0; r < 4; ++r) b1[i][r] = p.pb1[g * 32 + i * 16 + fq * 4 + r];
+        }
+    }
+
+    // post conv weights, stationary: wave w owns Z channels (w % WN2) * NF2 * 16 .. + NF2 * 16 and
+    // pixel fragments (w / WN2) * PF2 .. + PF2 of the tile
+    const int wn2 = wave % WN2, wm2 = wave / WN2;
+    uint4 a2[PG ? NF2 : 1][PG ? KB2 : 1];
+    float b2[PG ? NF2 : 1][4];
+    if constexpr (PG) {
+        const T* w2 = (const T*)p.pgw;
+#pragma unroll
+        for (int f = 0; f < NF2; ++f) {
+            const int n = (wn2 * NF2 + f) * 16;
+#pragma unroll
+            for (int kb = 0; kb < KB2; ++kb) a2[f][kb] = *(const uint4*)(w2 + (long long)(n + frow) * K2 + kb * 32 + fq * 8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) b2[f][r] = p.pgb[n + fq * 4 + r];
         }
     }
 
@@ -210,6 +242,36 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         }
     };
 
+    // post conv second operand: per-lane slot geometry as the residual's, PGC channels
+    int xgeo[GX > 0 ? GX : 1];
+#pragma unroll
+    for (int i = 0; i < GX; ++i) {
+        const int L = wave + NW * i;
+        const int sl = 64 * L + lane;
+        const int pl = sl / XS, ch = sl - pl * XS;
+        const int ty = pl / TX, tx = pl - ty * TX;
+        const bool st = L < XLOADS && sl < XSLOTS && ch < PGC / 8;
+        xgeo[i] = st ? (ty | (tx << 10) | (ch << 20)) : -1;
+    }
+    auto issue_x2 = [&](const TileC& c, int slot) {
+        if constexpr (GX > 0) {
+            const dma::u32x4 xsrc =
+                dma::srd((const T*)p.pgs + (long long)c.b * p.pgs_bs, (uint32_t)((long long)ohw * p.pgs_cs * 2));
+#pragma unroll
+            for (int i = 0; i < GX; ++i) {
+                const int L = wave + NW * i;
+                if (XLOADS % NW == 0 || i + 1 < GX || L < XLOADS) {
+                    const int g = xgeo[i];
+                    const int oy = c.oy0 + (g & 1023), ox = c.ox0 + ((g >> 10) & 1023);
+                    const bool ok = g >= 0 && oy < OH && ox < OW;
+                    const uint32_t voff = ok ? (uint32_t)(((oy * OW + ox) * p.pgs_cs + (g >> 20) * 8) * 2) : dma::kOob;
+                    dma::load16(xsrc, voff, 0u,
+                                __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(XOFF + slot * XTB + L * 1024)));
+                }
+            }
+        }
+    };
+
     // epilogue of a finished tile: bias, SiLU, residual (from the LDS staging slot), 8-byte
     // stores of 4 channels through a buffer descriptor (an invalid pixel / channel carries an
     // out-of-range offset: no branch, so the scheduler can spread it over the next tile's
@@ -219,7 +281,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     auto epi_ctx = [&](const TileC c, const int k) -> EpiCtx {
         return EpiCtx{__builtin_amdgcn_make_buffer_rsrc((void*)((T*)p.dst + (long long)c.b * p.dst_bs), (short)0,
                                                         (int)dbytes, 0x00020000),
-                      smem + 2 * HBYTES + RBYTES + (k % 3) * RTB, c};
+                      smem + 2 * HBYTES + RBYTES + (k % NRING) * RTB, c};
     };
     // one (pixel fragment o, channel fragment i) piece of the epilogue
     auto epi_piece = [&](const EpiCtx& e, const f32x4 (&ap)[FR][FCO], const int o, const int i) {
@@ -244,7 +306,12 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
         u32x2 u;
         __builtin_memcpy(&u, t, 8);
-        if (!(YXH_WS_PROBE & 1) || p.act == 12345) __builtin_amdgcn_raw_buffer_store_b64(u, e.dsrd, od, 0, 0);
+        if constexpr (PG) {
+            (void)od;  // Y stays in LDS, over this lane's own residual values
+            *(u32x2*)(e.rl + (pl * RS + (nl >> 3)) * 16 + (nl & 7) * 2) = u;
+        } else if (!(YXH_WS_PROBE & 1) || p.act == 12345) {
+            __builtin_amdgcn_raw_buffer_store_b64(u, e.dsrd, od, 0, 0);
+        }
     };
     auto epilogue = [&](const TileC c, const int k, const f32x4 (&ap)[FR][FCO]) {
         const EpiCtx e = epi_ctx(c, k);
@@ -252,6 +319,46 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         for (int o = 0; o < FCO; ++o)
 #pragma unroll
             for (int i = 0; i < FR; ++i) epi_piece(e, ap, o, i);
+    };
+
+    // post conv of a finished tile whose Y is complete in ring slot k % 2 (and X2 landed):
+    // Z = SiLU(W2 . [Y | X2] + b2), 8-byte stores of 4 channels through a buffer descriptor
+    auto pg_tile = [&](const TileC c, const int k) {
+        if constexpr (PG) {
+            const char* ys = smem + 2 * HBYTES + RBYTES + (k & 1) * RTB;
+            const char* xs = smem + XOFF + (k & 1) * XTB;
+            const __amdgpu_buffer_rsrc_t zsrd = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)((T*)p.pgd + (long long)c.b * p.pgd_bs), (short)0, (int)((long long)ohw * p.pgd_cs * 2),
+                0x00020000);
+#pragma unroll
+            for (int pf = 0; pf < PF2; ++pf) {
+                const int pl = (wm2 * PF2 + pf) * 16 + frow;
+                f32x4 z[NF2];
+#pragma unroll
+                for (int f = 0; f < NF2; ++f) z[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kb = 0; kb < KB2; ++kb) {
+                    const uint4 bv = kb < TN / 32 ? *(const uint4*)(ys + (pl * RS + kb * 4 + fq) * 16)
+                                                  : *(const uint4*)(xs + (pl * XS + (kb - TN / 32) * 4 + fq) * 16);
+#pragma unroll
+                    for (int f = 0; f < NF2; ++f) Mma<T>::run(z[f], a2[f][kb], bv);
+                }
+                const int ty = pl / TX, tx = pl - ty * TX;
+                const int oy = c.oy0 + ty, ox = c.ox0 + tx;
+                const bool ok = oy < OH && ox < OW;
+#pragma unroll
+                for (int f = 0; f < NF2; ++f) {
+                    const int n = (wn2 * NF2 + f) * 16 + fq * 4;
+                    T t[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) t[q] = from_f32<T>(yxh::silu<false>(z[f][q] + b2[f][q]));
+                    u32x2 u;
+                    __builtin_memcpy(&u, t, 8);
+                    const int od = ok ? ((oy * OW + ox) * p.pgd_cs + n) * 2 : (int)dma::kOob;
+                    __builtin_amdgcn_raw_buffer_store_b64(u, zsrd, od, 0, 0);
+                }
+            }
+        }
     };
 
     f32x4 accp[FR][FCO];  // owned fragments of the previous tile, waiting for their epilogue
@@ -271,8 +378,12 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             cnext = coords(next);
             if (!(YXH_WS_PROBE & 2)) {
                 issue_halo(cnext, kb ^ 1);
-                if (has_res) issue_res(cnext, (k + 1) % 3);
+                if (!PG && has_res) issue_res(cnext, (k + 1) % 3);
             }
+        }
+        if constexpr (PG) {  // this tile's residual / X2: read one step later (ring of two)
+            if (has_res) issue_res(cur, k & 1);
+            issue_x2(cur, k & 1);
         }
 
         if constexpr (F1) {
@@ -386,12 +497,16 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 #pragma unroll
                 for (int j = 0; j < FC; ++j) accp[i][j] = acc[i][j];
         }
+        if constexpr (PG && EPI) {  // the previous tile's Y is complete in LDS: its post conv
+            dma::barrier();
+            pg_tile(prev, k - 1);
+        }
         return next;
     };
 
     TileC cur = coords(tile), cnext{0, 0, 0};
     issue_halo(cur, 0);
-    if (has_res) issue_res(cur, 0);
+    if (!PG && has_res) issue_res(cur, 0);
     // the first tile is peeled off the loop: it consumes the weight loads, so the loop body
     // carries no compiler-visible pending load whose wait would also drain the halo DMA
     int next = tile_step(cur, tile, 0, cnext, cur, std::false_type{});
@@ -401,14 +516,29 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         cur = cnext;
         next = tile_step(cur, next, k, cnext, prev, std::true_type{});
     }
+    if constexpr (PG) {  // the last tile's residual / X2 were issued in its own step
+        dma::wait_vm<0>();
+        dma::barrier();
+    }
     epilogue(cur, k - 1, accp);
+    if constexpr (PG) {
+        dma::barrier();
+        pg_tile(cur, k - 1);
+    }
     (void)ohw;
 }
 
-template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC = 1, bool F1 = false>
+template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC = 1, bool F1 = false,
+          int PGN = 0, int PGC = 0>
 static int launch_ws(const ConvParams& p, hipStream_t st) {
     if (p.stride != S || p.cin != CIN) {
         set_error("conv_ws variant built for stride %d, %d input channels", S, CIN);
+        return YXH_EUNSUPPORTED;
+    }
+    if ((p.pgw != nullptr) != (PGN > 0) || (PGN > 0 && (p.pg_cout != PGN || p.pgs_ch != PGC || p.cout != TN))) {
+        set_error(PGN > 0 ? "conv_ws post tile built for %d -> %d channels + a %d-channel post_src, post conv %d"
+                          : "conv_ws plain tile with a post conv (%d -> %d, %d, %d)",
+                  CIN, TN, PGC, PGN);
         return YXH_EUNSUPPORTED;
     }
     if (p.grp2 && (F1 || (p.cout / 2) % TN)) {
@@ -421,7 +551,7 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
                   CIN);
         return YXH_EUNSUPPORTED;
     }
-    if (p.dst_f32 || p.accum || (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) || !p.vec_store ||
+    if (p.dst_f32 || p.accum || (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) || (!p.vec_store && PGN == 0) ||
         p.cout % 8 || (p.res && (S != 1 || ((uintptr_t)p.res % 16) || p.res_cs % 8 || p.res_bs % 8))) {
         set_error("conv_ws: 16-bit dst, SiLU/no activation, 8-byte aligned dst rows, 16-byte residual rows "
                   "(stride-1 variants) only");
@@ -435,7 +565,7 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
         return YXH_EINVAL;
     }
     const int nwork = (int)std::min<long long>(ntiles, std::max(1, p.cus * BPC / ntn));
-    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM, BPC, F1>), dim3((unsigned)(nwork * ntn)),
+    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM, BPC, F1, PGN, PGC>), dim3((unsigned)(nwork * ntn)),
                        dim3(64 * WN * WK * WM), 0, st, p, tiles_x, tiles_y, (int)ntiles, ntn, nwork);
     YXH_CHECK_LAUNCH("conv_ws launch");
     return YXH_OK;
@@ -456,8 +586,8 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 7: return launch_ws<T, 64, 2, 16, 4, 128, 4, 1, 2>(p, st);
         case 8: return launch_ws<T, 64, 2, 16, 2, 128, 4, 1, 1, 2>(p, st);
         // 128 input channels: 40x40 / 80x80 / 20x20 3x3s (dark4, PAFPN, head), s2 128 -> 128/256
-        case 9: return launch_ws<T, 128, 1, 16, 4, 128, 4, 2, 1>(p, st);
-        case 10: return launch_ws<T, 32, 1, 32, 8, 32, 1, 1, 4, 2>(p, st);
+        // ids 9 / 10 (128 -> 128 16x4 K-split two ways: 96 B/lane of scratch; 32 -> 32 32x8 two
+        // blocks per CU: missed its occupancy target) are withdrawn
         case 11: return launch_ws<T, 128, 1, 8, 4, 128, 4, 2, 1>(p, st);
         case 12: return launch_ws<T, 128, 1, 8, 8, 64, 2, 2, 1>(p, st);
         case 13: return launch_ws<T, 128, 2, 16, 2, 128, 4, 2, 1>(p, st);
@@ -491,6 +621,15 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 34: return launch_ws<T, 64, 1, 16, 8, 64, 2, 1, 2, 1, true>(p, st);
         case 35: return launch_ws<T, 128, 1, 16, 4, 128, 4, 1, 1, 1, true>(p, st);
         case 36: return launch_ws<T, 128, 1, 8, 4, 128, 4, 1, 1, 1, true>(p, st);
+        // 1x1 post conv (ids 41-48 = tiles 221-228): dark2's Bottleneck 3x3 32 -> 32 + CspLayer.conv3
+        // over [y | x_2] (64 -> 64); the 64 -> 64 3x3s of dark3's last Bottleneck / C3_p3 + conv3 over
+        // [y | x_2] (128 -> 128); dark3[0] (3x3 s2 64 -> 128) + CspLayer conv1 | conv2 (128 -> 128)
+        case 41: return launch_ws<T, 32, 1, 16, 8, 32, 1, 1, 4, 2, false, 64, 32>(p, st);
+        case 42: return launch_ws<T, 32, 1, 16, 8, 32, 1, 1, 4, 1, false, 64, 32>(p, st);
+        case 43: return launch_ws<T, 64, 1, 16, 4, 64, 2, 1, 2, 1, false, 128, 64>(p, st);
+        case 44: return launch_ws<T, 64, 1, 16, 8, 64, 2, 1, 2, 1, false, 128, 64>(p, st);
+        case 45: return launch_ws<T, 64, 2, 16, 2, 128, 4, 1, 1, 1, false, 128, 0>(p, st);
+        case 46: return launch_ws<T, 64, 2, 16, 4, 128, 4, 1, 1, 1, false, 128, 0>(p, st);
         default: set_error("conv_ws tile id %d", id); return YXH_EINVAL;
     }
 }

@@ -48,7 +48,9 @@ class ConvDesc(C.Structure):
                 ("dst_cstride", C.c_int32), ("act", C.c_int32), ("dst_bstride", C.c_int64),
                 ("decode_stride", C.c_float), ("decode_coff", C.c_int32), ("tile", C.c_int32),
                 ("flags", C.c_int32), ("grid_cap", C.c_int32), ("pre_weight", C.c_void_p), ("pre_bias", C.c_void_p),
-                ("weight_frag", C.c_void_p)]
+                ("weight_frag", C.c_void_p), ("post_weight", C.c_void_p), ("post_bias", C.c_void_p),
+                ("post_src", Src), ("post_dst", C.c_void_p), ("post_cout", C.c_int32),
+                ("post_dst_cstride", C.c_int32), ("post_dst_bstride", C.c_int64)]
 
 
 CONV_ACCUMULATE = 1

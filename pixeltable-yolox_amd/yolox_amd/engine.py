@@ -286,6 +286,45 @@ class PlanCtx:
         self.flops += 2.0 * self.batch * oh * ow * cout * kh * kw * (conv.in_channels // groups)
         return out
 
+    # (main conv cin, stride, post_src channels, post cout) shapes the conv_ws post tiles are built for
+    POST_SHAPES = {(32, 1, 32, 64), (64, 1, 64, 128), (64, 2, 0, 128)}
+
+    def post_fusable(self, m, post_ms, post_src_ch: int) -> bool:
+        """BaseConv ``m`` (3x3) followed by the 1x1 BaseConvs ``post_ms`` (stacked along cout)
+        over [m's output | a post_src of ``post_src_ch`` channels] as one conv_ws post launch."""
+        if not (self.csp_fusion and not self.fuse_bottleneck and hasattr(m, "conv")
+                and all(hasattr(q, "conv") for q in post_ms)):
+            return False
+        k = m.conv
+        pk = [q.conv for q in post_ms]
+        cout_post = sum(q.out_channels for q in pk)
+        acts = {getattr(q, "act_name", "silu") for q in [m] + list(post_ms)}
+        return (acts == {"silu"} and k.kernel_size == (3, 3) and k.padding == (1, 1) and k.groups == 1
+                and (k.out_channels == k.in_channels if k.stride == (1, 1) else k.out_channels == 2 * k.in_channels)
+                and (k.in_channels, k.stride[0], post_src_ch, cout_post) in self.POST_SHAPES
+                and all(q.kernel_size == (1, 1) and q.groups == 1 and q.stride == (1, 1)
+                        and q.in_channels == k.out_channels + post_src_ch for q in pk))
+
+    def conv_post(self, m, srcs: list, post_ms, post_src: Optional[View], post_out: View,
+                  residual: Optional[View] = None) -> View:
+        """conv ``m`` + the 1x1 post conv (``post_ms`` stacked) over [m's output | post_src] as
+        ONE launch (yxh_conv_desc.post_*): m's output never leaves the block's LDS."""
+        k = m.conv
+        lh, lw = srcs[0].lh, srcs[0].lw
+        s = k.stride[0]
+        oh, ow = (lh + 2 - 3) // s + 1, (lw + 2 - 3) // s + 1
+        cout_post = sum(q.conv.out_channels for q in post_ms)
+        if post_out.ch != cout_post or post_out.lh != oh or post_out.lw != ow:
+            raise ValueError("post conv output view does not match")
+        spec = self._weights([(k, m.bn)], k.in_channels)
+        pspec = self._weights([(q.conv, q.bn) for q in post_ms], k.out_channels + (post_src.ch if post_src else 0))
+        self.ops.append(OpRec(N.OP_CONV, dict(
+            srcs=list(srcs), out=None, residual=residual, spec=spec, cin=k.in_channels, cout=k.out_channels, k=3,
+            stride=s, pad=1, groups=1, in_h=lh, in_w=lw, out_h=oh, out_w=ow, act=N.ACT_CODE["silu"], dst_f32=False,
+            post_spec=pspec, post_src=post_src, post_out=post_out)))
+        self.flops += 2.0 * self.batch * oh * ow * (k.out_channels * 9 * k.in_channels + cout_post * pspec.cin_pad)
+        return post_out
+
     def bottleneck_fusable(self, b) -> bool:
         c1, c2 = b.conv1, b.conv2
         if not (self.fuse_bottleneck and hasattr(c1, "conv") and hasattr(c2, "conv")):
@@ -381,7 +420,7 @@ class OutBuffer:
 # conv_pwr kernel, 97-104 the dense 1x1 conv_pwf kernel, 113-150 the 3x3 conv_r3 kernel
 # (yoloxhip.h yxh_conv_desc.tile)
 TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
-                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 197)] + [2 * i for i in range(201, 211)]
+                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 197)] + [2 * i for i in range(201, 211)] + [2 * i for i in range(221, 227)]
 # 16-bit plans: the families that win on MI355X (profiles/r03/final/tune_r3fa_*.json: yolox_s picks only
 # conv_pwf / conv_ws / conv_ws1; yolox_l fp16 also conv_igemm and conv_r3 once or twice); the LDS-DMA
 # conv_glds, row-tiled conv_rows and the round-1 pointwise kernels never do and are tried only with
@@ -414,7 +453,7 @@ def _tune_key(d) -> tuple:
     return (d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w, d.cin, d.cout, d.kh, d.stride, d.nsrc,
             d.src[0].channels, d.src[0].upsample, d.src[1].upsample if d.nsrc > 1 else 0,
             bool(d.residual), d.dst_dtype, d.dst_cstride == d.cout, d.act >= N.ACT_DECODE, bool(d.pre_weight),
-            d.flags)
+            d.flags, d.post_cout, d.post_src.channels)
 
 
 def op_buffers(r: OpRec) -> tuple:
@@ -432,7 +471,12 @@ def op_buffers(r: OpRec) -> tuple:
     reads = [v.buf for v in a["srcs"]]
     if a.get("residual") is not None:
         reads.append(a["residual"].buf)
-    return reads, ([a["out"].buf] if a.get("out") is not None else [])
+    if a.get("post_src") is not None:
+        reads.append(a["post_src"].buf)
+    writes = [a["out"].buf] if a.get("out") is not None else []
+    if a.get("post_out") is not None:
+        writes.append(a["post_out"].buf)
+    return reads, writes
 
 
 def dependencies_rw(rw: list) -> list:
@@ -701,7 +745,24 @@ class Plan:
                     d.residual = self._ptr(res, c)
                     d.res_cstride, d.res_bstride = res.buf.c, res.buf.nelem_image
                 d.act = a["act"]
-                if a["dst_f32"]:
+                pspec = a.get("post_spec")
+                if pspec is not None:  # 1x1 post conv: its output replaces the conv's own
+                    d.post_weight = self.warena.data_ptr() + pspec.w_off
+                    d.post_bias = self.barena.data_ptr() + pspec.b_off
+                    d.post_cout = pspec.cout
+                    ps = a["post_src"]
+                    if ps is not None:
+                        q = d.post_src
+                        q.ptr = self._ptr(ps, c)
+                        q.channels, q.cstride, q.bstride = ps.ch, ps.buf.c, ps.buf.nelem_image
+                        q.h, q.w, q.upsample = ps.buf.h, ps.buf.w, 0
+                    po = a["post_out"]
+                    d.post_dst = self._ptr(po, c)
+                    d.post_dst_cstride, d.post_dst_bstride = po.buf.c, po.buf.nelem_image
+                    d.dst = d.post_dst
+                    d.dst_dtype = ctx.dcode
+                    d.dst_cstride, d.dst_bstride = po.buf.c, po.buf.nelem_image
+                elif a["dst_f32"]:
                     out, a_off, coff = a["head_out"]
                     row = out.row
                     d.dst = out_base + (a_off * row + coff) * 4

@@ -143,11 +143,13 @@ class CspLayer(_Planned):
         if fused_head is not None:
             cat, t0 = fused_head
             x1 = cat.slice(0, hidden)
-            b0 = self.m[0]
-            b0.conv2.plan(ctx, [t0], out=x1, residual=x1 if b0.use_add else None)
-            for b in list(self.m)[1:]:
-                b.plan(ctx, x1, out=x1)
-            return self.conv3.plan(ctx, [cat.full()], out=out)
+            rest = list(self.m)
+            if t0 is not None:  # the first Bottleneck's conv1 already ran
+                b0 = rest.pop(0)
+                if not rest and self._post_fusable(ctx, b0):
+                    return self._plan_post(ctx, b0, t0, x1, cat, out)
+                b0.conv2.plan(ctx, [t0], out=x1, residual=x1 if b0.use_add else None)
+            return self._plan_tail(ctx, rest, x1, cat, out)
         cat = ctx.buffer(srcs[0].lh, srcs[0].lw, 2 * hidden)
         x1 = cat.slice(0, hidden)
         # conv1 | conv2 read the same input: one conv writes the whole [x_1 | x_2]
@@ -164,7 +166,25 @@ class CspLayer(_Planned):
             if cur is not x1:
                 return self.conv3.plan(ctx, [cur, cat.slice(hidden, hidden)], out=out)
             return self.conv3.plan(ctx, [cat.full()], out=out)
-        for b in self.m:
+        return self._plan_tail(ctx, list(self.m), x1, cat, out)
+
+    def _post_fusable(self, ctx, b) -> bool:
+        hidden = self.conv1.conv.out_channels
+        return hasattr(ctx, "post_fusable") and ctx.post_fusable(b.conv2, [self.conv3], hidden)
+
+    def _plan_post(self, ctx, b, t, x1, cat, out):
+        """The last Bottleneck's 3x3 (+ shortcut) and conv3 over [its output | x_2] as one launch."""
+        hidden = self.conv1.conv.out_channels
+        if out is None:
+            out = ctx.buffer(x1.lh, x1.lw, self.conv3.conv.out_channels).full()
+        return ctx.conv_post(b.conv2, [t], [self.conv3], cat.slice(hidden, hidden), out,
+                             residual=x1 if b.use_add else None)
+
+    def _plan_tail(self, ctx, bottlenecks, x1, cat, out):
+        for i, b in enumerate(bottlenecks):
+            if i == len(bottlenecks) - 1 and self._post_fusable(ctx, b):
+                t = b.conv1.plan(ctx, [x1])
+                return self._plan_post(ctx, b, t, x1, cat, out)
             b.plan(ctx, x1, out=x1)
         return self.conv3.plan(ctx, [cat.full()], out=out)
 
@@ -215,9 +235,21 @@ class CspDarknet(_Planned):
             x = ctx.stem_s2(self.stem.conv, self.dark2[0], packed) if fused else self.stem.plan(ctx, packed)
         feats = []
         for stage in (self.dark2, self.dark3, self.dark4, self.dark5):
+            blocks = list(stage)[1:]
             if not (fused and stage is self.dark2):
-                x = stage[0].plan(ctx, [x])
-            for blk in list(stage)[1:]:
+                csp = blocks[0] if blocks and isinstance(blocks[0], CspLayer) else None
+                if (csp is not None and hasattr(ctx, "post_fusable")
+                        and ctx.post_fusable(stage[0], [csp.conv1, csp.conv2], 0)):
+                    # the stride-2 conv + the CspLayer's conv1 | conv2 as one launch (conv_ws post tile)
+                    h = csp.conv1.conv.out_channels
+                    oh, ow = (x.lh - 1) // 2 + 1, (x.lw - 1) // 2 + 1
+                    cat = ctx.buffer(oh, ow, 2 * h)
+                    ctx.conv_post(stage[0], [x], [csp.conv1, csp.conv2], None, cat.full())
+                    x = csp.plan(ctx, None, fused_head=(cat, None))
+                    blocks = blocks[1:]
+                else:
+                    x = stage[0].plan(ctx, [x])
+            for blk in blocks:
                 if head2 is not None and blk is csp2:
                     x = blk.plan(ctx, None, fused_head=head2)
                 else:

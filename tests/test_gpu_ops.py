@@ -75,8 +75,10 @@ def ref_conv(x, conv, bn, act):
 
 
 def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_coff=0, out_c=None, tile=0, flags=0,
-             pre=None, groups2=False, frag=False):
-    """srcs: list of (nhwc tensor [B,h,w,C], coff, ch, upsample)."""
+             pre=None, groups2=False, frag=False, post=None):
+    """srcs: list of (nhwc tensor [B,h,w,C], coff, ch, upsample).  post: (packed weight, bias,
+    (post_src tensor, coff, ch) or None, post_dst tensor, coff, post_cout): a 1x1 post conv
+    whose output goes to post_dst instead of the conv's own output."""
     n = N()
     B = srcs[0][0].shape[0]
     ups = srcs[0][3]
@@ -118,6 +120,17 @@ def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_cof
     if groups2:  # output half g reads source channels [g*cin, (g+1)*cin)
         d.cin = cin // 2
         d.flags = flags | n.CONV_GROUPS2
+    if post is not None:
+        pw, pb, psrc, pdst, pcoff, pcout = post
+        d.post_weight, d.post_bias, d.post_cout = pw.data_ptr(), pb.data_ptr(), pcout
+        if psrc is not None:
+            t, coff, ch = psrc
+            ps = d.post_src
+            ps.ptr = t.data_ptr() + coff * t.element_size()
+            ps.channels, ps.cstride, ps.bstride = ch, t.shape[3], t.shape[1] * t.shape[2] * t.shape[3]
+            ps.h, ps.w = t.shape[1], t.shape[2]
+        d.post_dst = pdst.data_ptr() + pcoff * pdst.element_size()
+        d.post_dst_cstride, d.post_dst_bstride = pdst.shape[3], pdst.shape[1] * pdst.shape[2] * pdst.shape[3]
     n.check(n.lib().yxh_conv2d(ctypes.byref(d), n.stream_ptr()), "conv2d")
     torch.cuda.synchronize()
     return out
@@ -689,6 +702,7 @@ def test_conv_r3_residual_and_strided_dst(dtype):
         close(y[..., 64:].permute(0, 3, 1, 2), want, dtype)
 
 
+WS_WITHDRAWN = {169, 170}  # spilled to scratch / missed the occupancy target (round 4): EINVAL now
 WS_GEOMS = [  # cin, cout, s, H, W (input), batch
     (32, 32, 1, 37, 45, 3), (32, 64, 2, 66, 70, 2), (64, 64, 1, 80, 80, 8), (64, 128, 2, 42, 38, 2),
     (128, 128, 1, 40, 40, 16), (128, 256, 1, 20, 22, 2), (128, 96, 2, 41, 40, 2), (256, 256, 1, 20, 20, 4),
@@ -709,6 +723,8 @@ def test_conv_ws_3x3(dtype, geom):
     wide[..., 16:16 + cin] = nhwc(x, dtype)
     ran = 0
     for tid in range(161, 191):
+        if tid in WS_WITHDRAWN:
+            continue
         try:
             y = run_conv([(wide, 16, cin, 0)], conv, bn, dtype, tile=2 * tid)
         except NotImplementedError as e:
@@ -720,6 +736,60 @@ def test_conv_ws_3x3(dtype, geom):
             assert torch.equal(yf, y), tid
         ran += 1
     assert ran >= 1
+
+
+POST_GEOMS = [  # cin(=cout), stride, post_src channels, post_cout, H, W (input), batch
+    (32, 1, 32, 64, 37, 45, 3), (32, 1, 32, 64, 160, 160, 2), (64, 1, 64, 128, 40, 24, 3),
+    (64, 1, 64, 128, 80, 80, 4), (64, 2, 0, 128, 42, 38, 2), (64, 2, 0, 128, 160, 160, 2)]
+
+
+@pytest.mark.parametrize("residual", [True, False])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("geom", POST_GEOMS)
+def test_conv_ws_post_conv(dtype, geom, residual):
+    """conv_ws post tiles (ids 221-226, round 4): a Bottleneck's 3x3 (+ shortcut) followed by
+    CspLayer.conv3 over [y | x_2] (network_blocks.py:95-99, 180-183), or a stage's stride-2 3x3
+    followed by its CspLayer conv1 | conv2 (darknet.py:148-156, network_blocks.py:176-178), in
+    one launch -- y never leaves LDS.  vs torch fp32 with y rounded to the compute dtype as the
+    split launches store it; partial tiles, channel-slice sources / destinations, the
+    destination's other channels untouched, every post tile built for the shape."""
+    cin, s, c2, pout, H, W, B = geom
+    if residual and s == 2:
+        pytest.skip("stride-2 convs have no shortcut")
+    conv, bn = make_conv(cin, cin if s == 1 else 2 * cin, 3, s, seed=cin + H)
+    cout = conv.out_channels
+    pconv, pbn = make_conv(cout + c2, pout, 1, 1, seed=cin + W)
+    g = torch.Generator().manual_seed(H * W + cin)
+    x = torch.randn(B, cin, H, W, generator=g)
+    oh, ow = (H - 1) // s + 1, (W - 1) // s + 1
+    r = torch.randn(B, cout, oh, ow, generator=g)
+    x2 = torch.randn(B, c2, oh, ow, generator=g) if c2 else None
+    y = ref_conv(x, conv, bn, "silu") + (r.to(dtype).float() if residual else 0)
+    yq = y.to(dtype).float()
+    zin = torch.cat([yq, x2.to(dtype).float()], 1) if c2 else yq
+    want = ref_conv(zin, pconv, pbn, "silu")
+    X = nhwc(x, dtype)
+    R = nhwc(r, dtype, cout + 8)  # residual in a wider buffer
+    X2 = torch.zeros(B, oh, ow, c2 + 32, dtype=dtype, device=DEV)
+    if c2:
+        X2[..., 32:] = nhwc(x2, dtype)
+    pw, pb = pack(pconv, pbn, dtype)
+    ran = 0
+    for tid in range(221, 227):
+        Z = torch.full((B, oh, ow, pout + 16), 3.0, dtype=dtype, device=DEV)
+        try:
+            run_conv([(X, 0, cin, 0)], conv, bn, dtype, residual=(R, 0) if residual else None, tile=2 * tid,
+                     post=(pw, pb, (X2, 32, c2) if c2 else None, Z, 8, pout))
+        except NotImplementedError:
+            continue
+        close(Z[..., 8:8 + pout].permute(0, 3, 1, 2), want, dtype)
+        assert (Z[..., :8] == 3.0).all() and (Z[..., 8 + pout:] == 3.0).all()
+        ran += 1
+    assert ran >= 1
+    with pytest.raises(NotImplementedError):  # plain tiles refuse a post conv
+        run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * 166,
+                 post=(pw, pb, (X2, 32, c2) if c2 else None, torch.zeros(B, oh, ow, pout, dtype=dtype, device=DEV),
+                       0, pout))
 
 
 def test_pack_frag_layout():
@@ -855,6 +925,8 @@ def test_conv_ws_two_groups(cin, H, W, B):
     X = nhwc(x, dtype)
     ran = 0
     for tid in range(161, 191):
+        if tid in WS_WITHDRAWN:
+            continue
         try:
             y = run_conv([(X, 0, 2 * cin, 0)], conv, bn, dtype, tile=2 * tid, groups2=True)
         except NotImplementedError as e:
