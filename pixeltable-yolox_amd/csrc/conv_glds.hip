@@ -174,10 +174,18 @@ __global__ __launch_bounds__(256) void conv_glds(ConvParams p) {
 template <typename T, int TN, int TM, int WR, int WC>
 static int launch(const ConvParams& p, int ks, hipStream_t st) {
     dim3 grid((p.M + TM - 1) / TM, (p.cout + TN - 1) / TN);
-    if (ks == 2)
-        hipLaunchKernelGGL((conv_glds<T, TN, TM, WR, WC, 2>), grid, dim3(256), 0, st, p);
-    else
+    // two-slab staging of the wide tiles spilled to scratch (tools/kernel_resources.py): not built
+    constexpr bool K2 = !(TM == 256 || TN == 80 || (TN == 128 && TM == 128));
+    if (ks == 2) {
+        if constexpr (K2) {
+            hipLaunchKernelGGL((conv_glds<T, TN, TM, WR, WC, 2>), grid, dim3(256), 0, st, p);
+        } else {
+            set_error("conv_glds %dx%d: two-slab staging is not built (it spilled)", TN, TM);
+            return YXH_EUNSUPPORTED;
+        }
+    } else {
         hipLaunchKernelGGL((conv_glds<T, TN, TM, WR, WC, 1>), grid, dim3(256), 0, st, p);
+    }
     YXH_CHECK_LAUNCH("conv_glds launch");
     return YXH_OK;
 }

@@ -499,9 +499,7 @@ static int r3_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 11: return launch_r3<T, 2, 8, 8, 4, 64, 2>(p, st);
         case 12: return launch_r3<T, 2, 16, 8, 4, 64, 2>(p, st);
         // 8-wave blocks, two-slot ring, two blocks per CU
-        case 13: return launch_r3<T, 1, 16, 16, 4, 64, 2, 8>(p, st);
         case 14: return launch_r3<T, 1, 32, 8, 4, 64, 2, 8>(p, st);
-        case 15: return launch_r3<T, 1, 16, 8, 4, 128, 2, 8>(p, st);
         case 16: return launch_r3<T, 1, 8, 8, 4, 128, 2, 8>(p, st);
         case 17: return launch_r3<T, 2, 8, 8, 4, 128, 2, 8>(p, st);
         case 18: return launch_r3<T, 2, 16, 8, 4, 64, 2, 8>(p, st);
@@ -510,17 +508,14 @@ static int r3_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         // 8 waves, three-slot ring (two stages in flight)
         case 21: return launch_r3<T, 1, 16, 8, 4, 64, 3, 8>(p, st);
         case 22: return launch_r3<T, 1, 32, 4, 4, 64, 3, 8>(p, st);
-        // 8 waves held to 80 registers: three blocks (6 waves per SIMD)
-        case 23: return launch_r3<T, 1, 16, 8, 4, 64, 2, 8, 6>(p, st);
-        case 24: return launch_r3<T, 1, 32, 4, 4, 64, 2, 8, 6>(p, st);
-        case 25: return launch_r3<T, 1, 8, 16, 4, 64, 2, 8, 6>(p, st);
+        // ids 13, 15, 23-25 and the 16-bit 29 spilled to scratch at their occupancy targets
+        // (tools/kernel_resources.py): withdrawn (EINVAL)
         // one block per CU, wide tiles (small late layers)
         case 26: return launch_r3<T, 1, 20, 16, 4, 64>(p, st);
         case 27: return launch_r3<T, 2, 20, 8, 4, 128>(p, st);
         // 32 output channels per block (cout = 32 layers)
         case 28: return launch_r3<T, 1, 32, 8, 4, 32, 2, 8>(p, st);
         // conv_r3h: halo tile staged once per channel block -> (stride, TX, TY, TN, waves)
-        case 29: return launch_r3h<T, 1, 16, 16, 64, 8>(p, st);
         case 30: return launch_r3h<T, 1, 32, 8, 64, 8>(p, st);
         case 31: return launch_r3h<T, 1, 16, 8, 64, 4>(p, st);
         case 32: return launch_r3h<T, 1, 32, 8, 32, 8>(p, st);
@@ -539,7 +534,9 @@ static int r3_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
 // so the kernel is MFMA-bound where its 16-bit form is DMA-bound.
 static int r3h_dispatch_f32(int id, const ConvParams& p, hipStream_t st) {
     switch (id) {
-        case 29: return launch_r3h<float, 1, 16, 16, 64, 8>(p, st);
+        // 16 x 16 TN 64 8 waves: held to 128 VGPRs (two blocks per CU) it spilled 16 B/lane; one
+        // block per CU, 256 VGPRs
+        case 29: return launch_r3h<float, 1, 16, 16, 64, 8, 2>(p, st);
         case 30: return launch_r3h<float, 1, 32, 8, 64, 8>(p, st);
         case 31: return launch_r3h<float, 1, 16, 8, 64, 4>(p, st);
         case 32: return launch_r3h<float, 1, 32, 8, 32, 8>(p, st);

@@ -636,6 +636,7 @@ def test_pointwise_pwf_upsampled_first_source(dtype):
     assert ran >= 4
 
 
+R3_WITHDRAWN = {125, 127, 135, 136, 137}  # spilled to scratch (round 4): EINVAL; 141 is fp32-only now
 R3_GEOMS = [  # cin, cout, s, H, W (input)
     (64, 96, 1, 11, 13), (32, 64, 1, 83, 41), (128, 64, 1, 20, 20), (64, 128, 2, 40, 40), (32, 48, 2, 17, 35),
     (256, 256, 1, 10, 10), (128, 256, 2, 21, 19)]
@@ -654,6 +655,8 @@ def test_conv_r3_3x3(dtype, geom):
     X = nhwc(x, dtype)
     ran = 0
     for tid in range(113, 151):
+        if tid in R3_WITHDRAWN or (tid == 141 and dtype != torch.float32):
+            continue
         try:
             y = run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * tid)
         except NotImplementedError as e:
@@ -695,7 +698,7 @@ def test_conv_r3_residual_and_strided_dst(dtype):
     r = torch.randn(2, 64, 20, 20, generator=torch.Generator().manual_seed(5))
     want = ref_conv(x, conv, bn, "silu") + r.to(dtype).float()
     buf = torch.zeros(2, 20, 20, 128, dtype=dtype, device=DEV)
-    for tid in (113, 117, 125, 126, 127, 133, 135, 138, 140, 141, 142, 144, 150):
+    for tid in (113, 117, 126, 133, 138, 140, 142, 144, 150):
         buf[..., 64:] = nhwc(r, dtype)
         y = run_conv([(nhwc(x, dtype), 0, 64, 0)], conv, bn, dtype, residual=(buf, 64), out=buf, out_coff=64,
                      tile=2 * tid)

@@ -73,3 +73,22 @@ def test_library_targets_gfx950_only():
     assert b"gfx950" in blob
     for other in (b"gfx90a", b"gfx942", b"sm_"):
         assert b"amdgcn-amd-amdhsa--" + other not in blob
+
+
+def test_no_shipped_kernel_uses_scratch():
+    """Every gfx950 kernel in libyoloxhip.so keeps its state in registers / LDS: no kernel's
+    code-object metadata reports a private segment (scratch spills cost vmcnt waits that drain
+    the LDS-DMA pipelines).  tools/kernel_resources.py reads the metadata of every offload
+    bundle in the library's .hip_fatbin section."""
+    import importlib.util
+    import shutil
+    if not shutil.which("/opt/rocm/lib/llvm/bin/llvm-readelf"):
+        pytest.skip("ROCm LLVM tools not installed")
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "kernel_resources.py")
+    spec = importlib.util.spec_from_file_location("kernel_resources", path)
+    kr = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(kr)
+    ks = kr.kernels()
+    assert len(ks) > 300  # every translation unit's bundle was read
+    spills = sorted((v["scratch"], k) for k, v in ks.items() if v.get("scratch", 0) > 0)
+    assert not spills, spills[:10]
