@@ -139,17 +139,34 @@ class YoloxConfig:
                            min_lr_ratio=self.min_lr_ratio)
 
     def get_data_loader(self, batch_size: int, is_distributed: bool, no_aug: bool = False, cache_img=None,
-                        dataset_size: int = 118287):
-        """config.py:214-273 with the synthetic dataset: the per-rank batch is
-        batch_size // world (:249-250) and every rank reads its rank-strided slice of one
-        seeded shuffled index stream (InfiniteSampler, samplers.py:28-82)."""
-        from .trainer import InfiniteSampler, SyntheticBatches, SyntheticCocoDataset
+                        dataset_size: int = 118287, device=None, distinct_images: int = 512, dataset=None):
+        """config.py:203-273 on the device pipeline: MosaicDetection (mosaic / random affine /
+        mixup) + TrainTransform (HSV / mirror / padded labels) over a ``pull_item`` detection
+        dataset whose images live in HBM (yolox_amd.data.GpuMosaicDetection: the host draws the
+        reference's random numbers in its order and does the label arithmetic, one
+        yxh_augment_batch launch renders the batch).  ``dataset`` defaults to the synthetic
+        COCO-shaped one (no datasets offline: ``dataset_size`` items over ``distinct_images``
+        resident images).  The per-rank batch is batch_size // world (:249-250) and every rank
+        reads its rank-strided slice of one seeded shuffled index stream (InfiniteSampler,
+        samplers.py:28-82); ``no_aug`` starts with mosaic off (YoloBatchSampler(mosaic=not
+        no_aug), :255-260), ``close_mosaic()`` turns it off later (trainer.py:217-230)."""
+        from .data.mosaic import GpuMosaicDetection, MosaicBatches, SyntheticDetectionDataset, TrainTransform
         from .launch import get_world_size
+        from .trainer import InfiniteSampler
         if is_distributed:
             batch_size = batch_size // get_world_size()
-        ds = SyntheticCocoDataset(dataset_size, self.input_size, seed=self.seed if self.seed else 0)
-        sampler = InfiniteSampler(len(ds), seed=self.seed if self.seed else 0)
-        return SyntheticBatches(ds, sampler, batch_size)
+        seed = self.seed if self.seed else 0
+        if dataset is None:
+            dataset = SyntheticDetectionDataset(dataset_size, self.input_size, seed=seed,
+                                                num_classes=self.num_classes, distinct=distinct_images)
+        ds = GpuMosaicDetection(
+            dataset, self.input_size, mosaic=not no_aug,
+            preproc=TrainTransform(max_labels=120, flip_prob=self.flip_prob, hsv_prob=self.hsv_prob),
+            degrees=self.degrees, translate=self.translate, mosaic_scale=self.mosaic_scale,
+            mixup_scale=self.mixup_scale, shear=self.shear, enable_mixup=self.enable_mixup,
+            mosaic_prob=self.mosaic_prob, mixup_prob=self.mixup_prob, device=device or "cuda")
+        sampler = InfiniteSampler(len(ds), seed=seed)
+        return MosaicBatches(ds, sampler, batch_size)
 
     def random_resize(self, data_loader, epoch: int, rank: int, is_distributed: bool):
         """config.py:275-294: rank 0 draws the next multiscale input size (multiples of 32

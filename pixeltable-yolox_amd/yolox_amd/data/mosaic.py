@@ -165,7 +165,20 @@ class ResidentImages:
         self.ids: list = []
         images = []
         off = 0
+        # a dataset whose items repeat stored images (source_index) uploads each image once
+        src_of = getattr(dataset, "source_index", None)
+        first: dict = {}
         for i in range(n):
+            src = src_of(i) if src_of is not None else i
+            if src in first:
+                j = first[src]
+                self.shapes[i], self.offsets[i] = self.shapes[j], self.offsets[j]
+                lab = dataset.load_anno(i) if hasattr(dataset, "load_anno") else self.labels[j]
+                self.labels.append(np.array(lab, copy=True))
+                self.infos.append(self.infos[j])
+                self.ids.append(np.array([i]))
+                continue
+            first[src] = i
             img, lab, info, img_id = dataset.pull_item(i)
             img = np.ascontiguousarray(img, dtype=np.uint8)
             if img.ndim != 3 or img.shape[2] != 3:
@@ -173,7 +186,7 @@ class ResidentImages:
             self.shapes[i] = img.shape[:2]
             self.offsets[i] = off
             off += (img.nbytes + 15) & ~15
-            images.append(img)
+            images.append((i, img))
             self.labels.append(np.array(lab, copy=True))
             self.infos.append(info)
             self.ids.append(img_id)
@@ -181,18 +194,18 @@ class ResidentImages:
         staging = torch.empty(min(max(off, 16), chunk_bytes), dtype=torch.uint8)
         if self.device.type == "cuda":
             staging = staging.pin_memory()
-        i = 0
-        while i < n:  # pack a chunk of whole images, copy it in one H2D transfer
-            j, start = i, int(self.offsets[i])
-            while j < n and int(self.offsets[j]) + images[j].nbytes - start <= staging.numel():
+        i, m = 0, len(images)
+        while i < m:  # pack a chunk of whole images, copy it in one H2D transfer
+            j, start = i, int(self.offsets[images[i][0]])
+            while j < m and int(self.offsets[images[j][0]]) + images[j][1].nbytes - start <= staging.numel():
                 j += 1
             if j == i:
-                raise ValueError(f"image {i} ({images[i].nbytes} bytes) exceeds the staging chunk")
+                raise ValueError(f"image {images[i][0]} ({images[i][1].nbytes} bytes) exceeds the staging chunk")
             view = staging.numpy()
             for k in range(i, j):
-                o = int(self.offsets[k]) - start
-                view[o:o + images[k].nbytes] = images[k].reshape(-1)
-            end = int(self.offsets[j - 1]) + images[j - 1].nbytes
+                o = int(self.offsets[images[k][0]]) - start
+                view[o:o + images[k][1].nbytes] = images[k][1].reshape(-1)
+            end = int(self.offsets[images[j - 1][0]]) + images[j - 1][1].nbytes
             self.pool[start:end].copy_(staging[:end - start], non_blocking=False)
             i = j
 
@@ -473,15 +486,23 @@ class SyntheticDetectionDataset:
     see structured content."""
 
     def __init__(self, size: int, img_size=(640, 640), seed: int = 0, num_classes: int = 80,
-                 min_side: int = 32, max_side: int = 960, empty_every: int = 7):
+                 min_side: int = 32, max_side: int = 960, empty_every: int = 7, distinct: Optional[int] = None):
+        """``distinct``: item i is item i % distinct (a dataset of ``size`` samples over that
+        many different images, so the resident pool stays small for COCO-sized epochs)."""
         self.size, self.img_size, self.seed = size, tuple(img_size), seed
         self.num_classes, self.min_side, self.max_side, self.empty_every = num_classes, min_side, max_side, empty_every
+        self.distinct = min(distinct, size) if distinct else None
         self._cache: dict = {}
+
+    def source_index(self, i: int) -> int:
+        """The stored image item i shows (ResidentImages uploads each once)."""
+        return i % self.distinct if self.distinct else i
 
     def __len__(self) -> int:
         return self.size
 
     def _item(self, i: int):
+        i = self.source_index(i)
         if i in self._cache:
             return self._cache[i]
         rng = np.random.default_rng((self.seed, i))

@@ -195,50 +195,6 @@ class InfiniteSampler:
         return self._size // self._world_size
 
 
-class SyntheticCocoDataset:
-    """COCO-shaped training samples (no datasets offline): item i is a seeded uint8 image
-    as float32 CHW in [0, 255] and ``[120, 5]`` padded targets (cls, cx, cy, w, h) in
-    pixels, the layout TrainTransform hands the trainer (data_augment.py:159-232)."""
-
-    def __init__(self, size: int, input_size, seed: int = 0, max_labels: int = 120):
-        self.size, self.input_size, self.seed, self.max_labels = size, tuple(input_size), seed, max_labels
-
-    def __len__(self) -> int:
-        return self.size
-
-    def __getitem__(self, i: int):
-        import numpy as np
-
-        from .weights import synthetic_labels
-        h, w = self.input_size
-        rng = np.random.default_rng((self.seed, int(i)))
-        img = rng.integers(0, 256, size=(3, h, w), dtype=np.uint8).astype(np.float32)
-        lab = synthetic_labels(1, h, w, max_labels=self.max_labels, seed=int(rng.integers(1 << 31)))[0]
-        return torch.from_numpy(img), torch.from_numpy(lab)
-
-
-class SyntheticBatches:
-    """Batches of ``batch_size`` samples in sampler order (YoloBatchSampler over an
-    InfiniteSampler, drop_last False: len = ceil(len(sampler) / batch_size))."""
-
-    def __init__(self, dataset: SyntheticCocoDataset, sampler: InfiniteSampler, batch_size: int):
-        self.dataset, self.sampler, self.batch_size = dataset, sampler, batch_size
-        self._it = iter(sampler)
-
-    def __len__(self) -> int:
-        return (len(self.sampler) + self.batch_size - 1) // self.batch_size
-
-    def next_indices(self) -> list:
-        return [next(self._it) for _ in range(self.batch_size)]
-
-    def next(self):
-        items = [self.dataset[i] for i in self.next_indices()]
-        return torch.stack([a for a, _ in items]), torch.stack([b for _, b in items])
-
-    def close_mosaic(self) -> None:  # no mosaic in the synthetic pipeline
-        pass
-
-
 # ------------------------------------------------------------------ trainer
 class Trainer:
     """core/trainer.py:34-330 on the HIP path: before_train builds the model, the reference

@@ -560,6 +560,18 @@ def gen_mosaic(ref) -> None:
             arrays[f"{case}.{s}.info"] = np.array(info, np.int64)
             arrays[f"{case}.{s}.id"] = np.array(img_id, np.int64).reshape(-1)
         print(f"mosaic {case}: {MOSAIC_SEEDS} samples")
+    # the close_mosaic boundary (trainer.py:217-230 -> YoloBatchSampler(mosaic=False)): ONE seed,
+    # MOSAIC_SEEDS samples drawn with mosaic on, then MOSAIC_SEEDS with it off -- pins which
+    # random draws each mode consumes across the switch
+    ds = mosaic.MosaicDetection(FixtureDataset(), MOSAIC_HW,
+                                preproc=ref.augment.TrainTransform(max_labels=120, flip_prob=0.5, hsv_prob=1.0),
+                                degrees=10.0, translate=0.1, shear=2.0, **MOSAIC_CASES["default"])
+    pyrandom.seed(4242)
+    np.random.seed(4242)
+    for s in range(2 * MOSAIC_SEEDS):
+        _, lab, _, _ = ds[(s < MOSAIC_SEEDS, (3 * s + 1) % len(images))]
+        arrays[f"boundary.{s}.labels"] = lab
+    print(f"mosaic boundary: {2 * MOSAIC_SEEDS} samples")
     save("mosaic_aug.npz", **arrays)
 
 

@@ -14,7 +14,8 @@ def probe(out_dir: str, batch_size: int, dataset_size: int) -> None:
     random.seed(1000 + rank)  # different on every rank: only the broadcast makes sizes agree
     cfg = named_config("yolox_s")
     sizes = [cfg.random_resize(None, 0, rank, world > 1) for _ in range(3)]
-    loader = cfg.get_data_loader(batch_size=batch_size, is_distributed=world > 1, dataset_size=dataset_size)
+    loader = cfg.get_data_loader(batch_size=batch_size, is_distributed=world > 1, dataset_size=dataset_size,
+                                 device="cpu", distinct_images=4)
     batches = [loader.next_indices() for _ in range(2)]
     x = torch.zeros(1, 3, 64, 64)
     t = torch.tensor([[[1.0, 32.0, 16.0, 8.0, 4.0]]])

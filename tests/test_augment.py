@@ -133,3 +133,49 @@ def test_synthetic_detection_dataset():
         np.testing.assert_array_equal(ds.load_anno(i), lab)
         shapes.add(img.shape)
     assert len(shapes) > 4
+
+
+def test_training_loader_is_the_mosaic_pipeline_across_close_mosaic(fixture):
+    """config.get_data_loader (config.py:203-273) builds the device MosaicDetection pipeline
+    with the config's augmentation parameters; across close_mosaic (trainer.py:217-230) the
+    random draws follow the reference's order: the fixture's `boundary` samples are the
+    reference's MosaicDetection seeded ONCE, 12 samples with mosaic on, then 12 with it off."""
+    from yolox_amd.config import named_config
+    g, images, labels = fixture
+    cfg = named_config("yolox_s")
+    cfg.input_size = tuple(int(v) for v in g["input_hw"])
+    loader = cfg.get_data_loader(batch_size=4, is_distributed=False, dataset=ArrayDataset(images, labels),
+                                 device="cpu")
+    ds = loader.dataset
+    assert isinstance(ds, M.GpuMosaicDetection) and ds.enable_mosaic
+    assert (ds.degrees, ds.translate, ds.shear, tuple(ds.scale), ds.enable_mixup) == (
+        cfg.degrees, cfg.translate, cfg.shear, tuple(cfg.mosaic_scale), cfg.enable_mixup)
+    random.seed(4242)
+    np.random.seed(4242)
+    n = len(images)
+    kinds = []
+    for s in range(2 * SEEDS):
+        if s == SEEDS:
+            loader.close_mosaic()
+        p, lab = ds.draw((3 * s + 1) % n)
+        kinds.append(p.mosaic)
+        np.testing.assert_array_equal(lab, g[f"boundary.{s}.labels"], err_msg=f"boundary sample {s}")
+    assert kinds == [True] * SEEDS + [False] * SEEDS
+
+
+def test_trainer_closes_mosaic_at_the_reference_epoch():
+    """Trainer.before_epoch (trainer.py:217-230): mosaic off and the L1 loss on from epoch
+    max_epoch - no_aug_epochs - 1 (0-based) onwards, or from the start with no_aug."""
+    import types
+
+    from yolox_amd.trainer import Trainer
+    cfg = types.SimpleNamespace(max_epoch=5, no_aug_epochs=2, ema=False, input_size=(64, 64))
+    for no_aug, first_closed in ((False, 2), (True, 0)):
+        tr = Trainer.__new__(Trainer)
+        tr.exp, tr.max_epoch, tr.no_aug, tr.is_distributed = cfg, cfg.max_epoch, no_aug, False
+        closed = []
+        tr.train_loader = types.SimpleNamespace(close_mosaic=lambda: closed.append(tr.epoch))
+        tr.model = types.SimpleNamespace(head=types.SimpleNamespace(use_l1=False))
+        for tr.epoch in range(cfg.max_epoch):
+            tr.before_epoch()
+        assert closed[0] == first_closed and tr.model.head.use_l1
