@@ -76,7 +76,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     constexpr int K2 = TN + PGC, KB2 = K2 / 32;
     constexpr int WN2 = PG ? (NW < PGN / 16 ? NW : PGN / 16) : 1, WM2 = NW / WN2;
     constexpr int NF2 = PG ? PGN / 16 / WN2 : 1, PF2 = TM / 16 / WM2;
-    static_assert(!PG || (WK == 1 && !F1 && TN % 32 == 0 && PGC % 32 == 0 && PGN % (16 * WN2) == 0 &&
+    static_assert(!PG || (!F1 && TN % 32 == 0 && PGC % 32 == 0 && PGN % (16 * WN2) == 0 &&
                           NW % WN2 == 0 && (TM / 16) % WM2 == 0), "post-conv tile");
     // fused Bottleneck (F1): t = act(W1 . x + b1) of the halo tile, computed into one more
     // halo-shaped LDS image that the 3x3 then reads; wave w computes t channels
@@ -630,6 +630,12 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 44: return launch_ws<T, 64, 1, 16, 8, 64, 2, 1, 2, 1, false, 128, 64>(p, st);
         case 45: return launch_ws<T, 64, 2, 16, 2, 128, 4, 1, 1, 1, false, 128, 0>(p, st);
         case 46: return launch_ws<T, 64, 2, 16, 4, 128, 4, 1, 1, 1, false, 128, 0>(p, st);
+        // K split over two waves: half the stationary weights per wave, so two blocks per CU
+        // (64 -> 64) or eight waves per block (s2 64 -> 128) fit the post conv's weights too
+        case 47: return launch_ws<T, 64, 1, 16, 2, 64, 2, 2, 1, 2, false, 128, 64>(p, st);
+        case 48: return launch_ws<T, 64, 1, 16, 4, 64, 2, 2, 1, 1, false, 128, 64>(p, st);
+        case 49: return launch_ws<T, 64, 2, 16, 2, 128, 4, 2, 1, 1, false, 128, 0>(p, st);
+        case 50: return launch_ws<T, 64, 2, 16, 4, 128, 4, 2, 1, 1, false, 128, 0>(p, st);
         default: set_error("conv_ws tile id %d", id); return YXH_EINVAL;
     }
 }

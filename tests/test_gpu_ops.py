@@ -750,7 +750,7 @@ POST_GEOMS = [  # cin(=cout), stride, post_src channels, post_cout, H, W (input)
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("geom", POST_GEOMS)
 def test_conv_ws_post_conv(dtype, geom, residual):
-    """conv_ws post tiles (ids 221-226, round 4): a Bottleneck's 3x3 (+ shortcut) followed by
+    """conv_ws post tiles (ids 221-230, round 4): a Bottleneck's 3x3 (+ shortcut) followed by
     CspLayer.conv3 over [y | x_2] (network_blocks.py:95-99, 180-183), or a stage's stride-2 3x3
     followed by its CspLayer conv1 | conv2 (darknet.py:148-156, network_blocks.py:176-178), in
     one launch -- y never leaves LDS.  vs torch fp32 with y rounded to the compute dtype as the
@@ -778,7 +778,7 @@ def test_conv_ws_post_conv(dtype, geom, residual):
         X2[..., 32:] = nhwc(x2, dtype)
     pw, pb = pack(pconv, pbn, dtype)
     ran = 0
-    for tid in range(221, 227):
+    for tid in range(221, 231):
         Z = torch.full((B, oh, ow, pout + 16), 3.0, dtype=dtype, device=DEV)
         try:
             run_conv([(X, 0, cin, 0)], conv, bn, dtype, residual=(R, 0) if residual else None, tile=2 * tid,
@@ -793,6 +793,37 @@ def test_conv_ws_post_conv(dtype, geom, residual):
         run_conv([(X, 0, cin, 0)], conv, bn, dtype, tile=2 * 166,
                  post=(pw, pb, (X2, 32, c2) if c2 else None, torch.zeros(B, oh, ow, pout, dtype=dtype, device=DEV),
                        0, pout))
+
+
+@pytest.mark.parametrize("geom", POST_GEOMS)
+def test_conv_ws_post_conv_bit_exact_vs_two_launches(geom):
+    """A post tile computes exactly what the two launches it replaces compute: the plain
+    conv_ws tile with the same wave tiling (same MFMA order, y rounded to bf16) storing y, then
+    a dense 1x1 (conv_pwf: K in the same 32-deep order) over [y | x_2] -- bit for bit."""
+    cin, s, c2, pout, H, W, B = geom
+    dtype = torch.bfloat16
+    conv, bn = make_conv(cin, cin if s == 1 else 2 * cin, 3, s, seed=cin + H + 1)
+    cout = conv.out_channels
+    pconv, pbn = make_conv(cout + c2, pout, 1, 1, seed=cin + W + 1)
+    g = torch.Generator().manual_seed(H * W + cin + 1)
+    X = nhwc(torch.randn(B, cin, H, W, generator=g), dtype)
+    oh, ow = (H - 1) // s + 1, (W - 1) // s + 1
+    residual = s == 1
+    cat = torch.zeros(B, oh, ow, cout + c2, dtype=dtype, device=DEV)
+    if residual:
+        cat[..., :cout] = nhwc(torch.randn(B, cout, oh, ow, generator=g), dtype)
+    if c2:
+        cat[..., cout:] = nhwc(torch.randn(B, c2, oh, ow, generator=g), dtype)
+    pw, pb = pack(pconv, pbn, dtype)
+    plain = {(32, 1): 178, (64, 1): 166, (64, 2): 168}[(cin, s)]  # conv_ws ids 18 / 6 / 8
+    post = {(32, 1): 221, (64, 1): 223, (64, 2): 225}[(cin, s)]   # the same wave tiling + post conv
+    Z = torch.zeros(B, oh, ow, pout, dtype=dtype, device=DEV)
+    run_conv([(X, 0, cin, 0)], conv, bn, dtype, residual=(cat, 0) if residual else None, tile=2 * post,
+             post=(pw, pb, (cat, cout, c2) if c2 else None, Z, 0, pout))
+    y = run_conv([(X, 0, cin, 0)], conv, bn, dtype, residual=(cat, 0) if residual else None, out=cat.clone(),
+                 tile=2 * plain)
+    z = run_conv([(y, 0, cout + c2, 0)], pconv, pbn, dtype, tile=2 * 97)
+    assert torch.equal(Z, z), (Z.float() - z.float()).abs().max().item()
 
 
 def test_pack_frag_layout():
