@@ -136,6 +136,16 @@ typedef struct {
     int32_t post_cout;
     int32_t post_dst_cstride;
     int64_t post_dst_bstride;
+    /* Head form (with YXH_CONV_GROUPS2: a level's cls_convs[k][1] | reg_convs[k][1]): group 0's
+     * tile feeds the class preds (post_weight [post_cout = C][cout/2], 65-80 classes), group 1's
+     * the reg | obj preds (post_weight2 [post_cout2 = 5][cout/2]); both write the level's fp32
+     * [B, A, 5 + C] rows (post_dst = the level's first row, post_dst_cstride = 5 + C) decoded as
+     * yxh_head_pred does (yolo_head.py:149-251): ch 0-1 (v + grid) * post_stride, 2-3
+     * exp(v) * post_stride, 4.. sigmoid. */
+    const void* post_weight2;
+    const float* post_bias2;
+    int32_t post_cout2;
+    float post_stride;
 } yxh_conv_desc;
 
 #define YXH_CONV_ACCUMULATE 1

@@ -513,20 +513,43 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     p.res_dense = d->residual && d->res_bstride == (long long)p.ohw * d->res_cstride;
     p.pw1 = d->pre_weight;
     p.pb1 = d->pre_bias;
+    YXH_CHECK_ARG(!d->weight_frag || (dt != YXH_F32 && aligned16(d->weight_frag) && d->cout % 16 == 0 &&
+                                      d->cin % 32 == 0 && d->groups == 1),
+                  "weight_frag: 16-bit, cout %% 16 == 0, cin %% 32 == 0, groups 1");
+    p.wf = d->weight_frag;
+    YXH_CHECK_ARG(d->grid_cap >= 0, "grid_cap %d", d->grid_cap);
+    p.cus = d->grid_cap > 0 && d->grid_cap < 256 ? d->grid_cap : 256;
+    p.grp2 = grp2 ? 1 : 0;
     if (d->post_weight) {
+        // a 1x1 post conv (or the head form: two groups, each with its own preds) runs on the
+        // conv_ws post tiles; dispatched here, after the grid / weight-copy fields are set
+        const bool head = grp2;
         YXH_CHECK_ARG(dt != YXH_F32 && d->post_bias && d->post_dst && aligned16(d->post_weight) && d->post_cout > 0 &&
-                          d->post_cout % 16 == 0 && d->kh == 3 && d->groups == 1 && !d->pre_weight && !grp2 &&
-                          d->post_src.channels >= 0 && d->post_src.channels % 32 == 0 &&
-                          (d->post_src.channels == 0 || (d->post_src.ptr && aligned16(d->post_src.ptr) &&
-                                                         d->post_src.cstride % 8 == 0 && d->post_src.bstride % 8 == 0 &&
-                                                         !d->post_src.upsample && d->post_src.h == d->out_h &&
-                                                         d->post_src.w == d->out_w)) &&
-                          ((uintptr_t)d->post_dst % 8) == 0 && d->post_dst_cstride % 4 == 0 &&
-                          d->post_dst_bstride % 4 == 0,
-                      "post conv: 16-bit 3x3 conv (no pre_weight / groups), post_cout %% 16, post_src channels %% 32 "
-                      "at the output size (16-byte rows), 8-byte aligned post_dst rows");
+                          d->kh == 3 && d->groups == 1 && !d->pre_weight && d->post_src.channels >= 0 &&
+                          d->post_src.channels % 32 == 0,
+                      "post conv: 16-bit 3x3 conv (no pre_weight / groups), post_src channels %% 32");
+        if (head) {
+            YXH_CHECK_ARG(d->post_weight2 && d->post_bias2 && aligned16(d->post_weight2) && d->post_cout2 == 5 &&
+                              d->post_cout >= 65 && d->post_cout <= 80 && d->post_src.channels == 0 &&
+                              ((uintptr_t)d->post_dst % 4) == 0 && d->post_dst_cstride == 5 + d->post_cout,
+                          "head post form: reg|obj (5) and 65-80 class preds, rows of 5 + classes fp32");
+        } else {
+            YXH_CHECK_ARG(d->post_cout % 16 == 0 && !d->post_weight2 &&
+                              (d->post_src.channels == 0 ||
+                               (d->post_src.ptr && aligned16(d->post_src.ptr) && d->post_src.cstride % 8 == 0 &&
+                                d->post_src.bstride % 8 == 0 && !d->post_src.upsample &&
+                                d->post_src.h == d->out_h && d->post_src.w == d->out_w)) &&
+                              ((uintptr_t)d->post_dst % 8) == 0 && d->post_dst_cstride % 4 == 0 &&
+                              d->post_dst_bstride % 4 == 0,
+                          "post conv: post_cout %% 16, post_src at the output size (16-byte rows), 8-byte aligned "
+                          "post_dst rows");
+        }
         p.pgw = d->post_weight;
         p.pgb = d->post_bias;
+        p.pgw2 = d->post_weight2;
+        p.pgb2 = d->post_bias2;
+        p.pg_cout2 = d->post_cout2;
+        p.pg_stride = d->post_stride;
         p.pgd = d->post_dst;
         p.pgd_cs = d->post_dst_cstride;
         p.pgd_bs = d->post_dst_bstride;
@@ -536,19 +559,13 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         p.pgs_ch = d->post_src.channels;
         p.pg_cout = d->post_cout;
         if (d->tile == 0)  // default post tile per shape
-            return conv_ws_dispatch(dt, d->stride == 2 ? 45 : d->cin == 32 ? 41 : 43, p, st);
+            return conv_ws_dispatch(dt, head ? 51 : d->stride == 2 ? 45 : d->cin == 32 ? 41 : 43, p, st);
         if (!((d->tile >> 1) > 220 && (d->tile >> 1) <= 220 + kNumWsPostTiles)) {
             set_error("a post conv runs on the conv_ws post tiles (ids 221-%d) only", 220 + kNumWsPostTiles);
             return YXH_EUNSUPPORTED;
         }
+        return conv_ws_dispatch(dt, (d->tile >> 1) - 220 + 40, p, st);
     }
-    YXH_CHECK_ARG(!d->weight_frag || (dt != YXH_F32 && aligned16(d->weight_frag) && d->cout % 16 == 0 &&
-                                      d->cin % 32 == 0 && d->groups == 1),
-                  "weight_frag: 16-bit, cout %% 16 == 0, cin %% 32 == 0, groups 1");
-    p.wf = d->weight_frag;
-    YXH_CHECK_ARG(d->grid_cap >= 0, "grid_cap %d", d->grid_cap);
-    p.cus = d->grid_cap > 0 && d->grid_cap < 256 ? d->grid_cap : 256;
-    p.grp2 = grp2 ? 1 : 0;
     if (grp2 && d->tile == 0) return conv_ws_dispatch(dt, d->cin == 256 ? 176 - 160 : 185 - 160, p, st);
     if (grp2 && !((d->tile >> 1) > 160 && (d->tile >> 1) <= 190)) {
         set_error("YXH_CONV_GROUPS2 runs on the plain conv_ws tiles (ids 161-190) only");

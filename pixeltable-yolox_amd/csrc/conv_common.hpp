@@ -42,6 +42,11 @@ struct ConvParams {
     int pgs_cs, pgs_ch;
     long long pgs_bs;
     int pg_cout;
+    // head form (groups2 + post_weight2): group 1's preds, the decode stride
+    const void* pgw2;
+    const float* pgb2;
+    int pg_cout2;
+    float pg_stride;
 };
 
 // Stationary weight fragment (i: 16 output channels from n_first, tap, kb: 32-channel K block)
@@ -299,7 +304,7 @@ int conv_ws_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumWsTiles = 36;  // 31..36: fused Bottleneck (pre_weight)
 // conv_ws tiles with a 1x1 post conv (yxh_conv_desc.post_weight): tile ids 221..220+kNumWsPostTiles
 // (conv_ws_dispatch ids 41..40+kNumWsPostTiles)
-constexpr int kNumWsPostTiles = 10;
+constexpr int kNumWsPostTiles = 13;
 // Weight-stationary persistent 1x1 conv over dense sources (conv_ws1.hip): tile ids 201..200+kNumWs1Tiles
 int conv_ws1_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumWs1Tiles = 10;

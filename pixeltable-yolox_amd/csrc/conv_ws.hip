@@ -45,7 +45,7 @@ constexpr int ws_hxp(int tx, int s) {
 }  // namespace
 
 template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC, bool F1, int PGN = 0,
-          int PGC = 0>
+          int PGC = 0, int PGH = 0>
 __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, int tiles_x, int tiles_y,
                                                                  int ntiles, int ntn, int nwork) {
     static_assert(sizeof(T) == 2, "16-bit operands");
@@ -67,10 +67,13 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     // residual slot layout (a ring of two slots, the residual DMA'd in and Y written over it
     // in place) and Z = SiLU(W2 . [Y | X2] + b2) of PGN channels leaves instead, X2 = PGC
     // channels of post_src DMA'd per tile (ring of two)
-    constexpr bool PG = PGN > 0;
-    constexpr int RS = TN / 8 + 1, RSLOTS = (S == 1 || PG) ? TM * RS : 0;
+    // Head form (PGH > 0 class fragments; YXH_CONV_GROUPS2): the same Y ring, and instead of a
+    // bf16 post conv each group's block runs its level's preds over Y (group 0: PGH x 16 class
+    // rows, group 1: the 5 reg | obj rows; weights in LDS) into decoded fp32 [B, A, 5 + C] rows
+    constexpr bool PG = PGN > 0, HP = PGH > 0, PGY = PG || HP;
+    constexpr int RS = TN / 8 + 1, RSLOTS = (S == 1 || PGY) ? TM * RS : 0;
     constexpr int RLOADS = (RSLOTS + 63) / 64, GR = (RLOADS + NW - 1) / NW, RTB = RLOADS * 1024;
-    constexpr int NRING = PG ? 2 : 3;
+    constexpr int NRING = PGY ? 2 : 3;
     constexpr int XS = PGC / 8 + 1, XSLOTS = PG && PGC > 0 ? TM * XS : 0;
     constexpr int XLOADS = (XSLOTS + 63) / 64, GX = (XLOADS + NW - 1) / NW, XTB = XLOADS * 1024;
     constexpr int K2 = TN + PGC, KB2 = K2 / 32;
@@ -78,13 +81,16 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     constexpr int NF2 = PG ? PGN / 16 / WN2 : 1, PF2 = TM / 16 / WM2;
     static_assert(!PG || (!F1 && TN % 32 == 0 && PGC % 32 == 0 && PGN % (16 * WN2) == 0 &&
                           NW % WN2 == 0 && (TM / 16) % WM2 == 0), "post-conv tile");
+    static_assert(!HP || (!PG && !F1 && S == 1 && TN % 32 == 0), "head-form tile");
+    constexpr int HROWS = HP ? PGH * 16 : 0, HBYTES_W = HROWS * RS * 16 + HROWS * 4;
     // fused Bottleneck (F1): t = act(W1 . x + b1) of the halo tile, computed into one more
     // halo-shaped LDS image that the 3x3 then reads; wave w computes t channels
     // 32 (w % NG) .. +32 of every R-th 16-pixel halo fragment
     constexpr int NG = CIN / 32, R1 = NW / NG, NPA = (HY * HXP + 15) / 16;
     constexpr int XOFF = 2 * HBYTES + RBYTES + NRING * RTB;
     constexpr int TOFF = XOFF + 2 * XTB;
-    constexpr int SMEM = TOFF + (F1 ? HBYTES : 0);
+    constexpr int HWOFF = TOFF + (F1 ? HBYTES : 0);
+    constexpr int SMEM = HWOFF + HBYTES_W;
     static_assert(!F1 || (S == 1 && NW % NG == 0), "fused Bottleneck tile");
     constexpr int FCO = (FC + WK - 1) / WK;  // pixel fragments this wave finishes
     static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0 && TM % (16 * WM) == 0, "tile");
@@ -154,6 +160,22 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 #pragma unroll
             for (int r = 0; r < 4; ++r) b2[f][r] = p.pgb[n + fq * 4 + r];
         }
+    }
+
+    // head form: this block's group's pred weights [rows][TN] (rows of RS 16-byte slots) and
+    // biases -> LDS once; rows past the group's count are zero (visible after the first barrier)
+    const bool hgrp1 = HP && n0 >= cout / 2;
+    const int hrows = HP ? (hgrp1 ? p.pg_cout2 : p.pg_cout) : 0;
+    if constexpr (HP) {
+        const T* hw = (const T*)(hgrp1 ? p.pgw2 : p.pgw);
+        const float* hb = hgrp1 ? p.pgb2 : p.pgb;
+        char* wl = smem + HWOFF;
+        for (int q = tid; q < HROWS * (TN / 8); q += 64 * NW) {
+            const int r = q / (TN / 8), c = q - (TN / 8) * (q / (TN / 8));
+            *(uint4*)(wl + (r * RS + c) * 16) = r < hrows ? *(const uint4*)(hw + (long long)r * TN + c * 8)
+                                                          : make_uint4(0, 0, 0, 0);
+        }
+        for (int q = tid; q < HROWS; q += 64 * NW) ((float*)(wl + HROWS * RS * 16))[q] = q < hrows ? hb[q] : 0.0f;
     }
 
     // ---- this lane's LDS byte offsets of its pixel fragments at tap (0, 0), channel block 0
@@ -306,7 +328,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
         u32x2 u;
         __builtin_memcpy(&u, t, 8);
-        if constexpr (PG) {
+        if constexpr (PGY) {
             (void)od;  // Y stays in LDS, over this lane's own residual values
             *(u32x2*)(e.rl + (pl * RS + (nl >> 3)) * 16 + (nl & 7) * 2) = u;
         } else if (!(YXH_WS_PROBE & 1) || p.act == 12345) {
@@ -361,6 +383,51 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         }
     };
 
+    // head form: the preds of a finished tile (Y complete in ring slot k % 2), decoded, as
+    // head.hip's head_pred (same MFMA order and exp / sigmoid), dword stores of fp32 rows
+    auto hp_tile = [&](const TileC c, const int k) {
+        if constexpr (HP) {
+            const char* ys = smem + 2 * HBYTES + RBYTES + (k & 1) * RTB;
+            const char* wl = smem + HWOFF;
+            const float* bl = (const float*)(wl + HROWS * RS * 16);
+            const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)((float*)p.pgd + (long long)c.b * p.pgd_bs), (short)0, (int)((long long)ohw * p.pgd_cs * 4),
+                0x00020000);
+            const int nf = hgrp1 ? 1 : PGH;
+            const int col0 = hgrp1 ? 0 : 5;
+            const float st = p.pg_stride;
+            for (int pf = wave; pf < TM / 16; pf += NW) {
+                const int pl = pf * 16 + frow;
+                const int ty = pl / TX, tx = pl - ty * TX;
+                const int oy = c.oy0 + ty, ox = c.ox0 + tx;
+                const bool okp = oy < OH && ox < OW;
+                const int rowo = (oy * OW + ox) * p.pgd_cs;
+                for (int f = 0; f < nf; ++f) {  // one 16-row fragment at a time (few live registers)
+                    f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int kb = 0; kb < TN / 32; ++kb)
+                        Mma<T>::run(z, *(const uint4*)(wl + ((f * 16 + frow) * RS + kb * 4 + fq) * 16),
+                                    *(const uint4*)(ys + (pl * RS + kb * 4 + fq) * 16));
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int ch = f * 16 + fq * 4 + r;
+                        float v = z[r] + bl[ch];
+                        if (hgrp1) {
+                            if (ch < 2) v = (v + (float)(ch == 0 ? ox : oy)) * st;
+                            else if (ch < 4) v = __builtin_amdgcn_exp2f(v * 1.4426950408889634f) * st;
+                            else v = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
+                        } else {
+                            v = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
+                        }
+                        const bool ok = okp && ch < hrows;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), osrd,
+                                                              ok ? (rowo + col0 + ch) * 4 : (int)dma::kOob, 0, 0);
+                    }
+                }
+            }
+        }
+    };
+
     f32x4 accp[FR][FCO];  // owned fragments of the previous tile, waiting for their epilogue
     constexpr int NS = WCB * 9;
     constexpr int NP = FR * FCO;  // epilogue pieces, one per K step while they last
@@ -378,10 +445,10 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             cnext = coords(next);
             if (!(YXH_WS_PROBE & 2)) {
                 issue_halo(cnext, kb ^ 1);
-                if (!PG && has_res) issue_res(cnext, (k + 1) % 3);
+                if (!PGY && has_res) issue_res(cnext, (k + 1) % 3);
             }
         }
-        if constexpr (PG) {  // this tile's residual / X2: read one step later (ring of two)
+        if constexpr (PGY) {  // this tile's residual / X2: read one step later (ring of two)
             if (has_res) issue_res(cur, k & 1);
             issue_x2(cur, k & 1);
         }
@@ -497,16 +564,17 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 #pragma unroll
                 for (int j = 0; j < FC; ++j) accp[i][j] = acc[i][j];
         }
-        if constexpr (PG && EPI) {  // the previous tile's Y is complete in LDS: its post conv
+        if constexpr (PGY && EPI) {  // the previous tile's Y is complete in LDS: its post conv
             dma::barrier();
-            pg_tile(prev, k - 1);
+            if constexpr (PG) pg_tile(prev, k - 1);
+            else hp_tile(prev, k - 1);
         }
         return next;
     };
 
     TileC cur = coords(tile), cnext{0, 0, 0};
     issue_halo(cur, 0);
-    if (!PG && has_res) issue_res(cur, 0);
+    if (!PGY && has_res) issue_res(cur, 0);
     // the first tile is peeled off the loop: it consumes the weight loads, so the loop body
     // carries no compiler-visible pending load whose wait would also drain the halo DMA
     int next = tile_step(cur, tile, 0, cnext, cur, std::false_type{});
@@ -516,32 +584,39 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         cur = cnext;
         next = tile_step(cur, next, k, cnext, prev, std::true_type{});
     }
-    if constexpr (PG) {  // the last tile's residual / X2 were issued in its own step
+    if constexpr (PGY) {  // the last tile's residual / X2 were issued in its own step
         dma::wait_vm<0>();
         dma::barrier();
     }
     epilogue(cur, k - 1, accp);
-    if constexpr (PG) {
+    if constexpr (PGY) {
         dma::barrier();
-        pg_tile(cur, k - 1);
+        if constexpr (PG) pg_tile(cur, k - 1);
+        else hp_tile(cur, k - 1);
     }
     (void)ohw;
 }
 
 template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC = 1, bool F1 = false,
-          int PGN = 0, int PGC = 0>
+          int PGN = 0, int PGC = 0, int PGH = 0>
 static int launch_ws(const ConvParams& p, hipStream_t st) {
     if (p.stride != S || p.cin != CIN) {
         set_error("conv_ws variant built for stride %d, %d input channels", S, CIN);
         return YXH_EUNSUPPORTED;
     }
-    if ((p.pgw != nullptr) != (PGN > 0) || (PGN > 0 && (p.pg_cout != PGN || p.pgs_ch != PGC || p.cout != TN))) {
+    if (PGH > 0) {
+        if (!p.grp2 || !p.pgw2 || p.cout != 2 * TN || (p.pg_cout + 15) / 16 != PGH) {
+            set_error("conv_ws head-form tile: two groups of %d channels, %d class fragments", TN, PGH);
+            return YXH_EUNSUPPORTED;
+        }
+    } else if ((p.pgw != nullptr) != (PGN > 0) || p.pgw2 ||
+               (PGN > 0 && (p.pg_cout != PGN || p.pgs_ch != PGC || p.cout != TN))) {
         set_error(PGN > 0 ? "conv_ws post tile built for %d -> %d channels + a %d-channel post_src, post conv %d"
                           : "conv_ws plain tile with a post conv (%d -> %d, %d, %d)",
                   CIN, TN, PGC, PGN);
         return YXH_EUNSUPPORTED;
     }
-    if (p.grp2 && (F1 || (p.cout / 2) % TN)) {
+    if (p.grp2 && (F1 || PGN > 0 || (p.cout / 2) % TN)) {
         set_error("conv_ws variant (%d input channels) cannot split its channel tiles over two groups", CIN);
         return YXH_EUNSUPPORTED;
     }
@@ -551,7 +626,8 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
                   CIN);
         return YXH_EUNSUPPORTED;
     }
-    if (p.dst_f32 || p.accum || (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) || (!p.vec_store && PGN == 0) ||
+    if (p.dst_f32 || p.accum || (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) ||
+        (!p.vec_store && PGN == 0 && PGH == 0) ||
         p.cout % 8 || (p.res && (S != 1 || ((uintptr_t)p.res % 16) || p.res_cs % 8 || p.res_bs % 8))) {
         set_error("conv_ws: 16-bit dst, SiLU/no activation, 8-byte aligned dst rows, 16-byte residual rows "
                   "(stride-1 variants) only");
@@ -565,7 +641,7 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
         return YXH_EINVAL;
     }
     const int nwork = (int)std::min<long long>(ntiles, std::max(1, p.cus * BPC / ntn));
-    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM, BPC, F1, PGN, PGC>), dim3((unsigned)(nwork * ntn)),
+    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM, BPC, F1, PGN, PGC, PGH>), dim3((unsigned)(nwork * ntn)),
                        dim3(64 * WN * WK * WM), 0, st, p, tiles_x, tiles_y, (int)ntiles, ntn, nwork);
     YXH_CHECK_LAUNCH("conv_ws launch");
     return YXH_OK;
@@ -636,6 +712,11 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 48: return launch_ws<T, 64, 1, 16, 4, 64, 2, 2, 1, 1, false, 128, 64>(p, st);
         case 49: return launch_ws<T, 64, 2, 16, 2, 128, 4, 2, 1, 1, false, 128, 0>(p, st);
         case 50: return launch_ws<T, 64, 2, 16, 4, 128, 4, 2, 1, 1, false, 128, 0>(p, st);
+        // head form (ids 51-53 = tiles 231-233): a level's cls_convs[k][1] | reg_convs[k][1] with
+        // each group's preds + decode (yolo_head.py:149-251) in the same launch
+        case 51: return launch_ws<T, 128, 1, 16, 4, 128, 4, 1, 1, 1, false, 0, 0, 5>(p, st);
+        case 52: return launch_ws<T, 128, 1, 8, 4, 128, 4, 2, 1, 1, false, 0, 0, 5>(p, st);
+        case 53: return launch_ws<T, 128, 1, 16, 2, 128, 4, 1, 1, 1, false, 0, 0, 5>(p, st);
         default: set_error("conv_ws tile id %d", id); return YXH_EINVAL;
     }
 }

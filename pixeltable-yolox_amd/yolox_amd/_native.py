@@ -50,7 +50,8 @@ class ConvDesc(C.Structure):
                 ("flags", C.c_int32), ("grid_cap", C.c_int32), ("pre_weight", C.c_void_p), ("pre_bias", C.c_void_p),
                 ("weight_frag", C.c_void_p), ("post_weight", C.c_void_p), ("post_bias", C.c_void_p),
                 ("post_src", Src), ("post_dst", C.c_void_p), ("post_cout", C.c_int32),
-                ("post_dst_cstride", C.c_int32), ("post_dst_bstride", C.c_int64)]
+                ("post_dst_cstride", C.c_int32), ("post_dst_bstride", C.c_int64), ("post_weight2", C.c_void_p),
+                ("post_bias2", C.c_void_p), ("post_cout2", C.c_int32), ("post_stride", C.c_float)]
 
 
 CONV_ACCUMULATE = 1

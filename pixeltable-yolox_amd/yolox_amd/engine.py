@@ -378,6 +378,31 @@ class PlanCtx:
         self.flops += 2.0 * self.batch * src.lh * src.lw * 2 * half * 9 * cin
         return out
 
+    def grouped2_head_fusable(self, head, src: View, train: bool) -> bool:
+        """cls_convs[k][1] | reg_convs[k][1] + the level's preds + decode as ONE conv_ws head-form
+        launch (yxh_conv_desc.post_weight / post_weight2): eval, 16-bit, 128 channels per group,
+        65-80 classes, 16-byte level rows."""
+        return (self.csp_fusion and not train and self.dtype != torch.float32 and src.ch == 256
+                and 65 <= head.num_classes <= 80)
+
+    def conv_grouped2_head(self, ms, src: View, head, k: int, out: "OutBuffer", a_off: int, stride: int) -> None:
+        """The two-group 3x3 (cls | reg, yolo_head.py:160-161) whose blocks keep their 128-channel
+        tiles in LDS and write the level's decoded rows (reg_preds | obj_preds over reg,
+        cls_preds over cls, :149-159, :185-187, :233-251) -- the [cls | reg] map never leaves the
+        CU and the separate pred launch disappears."""
+        ka, kb = ms[0].conv, ms[1].conv
+        cin, half = ka.in_channels, ka.out_channels
+        spec = self._weights([(ka, ms[0].bn), (kb, ms[1].bn)], cin)
+        ro = self._weights([(head.reg_preds[k], None), (head.obj_preds[k], None)], half)
+        cl = self._weights([(head.cls_preds[k], None)], half)
+        self.ops.append(OpRec(N.OP_CONV, dict(
+            srcs=[src], out=None, residual=None, spec=spec, cin=cin, cout=2 * half, k=3, stride=1, pad=1, groups=1,
+            in_h=src.lh, in_w=src.lw, out_h=src.lh, out_w=src.lw, act=N.ACT_CODE["silu"], dst_f32=False,
+            grouped2=True, head_post=dict(cls=cl, ro=ro, out=out, a_off=a_off, stride=float(stride),
+                                          num_classes=head.num_classes))))
+        hw = src.lh * src.lw
+        self.flops += 2.0 * self.batch * hw * 2 * half * 9 * cin + 2.0 * self.batch * hw * (5 + head.num_classes) * half
+
     def spp(self, cat: Buffer, hidden: int) -> None:
         self.ops.append(OpRec(N.OP_SPP, dict(buf=cat, c=hidden)))
 
@@ -420,7 +445,7 @@ class OutBuffer:
 # conv_pwr kernel, 97-104 the dense 1x1 conv_pwf kernel, 113-150 the 3x3 conv_r3 kernel
 # (yoloxhip.h yxh_conv_desc.tile)
 TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
-                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 197)] + [2 * i for i in range(201, 211)] + [2 * i for i in range(221, 231)]
+                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 197)] + [2 * i for i in range(201, 211)] + [2 * i for i in range(221, 234)]
 # 16-bit plans: the families that win on MI355X (profiles/r03/final/tune_r3fa_*.json: yolox_s picks only
 # conv_pwf / conv_ws / conv_ws1; yolox_l fp16 also conv_igemm and conv_r3 once or twice); the LDS-DMA
 # conv_glds, row-tiled conv_rows and the round-1 pointwise kernels never do and are tried only with
@@ -453,7 +478,7 @@ def _tune_key(d) -> tuple:
     return (d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w, d.cin, d.cout, d.kh, d.stride, d.nsrc,
             d.src[0].channels, d.src[0].upsample, d.src[1].upsample if d.nsrc > 1 else 0,
             bool(d.residual), d.dst_dtype, d.dst_cstride == d.cout, d.act >= N.ACT_DECODE, bool(d.pre_weight),
-            d.flags, d.post_cout, d.post_src.channels)
+            d.flags, d.post_cout, d.post_src.channels, d.post_cout2)
 
 
 def op_buffers(r: OpRec) -> tuple:
@@ -468,6 +493,8 @@ def op_buffers(r: OpRec) -> tuple:
         return [], [a["dst"].buf]
     if r.kind == N.OP_HEAD:
         return [a["reg"].buf, a["cls"].buf], []
+    if a.get("head_post") is not None:  # decoded rows (untracked, like OP_HEAD)
+        return [v.buf for v in a["srcs"]], []
     reads = [v.buf for v in a["srcs"]]
     if a.get("residual") is not None:
         reads.append(a["residual"].buf)
@@ -646,7 +673,8 @@ class Plan:
         out_base = out_ptr + c * B * self.anchors * self.out_spec.row * 4
         for i, rec in enumerate(ctx.ops):
             a = rec.args
-            if heads_only and not (rec.kind == N.OP_HEAD or (rec.kind == N.OP_CONV and a["dst_f32"])):
+            if heads_only and not (rec.kind == N.OP_HEAD or (rec.kind == N.OP_CONV and (a["dst_f32"] or
+                                                                                       a.get("head_post")))):
                 continue
             op = self._ops[c * self._nops + i]
             op.kind = rec.kind
@@ -746,7 +774,20 @@ class Plan:
                     d.res_cstride, d.res_bstride = res.buf.c, res.buf.nelem_image
                 d.act = a["act"]
                 pspec = a.get("post_spec")
-                if pspec is not None:  # 1x1 post conv: its output replaces the conv's own
+                hp = a.get("head_post")
+                if hp is not None:  # head form: each group's preds + decode into the level's rows
+                    out, a_off = hp["out"], hp["a_off"]
+                    d.post_weight = self.warena.data_ptr() + hp["cls"].w_off
+                    d.post_bias = self.barena.data_ptr() + hp["cls"].b_off
+                    d.post_weight2 = self.warena.data_ptr() + hp["ro"].w_off
+                    d.post_bias2 = self.barena.data_ptr() + hp["ro"].b_off
+                    d.post_cout, d.post_cout2, d.post_stride = hp["num_classes"], 5, hp["stride"]
+                    d.post_dst = out_base + a_off * out.row * 4
+                    d.post_dst_cstride, d.post_dst_bstride = out.row, out.anchors * out.row
+                    d.dst = d.post_dst
+                    d.dst_dtype = ctx.dcode
+                    d.dst_cstride, d.dst_bstride = out.row, out.anchors * out.row
+                elif pspec is not None:  # 1x1 post conv: its output replaces the conv's own
                     d.post_weight = self.warena.data_ptr() + pspec.w_off
                     d.post_bias = self.barena.data_ptr() + pspec.b_off
                     d.post_cout = pspec.cout

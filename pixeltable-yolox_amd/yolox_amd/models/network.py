@@ -403,8 +403,16 @@ class YoloxHead(_Planned):
             else:
                 c, r = c0.plan(ctx, [s]), r0.plan(ctx, [s])
             c1, r1 = self.cls_convs[k][1], self.reg_convs[k][1]
-            if (c.buf is r.buf and c.coff == 0 and r.coff == c.ch and c.buf.c == 2 * c.ch
-                    and ctx.grouped2_fusable(c1, r1, c.buf.full())):
+            two = (c.buf is r.buf and c.coff == 0 and r.coff == c.ch and c.buf.c == 2 * c.ch
+                   and ctx.grouped2_fusable(c1, r1, c.buf.full()))
+            if two and hasattr(ctx, "grouped2_head_fusable") and ctx.grouped2_head_fusable(self, c.buf.full(), train):
+                # ... with the level's preds + decode riding in the same launch
+                ctx.conv_grouped2_head([c1, r1], c.buf.full(), self, k, out, a_off, self.strides[k])
+                for rec in ctx.ops[n0:]:
+                    rec.lane = 1 + k
+                a_off += x.lh * x.lw
+                continue
+            if two:
                 # cls_convs[k][1] | reg_convs[k][1] over [cls | reg]: one two-group launch
                 cr2 = ctx.conv_grouped2([c1, r1], c.buf.full())
                 half = c1.conv.out_channels

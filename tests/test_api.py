@@ -120,8 +120,12 @@ def test_planner_topology_and_flops(name, hw, gflop, anchors):
     assert s2 == (1 if name == "yolox_s" else 0)
     assert kinds.count(3) + s2 == 1
     heads = kinds.count(4)
+    # ... and with 128-channel head convs (yolox_s) each level's preds ride in its two-group
+    # cls_convs[k][1] | reg_convs[k][1] launch instead (conv_ws head form)
+    n_head_post = sum(1 for o in ctx.ops if o.args.get("head_post") is not None)
+    assert n_head_post == (3 if name == "yolox_s" else 0)
     if name in ("yolox_s", "yolox_l"):  # head widths 128 / 256 (yolox_x: 320, unfused)
-        assert heads == 3
+        assert heads + n_head_post == 3
     # ... and a 16-bit plan folds each fusable Bottleneck's conv1 into its 3x3 (one op)
     n_fused_bneck = sum(1 for o in ctx.ops if o.args.get("pre_spec") is not None)
     n_bneck = sum(1 for x in m.modules() if x.__class__.__name__ == "Bottleneck")
@@ -138,7 +142,8 @@ def test_planner_topology_and_flops(name, hw, gflop, anchors):
     # CspLayer.conv3, a stride-2 stage conv + its CspLayer conv1 | conv2) are one op each
     n_post = sum(1 for o in ctx.ops if o.args.get("post_spec") is not None)
     assert n_post == (4 if name == "yolox_s" else n_post)
-    assert (kinds.count(0) == n_bn_convs - n_csp - fused_head + 2 * (3 - heads) - 1 - n_fused_bneck - n_grouped
+    assert (kinds.count(0) == n_bn_convs - n_csp - fused_head + 2 * (3 - heads - n_head_post) - 1 - n_fused_bneck
+            - n_grouped
             - s2 - 2 * n_stem_csp - n_post)
 
 

@@ -75,7 +75,7 @@ def ref_conv(x, conv, bn, act):
 
 
 def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_coff=0, out_c=None, tile=0, flags=0,
-             pre=None, groups2=False, frag=False, post=None):
+             pre=None, groups2=False, frag=False, post=None, head=None):
     """srcs: list of (nhwc tensor [B,h,w,C], coff, ch, upsample).  post: (packed weight, bias,
     (post_src tensor, coff, ch) or None, post_dst tensor, coff, post_cout): a 1x1 post conv
     whose output goes to post_dst instead of the conv's own output."""
@@ -131,6 +131,14 @@ def run_conv(srcs, conv, bn, dtype, act="silu", residual=None, out=None, out_cof
             ps.h, ps.w = t.shape[1], t.shape[2]
         d.post_dst = pdst.data_ptr() + pcoff * pdst.element_size()
         d.post_dst_cstride, d.post_dst_bstride = pdst.shape[3], pdst.shape[1] * pdst.shape[2] * pdst.shape[3]
+    if head is not None:  # head form: (w_cls, b_cls, w_ro, b_ro, rows [B, A, 5+C] fp32, a_off, stride)
+        wcl, bcl, wro, bro, rows, a_off, stride = head
+        C = wcl.shape[0]
+        d.post_weight, d.post_bias, d.post_weight2, d.post_bias2 = wcl.data_ptr(), bcl.data_ptr(), wro.data_ptr(), \
+            bro.data_ptr()
+        d.post_cout, d.post_cout2, d.post_stride = C, 5, stride
+        d.post_dst = rows.data_ptr() + a_off * (5 + C) * 4
+        d.post_dst_cstride, d.post_dst_bstride = 5 + C, rows.shape[1] * (5 + C)
     n.check(n.lib().yxh_conv2d(ctypes.byref(d), n.stream_ptr()), "conv2d")
     torch.cuda.synchronize()
     return out
@@ -824,6 +832,46 @@ def test_conv_ws_post_conv_bit_exact_vs_two_launches(geom):
                  tile=2 * plain)
     z = run_conv([(y, 0, cout + c2, 0)], pconv, pbn, dtype, tile=2 * 97)
     assert torch.equal(Z, z), (Z.float() - z.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("hw", [(80, 80), (20, 22), (13, 8)])
+def test_conv_ws_head_form_bit_exact_vs_two_launches(hw):
+    """Head-form tiles (ids 231-233, round 4): a level's cls_convs[k][1] | reg_convs[k][1]
+    (two groups) with each group's preds + decode in the same launch compute exactly what the
+    two launches they replace compute -- the plain two-group conv_ws tile with the same wave
+    tiling storing [cls | reg], then yxh_head_pred over it (yolo_head.py:149-251) -- bit for
+    bit, into rows [a_off, a_off + h*w) of a wider [B, A, 85] output (other rows untouched)."""
+    import ctypes as Cc
+    n = N()
+    H, W = hw
+    B, cin, C, stride = 3, 128, 80, 8.0
+    A, a_off = H * W + 40, 24
+    dtype = torch.bfloat16
+    conv, bn = make_conv(cin, 2 * cin, 3, 1, seed=H + 5)
+    g = torch.Generator().manual_seed(H * W)
+    X = nhwc(torch.randn(B, 2 * cin, H, W, generator=g), dtype)
+    wro = (torch.randn(5, cin, generator=g) / cin ** 0.5).to(DEV, dtype)
+    wcl = (torch.randn(C, cin, generator=g) / cin ** 0.5).to(DEV, dtype)
+    bro = (torch.randn(5, generator=g) * 0.2).to(DEV)
+    bcl = (torch.randn(C, generator=g) * 0.2 - 2).to(DEV)
+    for plain, fused in ((185, 231), (171, 232), (186, 233)):
+        y = run_conv([(X, 0, 2 * cin, 0)], conv, bn, dtype, tile=2 * plain, groups2=True)
+        ref = torch.full((B, A, 5 + C), -7.0, device=DEV)
+        d = n.HeadDesc()
+        d.dtype, d.batch, d.h, d.w, d.cin, d.num_classes = n.DTYPE_CODE[dtype], B, H, W, cin, C
+        esz = y.element_size()
+        for src, off in ((d.reg, cin), (d.cls, 0)):
+            src.ptr = y.data_ptr() + off * esz
+            src.channels, src.cstride, src.bstride, src.h, src.w, src.upsample = cin, 2 * cin, H * W * 2 * cin, H, W, 0
+        d.w_reg, d.b_reg, d.w_cls, d.b_cls = wro.data_ptr(), bro.data_ptr(), wcl.data_ptr(), bcl.data_ptr()
+        d.out, d.out_bstride, d.a_off, d.stride, d.train = ref.data_ptr(), A * (5 + C), a_off, stride, 0
+        n.check(n.lib().yxh_head_pred(Cc.byref(d), n.stream_ptr()), "head_pred")
+        got = torch.full((B, A, 5 + C), -7.0, device=DEV)
+        run_conv([(X, 0, 2 * cin, 0)], conv, bn, dtype, tile=2 * fused, groups2=True,
+                 head=(wcl, bcl, wro, bro, got, a_off, stride))
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), (fused, (got - ref).abs().max().item())
+        assert (got[:, :a_off] == -7.0).all() and (got[:, a_off + H * W:] == -7.0).all()
 
 
 def test_pack_frag_layout():
