@@ -74,34 +74,67 @@ def _act(x: Tensor, act: str) -> Tensor:
     raise AttributeError(act)
 
 
+# ------------------------------------------------------------------ storage rounding
+# Emulation of a 16-bit inference path's STORAGE precision (not of its summation order), the
+# yardstick the bf16/fp16 parity bounds are derived from: inside
+# ``stored_as(dtype)`` every BaseConv uses its BN-folded weight rounded to ``dtype`` (fp32 bias),
+# sums in fp32, and rounds its output (after the activation and any Bottleneck shortcut) to
+# ``dtype``, as the device stores every map; the head preds use rounded weights on the rounded
+# features and stay fp32.
+_STORE: Optional[torch.dtype] = None
+
+
+class stored_as:
+    def __init__(self, dtype: Optional[torch.dtype]):
+        self.dtype = dtype
+
+    def __enter__(self):
+        global _STORE
+        self.prev, _STORE = _STORE, self.dtype
+        return self
+
+    def __exit__(self, *exc):
+        global _STORE
+        _STORE = self.prev
+
+
+def _rnd(t: Tensor) -> Tensor:
+    return t.to(_STORE).float() if _STORE is not None else t
+
+
 # ------------------------------------------------------------------ blocks
 def base_conv(sd: SD, p: str, x: Tensor, k: int, s: int, act: str, eps: float,
-              groups: int = 1, bn_train: bool = False) -> Tensor:
-    """BaseConv: conv(bias=False, pad=(k-1)//2) -> BN -> act (network_blocks.py:27-52)."""
+              groups: int = 1, bn_train: bool = False, residual: Optional[Tensor] = None) -> Tensor:
+    """BaseConv: conv(bias=False, pad=(k-1)//2) -> BN -> act (network_blocks.py:27-52), then
+    the Bottleneck shortcut when given (network_blocks.py:97-99)."""
+    if _STORE is not None and not bn_train:
+        w, b = fuse_conv_bn(sd[p + ".conv.weight"], sd[p + ".bn.weight"], sd[p + ".bn.bias"],
+                            sd[p + ".bn.running_mean"], sd[p + ".bn.running_var"], eps)
+        y = _act(F.conv2d(x, _rnd(w), b, s, (k - 1) // 2, 1, groups), act)
+        return _rnd(y + residual if residual is not None else y)
     y = F.conv2d(x, sd[p + ".conv.weight"], None, s, (k - 1) // 2, 1, groups)
     y = F.batch_norm(y, sd[p + ".bn.running_mean"], sd[p + ".bn.running_var"],
                      sd[p + ".bn.weight"], sd[p + ".bn.bias"], bn_train, 0.03, eps)
-    return _act(y, act)
+    y = _act(y, act)
+    return y + residual if residual is not None else y
 
 
 def conv(sd: SD, p: str, x: Tensor, k: int, s: int, arch: Arch, bn_train: bool,
-         depthwise: Optional[bool] = None) -> Tensor:
+         depthwise: Optional[bool] = None, residual: Optional[Tensor] = None) -> Tensor:
     """BaseConv or DWConv (network_blocks.py:55-74) depending on the preset."""
     dw = arch.depthwise if depthwise is None else depthwise
     if dw:
         c = x.shape[1]
         x = base_conv(sd, p + ".dconv", x, k, s, arch.act, arch.bn_eps, groups=c, bn_train=bn_train)
-        return base_conv(sd, p + ".pconv", x, 1, 1, arch.act, arch.bn_eps, bn_train=bn_train)
-    return base_conv(sd, p, x, k, s, arch.act, arch.bn_eps, bn_train=bn_train)
+        return base_conv(sd, p + ".pconv", x, 1, 1, arch.act, arch.bn_eps, bn_train=bn_train, residual=residual)
+    return base_conv(sd, p, x, k, s, arch.act, arch.bn_eps, bn_train=bn_train, residual=residual)
 
 
 def bottleneck(sd: SD, p: str, x: Tensor, shortcut: bool, arch: Arch, bn_train: bool) -> Tensor:
     """network_blocks.py:77-99 (expansion 1.0 inside CSP)."""
     y = base_conv(sd, p + ".conv1", x, 1, 1, arch.act, arch.bn_eps, bn_train=bn_train)
-    y = conv(sd, p + ".conv2", y, 3, 1, arch, bn_train)
-    if shortcut and x.shape[1] == y.shape[1]:
-        y = y + x
-    return y
+    add = shortcut and x.shape[1] == sd[p + ".conv2" + (".pconv" if arch.depthwise else "") + ".conv.weight"].shape[0]
+    return conv(sd, p + ".conv2", y, 3, 1, arch, bn_train, residual=x if add else None)
 
 
 def csp(sd: SD, p: str, x: Tensor, n: int, shortcut: bool, arch: Arch, bn_train: bool) -> Tensor:
@@ -166,9 +199,9 @@ def head_raw(sd: SD, arch: Arch, feats, bn_train: bool = False):
         c = conv(sd, f"{h}.cls_convs.{k}.1", c, 3, 1, arch, bn_train)
         r = conv(sd, f"{h}.reg_convs.{k}.0", x, 3, 1, arch, bn_train)
         r = conv(sd, f"{h}.reg_convs.{k}.1", r, 3, 1, arch, bn_train)
-        cls = F.conv2d(c, sd[f"{h}.cls_preds.{k}.weight"], sd[f"{h}.cls_preds.{k}.bias"])
-        reg = F.conv2d(r, sd[f"{h}.reg_preds.{k}.weight"], sd[f"{h}.reg_preds.{k}.bias"])
-        obj = F.conv2d(r, sd[f"{h}.obj_preds.{k}.weight"], sd[f"{h}.obj_preds.{k}.bias"])
+        cls = F.conv2d(c, _rnd(sd[f"{h}.cls_preds.{k}.weight"]), sd[f"{h}.cls_preds.{k}.bias"])
+        reg = F.conv2d(r, _rnd(sd[f"{h}.reg_preds.{k}.weight"]), sd[f"{h}.reg_preds.{k}.bias"])
+        obj = F.conv2d(r, _rnd(sd[f"{h}.obj_preds.{k}.weight"]), sd[f"{h}.obj_preds.{k}.bias"])
         outs.append((reg, obj, cls))
     return outs
 

@@ -1,9 +1,10 @@
 """Parity at the BASELINE.json workloads themselves (not scaled-down stand-ins).
 
 configs[1]  yolox_s 640 bf16 batch 32: the autotuned, graph-captured plan bench.py
-            times; images 0 and 31 vs the oracle's fp32 forward (DESIGN.md §7 bf16
-            bounds), device NMS on the whole replayed batch bit-exact vs the oracle's
-            NMS on the same output.
+            times; all 32 images vs the oracle's fp32 forward, within bounds derived from
+            the oracle itself run with bf16 storage (weights and every stored map rounded,
+            oracle.stored_as: DESIGN.md §7), device NMS on the whole replayed batch
+            bit-exact vs the oracle's NMS on the same output.
 configs[2]  yolox_s 640 train step batch 8 in fp32 (the reference's default precision):
             the six loss values and every parameter gradient within 1e-3 of the
             oracle's autograd (north_star tolerance).
@@ -12,7 +13,7 @@ configs[0]  yolox_tiny 416 single image through Yolox.from_pretrained (a local c
             (processor_yolox_tiny_416.npz; the reference test's bars) and == the oracle NMS +
             formatting on the same device output.
 configs[3]  yolox_l 640 fp16 batch 16 (bench plan): all 16 images vs the oracle's fp32 forward
-            (fp16 bounds) and device NMS on the whole batch bit-exact vs the oracle's NMS on the
+            (bounds derived from the oracle with fp16 storage) and device NMS on the whole batch bit-exact vs the oracle's NMS on the
             same output.
 configs[4]  yolox_x 1280 --fp16 train: on-device SimOTA at A = 33600 anchors with up to
             120 GTs exact vs the oracle (fg mask, matched GT, num_fg; IoUs to fp32
@@ -38,13 +39,30 @@ def probs_close(out, ref, pmax, p99, xy):
     assert np.abs(out[..., :2] - ref[..., :2]).max() < xy
 
 
-def oracle_forward(oracle, name, images_u8):
+def oracle_forward(oracle, name, images_u8, stored=None):
+    """The oracle's fp32 forward, or (stored = bf16 / f16) the same with the device's storage
+    precision emulated (oracle.stored_as)."""
     from yolox_amd.config import named_config
     from yolox_amd.weights import synthetic_state_dict
     sd = synthetic_state_dict(named_config(name).get_model().state_dict(), seed=0, bn_stats=name)
     x = torch.from_numpy(oracle.letterbox_identity(images_u8))
-    with torch.no_grad():
+    with torch.no_grad(), oracle.stored_as(stored):
         return oracle.forward_eval(sd, oracle.ARCHS[name], x).numpy()
+
+
+def derived_bounds_hold(dev, ref, emu, factor):
+    """dev (device, 16-bit) vs ref (oracle fp32) within ``factor`` x the distance of emu (the
+    oracle with 16-bit storage) from ref: max and p99 of the probabilities, max of the box
+    centres -- a faithful 16-bit implementation differs from emu only in summation order."""
+    stats = {}
+    for name, sl in (("prob", np.s_[..., 4:]), ("xy", np.s_[..., :2])):
+        d_dev, d_emu = np.abs(dev[sl] - ref[sl]), np.abs(emu[sl] - ref[sl])
+        stats[name] = (float(d_dev.max()), float(d_emu.max()), float(np.quantile(d_dev, 0.99)),
+                       float(np.quantile(d_emu, 0.99)))
+    pm, pe, p99m, p99e = stats["prob"]
+    assert pm <= factor * pe and p99m <= factor * p99e, stats
+    assert stats["xy"][0] <= factor * stats["xy"][1] + 0.25, stats
+    return stats
 
 
 def bench_plan(name, batch, size, dtype):
@@ -69,9 +87,12 @@ def test_configs1_yolox_s_640_bf16_batch32(oracle):
     torch.cuda.synchronize()
     assert torch.equal(out, out2)  # replays are deterministic
     host = out.cpu().numpy()
-    ref = oracle_forward(oracle, "yolox_s", imgs[[0, 31]])
-    for got, want in zip(host[[0, 31]], ref):
-        probs_close(got, want, 0.2, 0.06, 2.0)
+    # all 32 images; the factor (1.5) leaves room for the summation order only: measured on
+    # MI355X the device sits at 0.6-1.0x the emulated bf16 distance (stats printed with -s)
+    ref = oracle_forward(oracle, "yolox_s", imgs)
+    emu = oracle_forward(oracle, "yolox_s", imgs, torch.bfloat16)
+    print("configs1 bf16 vs fp32 oracle (dev max, emu max, dev p99, emu p99):",
+          derived_bounds_hold(host, ref, emu, 1.5))
     # device NMS (bench step: conf 0.5, nms 0.65) on the replayed output == oracle NMS
     pred = out.clone()
     det, counts = postprocess_device(pred, 80, 0.5, 0.65)
@@ -154,8 +175,9 @@ def test_configs3_yolox_l_640_fp16_batch16(oracle):
     host = out.cpu().numpy()
     torch.set_num_threads(16)
     ref = oracle_forward(oracle, "yolox_l", imgs)
-    for got, want in zip(host, ref):
-        probs_close(got, want, 0.05, 0.01, 0.5)
+    emu = oracle_forward(oracle, "yolox_l", imgs, torch.float16)
+    print("configs3 fp16 vs fp32 oracle (dev max, emu max, dev p99, emu p99):",
+          derived_bounds_hold(host, ref, emu, 1.5))
     # device NMS (processor defaults conf 0.5, nms 0.65) on the replayed fp16-plan output
     pred = out.clone()
     det, counts = postprocess_device(pred, 80, 0.5, 0.65)

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ -n "$TESTS" ]; then
-  eval timeout -k 10 400 python -u -m pytest $TESTS -m gpu -x -q --timeout 200 --timeout-method thread \
+  eval timeout -k 10 400 python -u -m pytest $TESTS -m gpu -x -q -s --timeout 200 --timeout-method thread \
       > gpurun_out/tests_$TAG.log 2>&1; rc=$?
   tail -4 gpurun_out/tests_$TAG.log
   [ $rc -eq 0 ] || { grep -E "^E |Error" gpurun_out/tests_$TAG.log | head -20; exit $rc; }

@@ -1,0 +1,28 @@
+#!/bin/bash
+# GPU box: evidence for one bench configuration -- bench (+ per-layer table, tune file), rocprofv3
+# kernel trace + stats of the same bench, PMC HBM traffic (FETCH_SIZE / WRITE_SIZE in separate
+# passes, MI355X_MICROARCH.md HBM section) and an SQ / GRBM pass for MFMA utilisation per kernel.
+# Usage: bash tools/gpu_profile.sh TAG [bench args...]   (e.g. --model yolox_l --batch 16 --dtype fp16)
+set -o pipefail
+TAG=${1:-run}
+shift
+ARGS="$*"
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TUNE=gpurun_out/tune_$TAG.json
+timeout -k 10 300 python bench.py $ARGS --layers --tune-file $TUNE > gpurun_out/bench_$TAG.json \
+    2> gpurun_out/bench_$TAG.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
+    -- python bench.py $ARGS --steps 10 --warmup 3 --no-cpu-baseline --tune-file $TUNE \
+    > gpurun_out/prof_$TAG.log 2>&1 || exit 1
+for CNT in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 120 rocprofv3 --pmc $CNT -d gpurun_out/pmc_${TAG}_$CNT -o run --output-format csv \
+      -- python bench.py $ARGS --steps 4 --warmup 1 --no-cpu-baseline --tune-file $TUNE \
+      > gpurun_out/pmc_${TAG}_$CNT.log 2>&1 || exit 1
+done
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE \
+    -d gpurun_out/pmc_${TAG}_SQ -o run --output-format csv \
+    -- python bench.py $ARGS --steps 4 --warmup 1 --no-cpu-baseline --tune-file $TUNE \
+    > gpurun_out/pmc_${TAG}_SQ.log 2>&1 || exit 1
+echo "profile $TAG done"

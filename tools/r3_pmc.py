@@ -1,5 +1,5 @@
 """One 3x3 conv shape of yolox_s bs32 launched 50x with a fixed tile, for rocprofv3 --pmc
-passes (tools/gpu_r3pmc.sh).  Usage: python tools/r3_pmc.py S H CIN COUT TILE"""
+passes (a --pmc run of tools/r3_probe.py; round-3 script retired).  Usage: python tools/r3_pmc.py S H CIN COUT TILE"""
 import ctypes as C
 import os
 import sys

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Aggregate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh)
+"""Aggregate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/gpu_profile.sh)
 into HBM bytes per forward of the bench workload -> profiles/traffic_<tag>.json.
 
 Units and the gfx950 correction follow /opt/skills/guides/MI355X_MICROARCH.md (HBM):
