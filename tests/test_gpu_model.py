@@ -140,8 +140,11 @@ def test_fused_bottleneck_plan_matches_split_plan(golden):
     d = golden("fwd_yolox_s_128.npz")
     m = model("yolox_s", torch.bfloat16)
     x = torch.from_numpy(d["input_u8"]).cuda()
-    fused = Plan(m, 2, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8, fuse_bottleneck=True)
-    split = Plan(m, 2, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8, fuse_bottleneck=False)
+    # (the round-4 1x1 folds off in both, so the op counts isolate the Bottleneck fusion)
+    fused = Plan(m, 2, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8, fuse_bottleneck=True,
+                 csp_fusion=False)
+    split = Plan(m, 2, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8, fuse_bottleneck=False,
+                 csp_fusion=False)
     n_pre = sum(1 for o in fused.ctx.ops if o.args.get("pre_spec") is not None)
     assert n_pre == 1 + 3 + 3 + 1 + 1 + 1  # dark2, dark3, dark4, C3_p4, C3_p3, C3_n3 (C = 32/64/128)
     assert len(fused.ctx.ops) == len(split.ctx.ops) - n_pre
