@@ -64,16 +64,17 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     // channels by LDS-DMA with the halo, one 16-byte pad slot per pixel row, a ring of three
     // (the epilogue of tile k-1 runs during tile k while tile k+1 lands)
     // Post conv (PGN > 0, yxh_conv_desc.post_weight): the tile's output Y stays in LDS in the
-    // residual slot layout (a ring of two slots, the residual DMA'd in and Y written over it
-    // in place) and Z = SiLU(W2 . [Y | X2] + b2) of PGN channels leaves instead, X2 = PGC
-    // channels of post_src DMA'd per tile (ring of two)
+    // residual slot layout (ring slot = tile % 3: the residual DMA'd in at the tile's own step,
+    // Y written over it in place by the epilogue pieces riding the next tile's MFMAs) and
+    // Z = SiLU(W2 . [Y | X2] + b2) of PGN channels leaves instead, computed in pieces riding
+    // the MFMAs of the tile after that; X2 = PGC channels of post_src DMA'd per tile (ring of 3)
     // Head form (PGH > 0 class fragments; YXH_CONV_GROUPS2): the same Y ring, and instead of a
     // bf16 post conv each group's block runs its level's preds over Y (group 0: PGH x 16 class
     // rows, group 1: the 5 reg | obj rows; weights in LDS) into decoded fp32 [B, A, 5 + C] rows
     constexpr bool PG = PGN > 0, HP = PGH > 0, PGY = PG || HP;
     constexpr int RS = TN / 8 + 1, RSLOTS = (S == 1 || PGY) ? TM * RS : 0;
     constexpr int RLOADS = (RSLOTS + 63) / 64, GR = (RLOADS + NW - 1) / NW, RTB = RLOADS * 1024;
-    constexpr int NRING = PGY ? 2 : 3;
+    constexpr int NRING = 3;
     constexpr int XS = PGC / 8 + 1, XSLOTS = PG && PGC > 0 ? TM * XS : 0;
     constexpr int XLOADS = (XSLOTS + 63) / 64, GX = (XLOADS + NW - 1) / NW, XTB = XLOADS * 1024;
     constexpr int K2 = TN + PGC, KB2 = K2 / 32;
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     // 32 (w % NG) .. +32 of every R-th 16-pixel halo fragment
     constexpr int NG = CIN / 32, R1 = NW / NG, NPA = (HY * HXP + 15) / 16;
     constexpr int XOFF = 2 * HBYTES + RBYTES + NRING * RTB;
-    constexpr int TOFF = XOFF + 2 * XTB;
+    constexpr int TOFF = XOFF + 3 * XTB;
     constexpr int HWOFF = TOFF + (F1 ? HBYTES : 0);
     constexpr int SMEM = HWOFF + HBYTES_W;
     static_assert(!F1 || (S == 1 && NW % NG == 0), "fused Bottleneck tile");
@@ -343,89 +344,81 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             for (int i = 0; i < FR; ++i) epi_piece(e, ap, o, i);
     };
 
-    // post conv of a finished tile whose Y is complete in ring slot k % 2 (and X2 landed):
-    // Z = SiLU(W2 . [Y | X2] + b2), 8-byte stores of 4 channels through a buffer descriptor
-    auto pg_tile = [&](const TileC c, const int k) {
+    // Post work of a finished tile whose Y is complete in ring slot k % 3 (and X2 landed), as
+    // independent pieces -- one 16-pixel fragment x one 16-row output fragment each -- that ride
+    // the MFMA loop two tiles later (or run at the end):
+    //  * PG: Z = SiLU(W2 . [Y | X2] + b2) (W2 stationary in VGPRs), 8-byte bf16 stores;
+    //  * HP: the level's preds over Y (weights in LDS) decoded as head.hip's head_pred (same
+    //    MFMA order, hardware exp2 / rcp), dword stores of the fp32 rows
+    struct PostCtx { __amdgpu_buffer_rsrc_t srd; const char* ys; const char* xs; TileC c; };
+    auto post_ctx = [&](const TileC c, const int k) -> PostCtx {
+        PostCtx q;
+        q.c = c;
+        q.ys = smem + 2 * HBYTES + RBYTES + (k % NRING) * RTB;
+        q.xs = smem + XOFF + (k % 3) * XTB;
+        const int es = HP ? 4 : 2;
+        q.srd = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)p.pgd + (long long)c.b * p.pgd_bs * es), (short)0,
+                                                  (int)((long long)ohw * p.pgd_cs * es), 0x00020000);
+        return q;
+    };
+    constexpr int HPF = (TM / 16 + NW - 1) / NW;  // HP: pixel fragments per wave
+    constexpr int NPU = PG ? PF2 * NF2 : HP ? HPF * PGH : 0;  // post pieces per wave per tile
+    auto post_piece = [&](const PostCtx& q, const int u) {
         if constexpr (PG) {
-            const char* ys = smem + 2 * HBYTES + RBYTES + (k & 1) * RTB;
-            const char* xs = smem + XOFF + (k & 1) * XTB;
-            const __amdgpu_buffer_rsrc_t zsrd = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)((T*)p.pgd + (long long)c.b * p.pgd_bs), (short)0, (int)((long long)ohw * p.pgd_cs * 2),
-                0x00020000);
+            const int pf = u / NF2, f = u - NF2 * (u / NF2);
+            const int pl = (wm2 * PF2 + pf) * 16 + frow;
+            f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int pf = 0; pf < PF2; ++pf) {
-                const int pl = (wm2 * PF2 + pf) * 16 + frow;
-                f32x4 z[NF2];
+            for (int kb = 0; kb < KB2; ++kb) {
+                const uint4 bv = kb < TN / 32 ? *(const uint4*)(q.ys + (pl * RS + kb * 4 + fq) * 16)
+                                              : *(const uint4*)(q.xs + (pl * XS + (kb - TN / 32) * 4 + fq) * 16);
+                Mma<T>::run(z, a2[f][kb], bv);
+            }
+            const int ty = pl / TX, tx = pl - ty * TX;
+            const int oy = q.c.oy0 + ty, ox = q.c.ox0 + tx;
+            const int n = (wn2 * NF2 + f) * 16 + fq * 4;
+            T t[4];
 #pragma unroll
-                for (int f = 0; f < NF2; ++f) z[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int r = 0; r < 4; ++r) t[r] = from_f32<T>(yxh::silu<false>(z[r] + b2[f][r]));
+            u32x2 uv;
+            __builtin_memcpy(&uv, t, 8);
+            const int od = oy < OH && ox < OW ? ((oy * OW + ox) * p.pgd_cs + n) * 2 : (int)dma::kOob;
+            __builtin_amdgcn_raw_buffer_store_b64(uv, q.srd, od, 0, 0);
+        } else if constexpr (HP) {
+            const int pf = wave + NW * (u / PGH), f = u - PGH * (u / PGH);
+            if (pf >= TM / 16 || f >= (hgrp1 ? 1 : PGH)) return;  // wave-uniform
+            const char* wl = smem + HWOFF;
+            const float* bl = (const float*)(wl + HROWS * RS * 16);
+            const int pl = pf * 16 + frow;
+            f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int kb = 0; kb < KB2; ++kb) {
-                    const uint4 bv = kb < TN / 32 ? *(const uint4*)(ys + (pl * RS + kb * 4 + fq) * 16)
-                                                  : *(const uint4*)(xs + (pl * XS + (kb - TN / 32) * 4 + fq) * 16);
+            for (int kb = 0; kb < TN / 32; ++kb)
+                Mma<T>::run(z, *(const uint4*)(wl + ((f * 16 + frow) * RS + kb * 4 + fq) * 16),
+                            *(const uint4*)(q.ys + (pl * RS + kb * 4 + fq) * 16));
+            const int ty = pl / TX, tx = pl - ty * TX;
+            const int oy = q.c.oy0 + ty, ox = q.c.ox0 + tx;
+            const bool okp = oy < OH && ox < OW;
+            const int rowo = (oy * OW + ox) * p.pgd_cs + (hgrp1 ? 0 : 5);
+            const float st = p.pg_stride;
 #pragma unroll
-                    for (int f = 0; f < NF2; ++f) Mma<T>::run(z[f], a2[f][kb], bv);
+            for (int r = 0; r < 4; ++r) {
+                const int ch = f * 16 + fq * 4 + r;
+                float v = z[r] + bl[ch];
+                if (hgrp1) {
+                    if (ch < 2) v = (v + (float)(ch == 0 ? ox : oy)) * st;
+                    else if (ch < 4) v = __builtin_amdgcn_exp2f(v * 1.4426950408889634f) * st;
+                    else v = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
+                } else {
+                    v = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
                 }
-                const int ty = pl / TX, tx = pl - ty * TX;
-                const int oy = c.oy0 + ty, ox = c.ox0 + tx;
-                const bool ok = oy < OH && ox < OW;
-#pragma unroll
-                for (int f = 0; f < NF2; ++f) {
-                    const int n = (wn2 * NF2 + f) * 16 + fq * 4;
-                    T t[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) t[q] = from_f32<T>(yxh::silu<false>(z[f][q] + b2[f][q]));
-                    u32x2 u;
-                    __builtin_memcpy(&u, t, 8);
-                    const int od = ok ? ((oy * OW + ox) * p.pgd_cs + n) * 2 : (int)dma::kOob;
-                    __builtin_amdgcn_raw_buffer_store_b64(u, zsrd, od, 0, 0);
-                }
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), q.srd,
+                                                      okp && ch < hrows ? (rowo + ch) * 4 : (int)dma::kOob, 0, 0);
             }
         }
     };
-
-    // head form: the preds of a finished tile (Y complete in ring slot k % 2), decoded, as
-    // head.hip's head_pred (same MFMA order and exp / sigmoid), dword stores of fp32 rows
-    auto hp_tile = [&](const TileC c, const int k) {
-        if constexpr (HP) {
-            const char* ys = smem + 2 * HBYTES + RBYTES + (k & 1) * RTB;
-            const char* wl = smem + HWOFF;
-            const float* bl = (const float*)(wl + HROWS * RS * 16);
-            const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)((float*)p.pgd + (long long)c.b * p.pgd_bs), (short)0, (int)((long long)ohw * p.pgd_cs * 4),
-                0x00020000);
-            const int nf = hgrp1 ? 1 : PGH;
-            const int col0 = hgrp1 ? 0 : 5;
-            const float st = p.pg_stride;
-            for (int pf = wave; pf < TM / 16; pf += NW) {
-                const int pl = pf * 16 + frow;
-                const int ty = pl / TX, tx = pl - ty * TX;
-                const int oy = c.oy0 + ty, ox = c.ox0 + tx;
-                const bool okp = oy < OH && ox < OW;
-                const int rowo = (oy * OW + ox) * p.pgd_cs;
-                for (int f = 0; f < nf; ++f) {  // one 16-row fragment at a time (few live registers)
-                    f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto post_all = [&](const PostCtx& q) {
 #pragma unroll
-                    for (int kb = 0; kb < TN / 32; ++kb)
-                        Mma<T>::run(z, *(const uint4*)(wl + ((f * 16 + frow) * RS + kb * 4 + fq) * 16),
-                                    *(const uint4*)(ys + (pl * RS + kb * 4 + fq) * 16));
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int ch = f * 16 + fq * 4 + r;
-                        float v = z[r] + bl[ch];
-                        if (hgrp1) {
-                            if (ch < 2) v = (v + (float)(ch == 0 ? ox : oy)) * st;
-                            else if (ch < 4) v = __builtin_amdgcn_exp2f(v * 1.4426950408889634f) * st;
-                            else v = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
-                        } else {
-                            v = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
-                        }
-                        const bool ok = okp && ch < hrows;
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), osrd,
-                                                              ok ? (rowo + col0 + ch) * 4 : (int)dma::kOob, 0, 0);
-                    }
-                }
-            }
-        }
+        for (int u = 0; u < NPU; ++u) post_piece(q, u);
     };
 
     f32x4 accp[FR][FCO];  // owned fragments of the previous tile, waiting for their epilogue
@@ -435,8 +428,9 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     // one tile: wait for its halo, start tile k+1's halo (+ residual), MMA of tile k with the
     // epilogue of tile k-1 spread over it, then the K-split reduce of tile k into accp
     auto tile_step = [&](const TileC cur, const int tile, const int k, TileC& cnext, const TileC prev,
-                         auto epi) -> int {
+                         const TileC prev2, auto epi, auto post) -> int {
         constexpr bool EPI = decltype(epi)::value;
+        constexpr bool POST = decltype(post)::value && PGY;
         const int kb = k & 1;
         const int next = tile + nwork;
         dma::wait_vm<0>();
@@ -448,9 +442,9 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
                 if (!PGY && has_res) issue_res(cnext, (k + 1) % 3);
             }
         }
-        if constexpr (PGY) {  // this tile's residual / X2: read one step later (ring of two)
-            if (has_res) issue_res(cur, k & 1);
-            issue_x2(cur, k & 1);
+        if constexpr (PGY) {  // this tile's residual / X2 (ring slot k % 3: its post runs two steps on)
+            if (has_res) issue_res(cur, k % 3);
+            issue_x2(cur, k % 3);
         }
 
         if constexpr (F1) {
@@ -508,6 +502,8 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);
         EpiCtx e{};
         if constexpr (EPI) e = epi_ctx(prev, k - 1);
+        PostCtx pc{};
+        if constexpr (POST) pc = post_ctx(prev2, k - 2);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             if (s + 1 < NS) load_b(s + 1, bf[(s + 1) & 1]);
@@ -519,6 +515,9 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             // piece s of the previous tile's epilogue rides on this step's MFMAs
             if constexpr (EPI)
                 if (s < NP) epi_piece(e, accp, s / FR, s % FR);
+            // ... and piece s of the post work of the tile before that
+            if constexpr (POST)
+                if (s < NPU) post_piece(pc, s);
             // keep the one-step-ahead read distance (the scheduler would otherwise pull each
             // read down next to its first MFMA) and put two VALU ops in each MFMA's shadow
             if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);  // DS reads
@@ -531,6 +530,9 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         if constexpr (EPI)
 #pragma unroll
             for (int q = NS; q < NP; ++q) epi_piece(e, accp, q / FR, q % FR);
+        if constexpr (POST)
+#pragma unroll
+            for (int u = NS; u < NPU; ++u) post_piece(pc, u);
 
         // ---- K-split: partial sums of the fragments other waves finish go through LDS
         if constexpr (WK > 1) {
@@ -564,35 +566,34 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 #pragma unroll
                 for (int j = 0; j < FC; ++j) accp[i][j] = acc[i][j];
         }
-        if constexpr (PGY && EPI) {  // the previous tile's Y is complete in LDS: its post conv
-            dma::barrier();
-            if constexpr (PG) pg_tile(prev, k - 1);
-            else hp_tile(prev, k - 1);
-        }
         return next;
     };
 
-    TileC cur = coords(tile), cnext{0, 0, 0};
+    TileC cur = coords(tile), cnext{0, 0, 0}, prev{0, 0, 0}, prev2{0, 0, 0};
     issue_halo(cur, 0);
     if (!PGY && has_res) issue_res(cur, 0);
     // the first tile is peeled off the loop: it consumes the weight loads, so the loop body
     // carries no compiler-visible pending load whose wait would also drain the halo DMA
-    int next = tile_step(cur, tile, 0, cnext, cur, std::false_type{});
+    int next = tile_step(cur, tile, 0, cnext, cur, cur, std::false_type{}, std::false_type{});
     int k = 1;
     for (; next < ntiles; ++k) {
-        const TileC prev = cur;
+        prev2 = prev;
+        prev = cur;
         cur = cnext;
-        next = tile_step(cur, next, k, cnext, prev, std::true_type{});
+        if (PGY && k >= 2)  // the post pieces of tile k - 2 ride this tile's MFMAs
+            next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::integral_constant<bool, PGY>{});
+        else
+            next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::false_type{});
     }
-    if constexpr (PGY) {  // the last tile's residual / X2 were issued in its own step
+    if constexpr (PGY) {  // the last tile's residual / X2 landed, the tile before it has its Y
         dma::wait_vm<0>();
         dma::barrier();
+        if (k >= 2) post_all(post_ctx(prev, k - 2));
     }
     epilogue(cur, k - 1, accp);
     if constexpr (PGY) {
         dma::barrier();
-        if constexpr (PG) pg_tile(cur, k - 1);
-        else hp_tile(cur, k - 1);
+        post_all(post_ctx(cur, k - 1));
     }
     (void)ohw;
 }
@@ -700,10 +701,10 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         // 1x1 post conv (ids 41-48 = tiles 221-228): dark2's Bottleneck 3x3 32 -> 32 + CspLayer.conv3
         // over [y | x_2] (64 -> 64); the 64 -> 64 3x3s of dark3's last Bottleneck / C3_p3 + conv3 over
         // [y | x_2] (128 -> 128); dark3[0] (3x3 s2 64 -> 128) + CspLayer conv1 | conv2 (128 -> 128)
-        case 41: return launch_ws<T, 32, 1, 16, 8, 32, 1, 1, 4, 2, false, 64, 32>(p, st);
-        case 42: return launch_ws<T, 32, 1, 16, 8, 32, 1, 1, 4, 1, false, 64, 32>(p, st);
+        case 41: return launch_ws<T, 32, 1, 16, 8, 32, 1, 1, 4, 1, false, 64, 32>(p, st);
+        case 42: return launch_ws<T, 32, 1, 16, 4, 32, 1, 1, 4, 2, false, 64, 32>(p, st);
         case 43: return launch_ws<T, 64, 1, 16, 4, 64, 2, 1, 2, 1, false, 128, 64>(p, st);
-        case 44: return launch_ws<T, 64, 1, 16, 8, 64, 2, 1, 2, 1, false, 128, 64>(p, st);
+        case 44: return launch_ws<T, 64, 1, 8, 4, 64, 2, 2, 1, 2, false, 128, 64>(p, st);
         case 45: return launch_ws<T, 64, 2, 16, 2, 128, 4, 1, 1, 1, false, 128, 0>(p, st);
         case 46: return launch_ws<T, 64, 2, 16, 4, 128, 4, 1, 1, 1, false, 128, 0>(p, st);
         // K split over two waves: half the stationary weights per wave, so two blocks per CU
@@ -711,11 +712,11 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 47: return launch_ws<T, 64, 1, 16, 2, 64, 2, 2, 1, 2, false, 128, 64>(p, st);
         case 48: return launch_ws<T, 64, 1, 16, 4, 64, 2, 2, 1, 1, false, 128, 64>(p, st);
         case 49: return launch_ws<T, 64, 2, 16, 2, 128, 4, 2, 1, 1, false, 128, 0>(p, st);
-        case 50: return launch_ws<T, 64, 2, 16, 4, 128, 4, 2, 1, 1, false, 128, 0>(p, st);
+        case 50: return launch_ws<T, 64, 2, 8, 4, 128, 4, 2, 1, 1, false, 128, 0>(p, st);
         // head form (ids 51-53 = tiles 231-233): a level's cls_convs[k][1] | reg_convs[k][1] with
         // each group's preds + decode (yolo_head.py:149-251) in the same launch
         case 51: return launch_ws<T, 128, 1, 16, 4, 128, 4, 1, 1, 1, false, 0, 0, 5>(p, st);
-        case 52: return launch_ws<T, 128, 1, 8, 4, 128, 4, 2, 1, 1, false, 0, 0, 5>(p, st);
+        // (id 52, the eight-wave K-split head form, spilled once its post pieces rode the MFMA loop)
         case 53: return launch_ws<T, 128, 1, 16, 2, 128, 4, 1, 1, 1, false, 0, 0, 5>(p, st);
         default: set_error("conv_ws tile id %d", id); return YXH_EINVAL;
     }
