@@ -94,6 +94,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     constexpr int SMEM = HWOFF + HBYTES_W;
     static_assert(!F1 || (S == 1 && NW % NG == 0), "fused Bottleneck tile");
     constexpr int FCO = (FC + WK - 1) / WK;  // pixel fragments this wave finishes
+    constexpr int PD = FR * FC >= 8 ? 1 : FR * FC >= 4 ? 2 : 3;  // fragment-read distance in K steps
     static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0 && TM % (16 * WM) == 0, "tile");
     // weights must stay in VGPRs: 160 of 256 (2 waves per SIMD), 288 of 512 (one 4-wave block per CU)
     static_assert(FR * 9 * WCB * 4 <= (NW == 4 && BPC == 1 ? 288 : 160), "weights must stay in VGPRs");
@@ -113,71 +114,6 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     const int cin_ = p.cin, cout = p.cout, in_w = p.in_w, in_h = p.in_h, scs = p.scs[0];
     const int OH = p.out_h, OW = p.out_w, ohw = p.ohw;
     (void)cin_;
-
-    // ---- stationary weights: a[i][tap][c] = 16 channels x 32 K of fragment i
-    uint4 a[FR][9][WCB];
-#pragma unroll
-    for (int i = 0; i < FR; ++i)
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-            for (int c = 0; c < WCB; ++c)
-                a[i][tap][c] = ws_weight<T>(p, n0 + wn * WTN + i * 16, tap, 9, CIN, wk * WCB + c, lane);
-    float bias[FR][4];
-#pragma unroll
-    for (int i = 0; i < FR; ++i) {
-        const int n = n0 + wn * WTN + i * 16 + fq * 4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bias[i][r] = n + r < cout ? p.bias[n + r] : 0.0f;
-    }
-
-    uint4 a1[F1 ? 2 : 1][F1 ? NG : 1];
-    float b1[2][4];
-    if constexpr (F1) {
-        const T* w1 = (const T*)p.pw1;
-        const int g = wave % NG;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-#pragma unroll
-            for (int cb = 0; cb < NG; ++cb)
-                a1[i][cb] = *(const uint4*)(w1 + (g * 32 + i * 16 + frow) * CIN + cb * 32 + fq * 8);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) b1[i][r] = p.pb1[g * 32 + i * 16 + fq * 4 + r];
-        }
-    }
-
-    // post conv weights, stationary: wave w owns Z channels (w % WN2) * NF2 * 16 .. + NF2 * 16 and
-    // pixel fragments (w / WN2) * PF2 .. + PF2 of the tile
-    const int wn2 = wave % WN2, wm2 = wave / WN2;
-    uint4 a2[PG ? NF2 : 1][PG ? KB2 : 1];
-    float b2[PG ? NF2 : 1][4];
-    if constexpr (PG) {
-        const T* w2 = (const T*)p.pgw;
-#pragma unroll
-        for (int f = 0; f < NF2; ++f) {
-            const int n = (wn2 * NF2 + f) * 16;
-#pragma unroll
-            for (int kb = 0; kb < KB2; ++kb) a2[f][kb] = *(const uint4*)(w2 + (long long)(n + frow) * K2 + kb * 32 + fq * 8);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) b2[f][r] = p.pgb[n + fq * 4 + r];
-        }
-    }
-
-    // head form: this block's group's pred weights [rows][TN] (rows of RS 16-byte slots) and
-    // biases -> LDS once; rows past the group's count are zero (visible after the first barrier)
-    const bool hgrp1 = HP && n0 >= cout / 2;
-    const int hrows = HP ? (hgrp1 ? p.pg_cout2 : p.pg_cout) : 0;
-    if constexpr (HP) {
-        const T* hw = (const T*)(hgrp1 ? p.pgw2 : p.pgw);
-        const float* hb = hgrp1 ? p.pgb2 : p.pgb;
-        char* wl = smem + HWOFF;
-        for (int q = tid; q < HROWS * (TN / 8); q += 64 * NW) {
-            const int r = q / (TN / 8), c = q - (TN / 8) * (q / (TN / 8));
-            *(uint4*)(wl + (r * RS + c) * 16) = r < hrows ? *(const uint4*)(hw + (long long)r * TN + c * 8)
-                                                          : make_uint4(0, 0, 0, 0);
-        }
-        for (int q = tid; q < HROWS; q += 64 * NW) ((float*)(wl + HROWS * RS * 16))[q] = q < hrows ? hb[q] : 0.0f;
-    }
 
     // ---- this lane's LDS byte offsets of its pixel fragments at tap (0, 0), channel block 0
     uint32_t boff[FC];
@@ -294,6 +230,72 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             }
         }
     };
+
+    // ---- prologue: this tile's halo (+ residual) and the next tile's go out first, then the
+    // weights behind them (the first tile waits only for the halos: see tile_step's FIRST)
+    TileC cur = coords(tile), cnext{0, 0, 0}, prev{0, 0, 0}, prev2{0, 0, 0};
+    issue_halo(cur, 0);
+    if (!PGY && has_res) issue_res(cur, 0);
+    if (tile + nwork < ntiles) {
+        cnext = coords(tile + nwork);
+        issue_halo(cnext, 1);
+        if (!PGY && has_res) issue_res(cnext, 1);
+    }
+
+    const bool hgrp1 = HP && n0 >= cout / 2;
+    const int hrows = HP ? (hgrp1 ? p.pg_cout2 : p.pg_cout) : 0;
+
+    uint4 a1[F1 ? 2 : 1][F1 ? NG : 1];
+    float b1[2][4];
+    if constexpr (F1) {
+        const T* w1 = (const T*)p.pw1;
+        const int g = wave % NG;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+            for (int cb = 0; cb < NG; ++cb)
+                a1[i][cb] = *(const uint4*)(w1 + (g * 32 + i * 16 + frow) * CIN + cb * 32 + fq * 8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) b1[i][r] = p.pb1[g * 32 + i * 16 + fq * 4 + r];
+        }
+    }
+
+    // ---- stationary weights: a[i][tap][c] = 16 channels x 32 K of fragment i, loaded in the
+    // order the first tile's K steps consume them (the compiler's per-use vmcnt waits then let
+    // that tile's MFMAs start while the rest of the weights are still arriving)
+    uint4 a[FR][9][WCB];
+#pragma unroll
+    for (int c = 0; c < WCB; ++c)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+                a[i][tap][c] = ws_weight<T>(p, n0 + wn * WTN + i * 16, tap, 9, CIN, wk * WCB + c, lane);
+    float bias[FR][4];
+#pragma unroll
+    for (int i = 0; i < FR; ++i) {
+        const int n = n0 + wn * WTN + i * 16 + fq * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[i][r] = n + r < cout ? p.bias[n + r] : 0.0f;
+    }
+
+
+    // post conv weights, stationary: wave w owns Z channels (w % WN2) * NF2 * 16 .. + NF2 * 16 and
+    // pixel fragments (w / WN2) * PF2 .. + PF2 of the tile
+    const int wn2 = wave % WN2, wm2 = wave / WN2;
+    uint4 a2[PG ? NF2 : 1][PG ? KB2 : 1];
+    float b2[PG ? NF2 : 1][4];
+    if constexpr (PG) {
+        const T* w2 = (const T*)p.pgw;
+#pragma unroll
+        for (int f = 0; f < NF2; ++f) {
+            const int n = (wn2 * NF2 + f) * 16;
+#pragma unroll
+            for (int kb = 0; kb < KB2; ++kb) a2[f][kb] = *(const uint4*)(w2 + (long long)(n + frow) * K2 + kb * 32 + fq * 8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) b2[f][r] = p.pgb[n + fq * 4 + r];
+        }
+    }
 
     // epilogue of a finished tile: bias, SiLU, residual (from the LDS staging slot), 8-byte
     // stores of 4 channels through a buffer descriptor (an invalid pixel / channel carries an
@@ -428,16 +430,20 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     // one tile: wait for its halo, start tile k+1's halo (+ residual), MMA of tile k with the
     // epilogue of tile k-1 spread over it, then the K-split reduce of tile k into accp
     auto tile_step = [&](const TileC cur, const int tile, const int k, TileC& cnext, const TileC prev,
-                         const TileC prev2, auto epi, auto post) -> int {
+                         const TileC prev2, auto epi, auto post, auto first) -> int {
         constexpr bool EPI = decltype(epi)::value;
         constexpr bool POST = decltype(post)::value && PGY;
+        constexpr bool FIRST = decltype(first)::value;
         const int kb = k & 1;
         const int next = tile + nwork;
-        dma::wait_vm<0>();
+        // FIRST: the halos (and residuals) went out before the weight loads, and vmcnt retires
+        // in issue order, so once no more than the weight loads are pending they have landed
+        if constexpr (FIRST) dma::wait_vm<(FR * 9 * WCB < 63 ? FR * 9 * WCB : 63)>();
+        else dma::wait_vm<0>();
         dma::barrier();
         if (next < ntiles) {
             cnext = coords(next);
-            if (!(YXH_WS_PROBE & 2)) {
+            if (!FIRST && !(YXH_WS_PROBE & 2)) {
                 issue_halo(cnext, kb ^ 1);
                 if (!PGY && has_res) issue_res(cnext, (k + 1) % 3);
             }
@@ -488,9 +494,11 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 #pragma unroll
             for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         const char* hb = F1 ? smem + TOFF : smem + kb * HBYTES;
-        // K steps s = (channel block c, tap); the pixel fragments of step s + 1 are read
-        // before the MFMAs of step s, so the LDS latency hides behind them
-        uint4 bf[2][FC];
+        // K steps s = (channel block c, tap); the pixel fragments of step s + PD are read
+        // before the MFMAs of step s, so the LDS latency hides behind PD steps of MFMAs (about
+        // 8 MFMAs: one 4-MFMA step does not cover an LDS read under load; measured, PD 1 -> 2:
+        // 80x80 128->128 76 -> 70 us, 40->20 s2 256->512 64 -> 57 us)
+        uint4 bf[PD + 1][FC];
         auto load_b = [&](int s, uint4 (&d)[FC]) {
             const int c = s / 9, tap = s - 9 * (s / 9);
             const int ky = tap / 3, kx = tap - 3 * (tap / 3);
@@ -498,20 +506,22 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 #pragma unroll
             for (int j = 0; j < FC; ++j) d[j] = *(const uint4*)(hb + boff[j] + so);
         };
-        load_b(0, bf[0]);
-        __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);
+#pragma unroll
+        for (int q = 0; q < PD; ++q)
+            if (q < NS) load_b(q, bf[q]);
+        __builtin_amdgcn_sched_group_barrier(0x100, FC * (PD < NS ? PD : NS), 0);
         EpiCtx e{};
         if constexpr (EPI) e = epi_ctx(prev, k - 1);
         PostCtx pc{};
         if constexpr (POST) pc = post_ctx(prev2, k - 2);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            if (s + 1 < NS) load_b(s + 1, bf[(s + 1) & 1]);
+            if (s + PD < NS) load_b(s + PD, bf[(s + PD) % (PD + 1)]);
             const int c = s / 9, tap = s - 9 * (s / 9);
 #pragma unroll
             for (int i = 0; i < FR; ++i)
 #pragma unroll
-                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], a[i][tap][c], bf[s & 1][j]);
+                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], a[i][tap][c], bf[s % (PD + 1)][j]);
             // piece s of the previous tile's epilogue rides on this step's MFMAs
             if constexpr (EPI)
                 if (s < NP) epi_piece(e, accp, s / FR, s % FR);
@@ -520,7 +530,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
                 if (s < NPU) post_piece(pc, s);
             // keep the one-step-ahead read distance (the scheduler would otherwise pull each
             // read down next to its first MFMA) and put two VALU ops in each MFMA's shadow
-            if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);  // DS reads
+            if (s + PD < NS) __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);  // DS reads
 #pragma unroll
             for (int m = 0; m < FR * FC; ++m) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -569,21 +579,33 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         return next;
     };
 
-    TileC cur = coords(tile), cnext{0, 0, 0}, prev{0, 0, 0}, prev2{0, 0, 0};
-    issue_halo(cur, 0);
-    if (!PGY && has_res) issue_res(cur, 0);
     // the first tile is peeled off the loop: it consumes the weight loads, so the loop body
     // carries no compiler-visible pending load whose wait would also drain the halo DMA
-    int next = tile_step(cur, tile, 0, cnext, cur, cur, std::false_type{}, std::false_type{});
+    int next = tile_step(cur, tile, 0, cnext, cur, cur, std::false_type{}, std::false_type{}, std::true_type{});
+    // head form: this block's group's pred weights [rows][TN] (rows of RS 16-byte slots) and
+    // biases -> LDS once, after the first tile (read from tile 2 on, behind tile 1's barriers);
+    // rows past the group's count are zero
+    if constexpr (HP) {
+        const T* hw = (const T*)(hgrp1 ? p.pgw2 : p.pgw);
+        const float* hb = hgrp1 ? p.pgb2 : p.pgb;
+        char* wl = smem + HWOFF;
+        for (int q = tid; q < HROWS * (TN / 8); q += 64 * NW) {
+            const int r = q / (TN / 8), c = q - (TN / 8) * (q / (TN / 8));
+            *(uint4*)(wl + (r * RS + c) * 16) = r < hrows ? *(const uint4*)(hw + (long long)r * TN + c * 8)
+                                                          : make_uint4(0, 0, 0, 0);
+        }
+        for (int q = tid; q < HROWS; q += 64 * NW) ((float*)(wl + HROWS * RS * 16))[q] = q < hrows ? hb[q] : 0.0f;
+    }
+
     int k = 1;
     for (; next < ntiles; ++k) {
         prev2 = prev;
         prev = cur;
         cur = cnext;
         if (PGY && k >= 2)  // the post pieces of tile k - 2 ride this tile's MFMAs
-            next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::integral_constant<bool, PGY>{});
+            next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::integral_constant<bool, PGY>{}, std::false_type{});
         else
-            next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::false_type{});
+            next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::false_type{}, std::false_type{});
     }
     if constexpr (PGY) {  // the last tile's residual / X2 landed, the tile before it has its Y
         dma::wait_vm<0>();

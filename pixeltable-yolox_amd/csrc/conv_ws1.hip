@@ -29,6 +29,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
     constexpr int RBYTES = WK > 1 ? WN * WM * FR * FC * (WK - 1) * 1024 : 0;
     constexpr int SMEM = 2 * HBYTES + RBYTES;
     constexpr int FCO = (FC + WK - 1) / WK;
+    constexpr int PD = FR * FC >= 8 ? 1 : FR * FC >= 4 ? 2 : 3;  // fragment-read distance in K steps
     static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0, "tile");
     static_assert(FR * WCB * 4 <= (NW == 4 && BPC == 1 ? 288 : 160), "weights must stay in VGPRs");
     static_assert(SMEM <= 160 * 1024, "LDS");
@@ -47,18 +48,6 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
     const int c0 = p.src0_ch, ncb0 = c0 / 32;
     const int c1 = CIN - c0;
 
-    uint4 a[FR][WCB];
-#pragma unroll
-    for (int i = 0; i < FR; ++i)
-#pragma unroll
-        for (int c = 0; c < WCB; ++c) a[i][c] = ws_weight<T>(p, n0 + wn * WTN + i * 16, 0, 1, CIN, wk * WCB + c, lane);
-    float bias[FR][4];
-#pragma unroll
-    for (int i = 0; i < FR; ++i) {
-        const int n = n0 + wn * WTN + i * 16 + fq * 4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bias[i][r] = n + r < cout ? p.bias[n + r] : 0.0f;
-    }
     uint32_t boff[FC];
 #pragma unroll
     for (int j = 0; j < FC; ++j) boff[j] = (uint32_t)(((wm * FC + j) * 16 + frow) * ps * 16 + fq * 16);
@@ -102,6 +91,23 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
         }
     };
 
+    // prologue: the first two tiles' rows go out before the weights, which then load in the
+    // order the first tile's K steps consume them (tile_step's FIRST waits for the rows only)
+    issue(tile, 0);
+    if (tile + nwork < ntiles) issue(tile + nwork, 1);
+    uint4 a[FR][WCB];
+#pragma unroll
+    for (int c = 0; c < WCB; ++c)
+#pragma unroll
+        for (int i = 0; i < FR; ++i) a[i][c] = ws_weight<T>(p, n0 + wn * WTN + i * 16, 0, 1, CIN, wk * WCB + c, lane);
+    float bias[FR][4];
+#pragma unroll
+    for (int i = 0; i < FR; ++i) {
+        const int n = n0 + wn * WTN + i * 16 + fq * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[i][r] = n + r < cout ? p.bias[n + r] : 0.0f;
+    }
+
     const bool silu = p.act == YXH_ACT_SILU;
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     const __amdgpu_buffer_rsrc_t dsrd =
@@ -125,13 +131,16 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
 
     f32x4 accp[FR][FCO];
     constexpr int NP = FR * FCO;
-    auto tile_step = [&](const int t, const int k, const int tprev, auto epi) -> int {
+    auto tile_step = [&](const int t, const int k, const int tprev, auto epi, auto first) -> int {
         constexpr bool EPI = decltype(epi)::value;
+        constexpr bool FIRST = decltype(first)::value;
         const int kb = k & 1;
         const int next = t + nwork;
-        dma::wait_vm<0>();
+        // FIRST: vmcnt retires in issue order and the rows went out before the weight loads
+        if constexpr (FIRST) dma::wait_vm<(FR * WCB < 63 ? FR * WCB : 63)>();
+        else dma::wait_vm<0>();
         dma::barrier();
-        if (next < ntiles) issue(next, kb ^ 1);
+        if (!FIRST && next < ntiles) issue(next, kb ^ 1);
 
         f32x4 acc[FR][FC];
 #pragma unroll
@@ -139,25 +148,28 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
 #pragma unroll
             for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         const char* hb = smem + kb * HBYTES;
-        uint4 bf[2][FC];
+        // pixel fragments read PD K steps ahead (conv_ws.hip: about 8 MFMAs of cover)
+        uint4 bf[PD + 1][FC];
         auto load_b = [&](int s, uint4 (&d)[FC]) {
             const int cg = wk * WCB + s;
             const int so = cg < ncb0 ? cg * 64 : l0 * 1024 + (cg - ncb0) * 64;
 #pragma unroll
             for (int j = 0; j < FC; ++j) d[j] = *(const uint4*)(hb + boff[j] + so);
         };
-        load_b(0, bf[0]);
-        __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);
+#pragma unroll
+        for (int q = 0; q < PD; ++q)
+            if (q < WCB) load_b(q, bf[q]);
+        __builtin_amdgcn_sched_group_barrier(0x100, FC * (PD < WCB ? PD : WCB), 0);
 #pragma unroll
         for (int s = 0; s < WCB; ++s) {
-            if (s + 1 < WCB) load_b(s + 1, bf[(s + 1) & 1]);
+            if (s + PD < WCB) load_b(s + PD, bf[(s + PD) % (PD + 1)]);
 #pragma unroll
             for (int i = 0; i < FR; ++i)
 #pragma unroll
-                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], a[i][s], bf[s & 1][j]);
+                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], a[i][s], bf[s % (PD + 1)][j]);
             if constexpr (EPI)
                 if (s < NP) epi_piece(tprev, accp, s / FR, s % FR);
-            if (s + 1 < WCB) __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);
+            if (s + PD < WCB) __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);
 #pragma unroll
             for (int m = 0; m < FR * FC; ++m) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -202,14 +214,13 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
         return next;
     };
 
-    issue(tile, 0);
     int cur = tile;
-    int next = tile_step(cur, 0, 0, std::false_type{});
+    int next = tile_step(cur, 0, 0, std::false_type{}, std::true_type{});
     int k = 1;
     for (; next < ntiles; ++k) {
         const int prev = cur;
         cur = next;
-        next = tile_step(cur, k, prev, std::true_type{});
+        next = tile_step(cur, k, prev, std::true_type{}, std::false_type{});
     }
 #pragma unroll
     for (int o = 0; o < FCO; ++o)
@@ -261,7 +272,7 @@ static int ws1_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 1: return launch_ws1<T, 64, 128, 64, 2, 1, 2, 2>(p, st);
         case 2: return launch_ws1<T, 64, 256, 64, 2, 1, 4, 1>(p, st);
         case 3: return launch_ws1<T, 128, 64, 128, 4, 1, 1, 2>(p, st);
-        case 4: return launch_ws1<T, 128, 128, 64, 2, 1, 2, 2>(p, st);
+        case 4: return launch_ws1<T, 128, 128, 64, 2, 1, 2, 1>(p, st);  // 80 KiB of LDS: one block per CU
         case 5: return launch_ws1<T, 256, 64, 128, 4, 1, 1, 2>(p, st);
         case 6: return launch_ws1<T, 256, 64, 64, 2, 1, 2, 2>(p, st);
         case 7: return launch_ws1<T, 512, 32, 128, 4, 1, 1, 1>(p, st);

@@ -556,14 +556,21 @@ class Plan:
                  input_layout: int = N.NCHW, input_dtype: torch.dtype = torch.float32, train: bool = False,
                  fuse_stem: bool = True, chunk: Optional[int] = None, fuse_bottleneck: bool = _FUSE_BOTTLENECK,
                  parallel_chunks: bool = False, fuse_stem_s2: bool = True, stage: str = "full",
-                 head_inputs: Optional[list] = None, csp_fusion: Optional[bool] = None):
+                 head_inputs: Optional[list] = None, csp_fusion: Optional[bool] = None, block=None):
         """``stage``: "full" (image -> decoded rows), "features" (image -> the three PAFPN
-        maps: YoloPafpn.forward) or "head" (three feature maps of ``head_inputs`` shapes
-        [(C, H, W)] -> decoded rows: YoloxHead.forward)."""
-        if stage not in ("full", "features", "head"):
+        maps: YoloPafpn.forward), "head" (three feature maps of ``head_inputs`` shapes
+        [(C, H, W)] -> decoded rows: YoloxHead.forward) or "block" (one building block of the
+        module tree -- ``block.plan_block`` -- over one NCHW map of ``head_inputs[0]``'s shape, or
+        over the image when ``block.takes_image``: the blocks' standalone forward)."""
+        if stage not in ("full", "features", "head", "block"):
             raise ValueError(f"unknown plan stage {stage!r}")
         self.stage = stage
-        if height % 32 or width % 32:
+        if stage == "block":
+            if block is None or (not block.takes_image and (not head_inputs or len(head_inputs) != 1)):
+                raise ValueError("a block plan takes the block and its one input shape")
+            if block.takes_image and (height % 2 or width % 2):
+                raise ValueError("the Focus stem needs an even input size")
+        elif height % 32 or width % 32:
             raise ValueError("input size must be multiples of 32")
         chunk = chunk or batch
         if chunk <= 0 or batch % chunk:
@@ -585,12 +592,23 @@ class Plan:
             if chunk != batch or not head_inputs or len(head_inputs) != 3:
                 raise ValueError("a head plan takes three feature maps and no chunking")
             feats = [ctx.buffer(h, w, c).full() for c, h, w in head_inputs]
+        elif stage == "block":
+            if chunk != batch:
+                raise ValueError("a block plan takes no chunking")
+            if block.takes_image:
+                self.block_input = None
+                outs = block.plan_block(ctx, ctx.image(height, width))
+            else:
+                c, h, w = head_inputs[0]
+                self.block_input = ctx.buffer(h, w, c).full()
+                outs = block.plan_block(ctx, self.block_input)
+            feats = list(outs) if isinstance(outs, (tuple, list)) else [outs]
         else:
             feats = model.backbone.plan(ctx, ctx.image(height, width))
         self.feats = feats
         anchors = sum(f.lh * f.lw for f in feats)
         self.out_spec = OutBuffer(anchors, 5 + self.num_classes)
-        if stage != "features":
+        if stage in ("full", "head"):
             head.plan(ctx, feats, self.out_spec, train=train)
         elif chunk != batch:
             raise ValueError("a features plan takes no chunking")
@@ -642,7 +660,7 @@ class Plan:
                     foff += _align(sp.cout * sp.kh * sp.kw * sp.cin_pad * ctx.esize)
         self.farena = torch.empty(max(foff, 1), dtype=torch.uint8, device=self.device)
         self.barena = torch.empty(max(boff, 1), dtype=torch.uint8, device=self.device)
-        self.output = torch.empty(batch, anchors if stage != "features" else 0, 5 + self.num_classes,
+        self.output = torch.empty(batch, anchors if stage in ("full", "head") else 0, 5 + self.num_classes,
                                   dtype=torch.float32, device=self.device)
         self._input_slot: Optional[torch.Tensor] = None
         self._nops = len(ctx.ops)
@@ -934,6 +952,22 @@ class Plan:
         self._bind_input(x)
         N.check(self.lib.yxh_run_ops(self._ops, len(self._ops), N.stream_ptr(self.device)), "backbone")
         return tuple(self.feature_view(v) for v in self.feats)
+
+    def run_block(self, x: torch.Tensor) -> list:
+        """stage "block": the block's output map(s) of one NCHW input, NCHW in the compute dtype."""
+        if self.stage != "block":
+            raise RuntimeError("run_block needs a block plan")
+        self.pack_weights()
+        if self.block_input is None:
+            self._bind_input(x)
+        else:
+            b = self.block_input.buf
+            if tuple(x.shape) != (self.batch, b.c, b.h, b.w):
+                raise ValueError(f"input shape {tuple(x.shape)} != planned {(self.batch, b.c, b.h, b.w)}")
+            dst = self.arena[b.offset:b.offset + self.batch * b.nelem_image * b.esize].view(self.dtype)
+            dst.view(self.batch, b.h, b.w, b.c).copy_(x.to(self.device).permute(0, 2, 3, 1))
+        N.check(self.lib.yxh_run_ops(self._ops, len(self._ops), N.stream_ptr(self.device)), "block")
+        return [self.feature_view(v) for v in self.feats]
 
     def run_head(self, xin, out: torch.Tensor) -> torch.Tensor:
         """stage "head": decoded [B, A, 5+C] rows of three NCHW feature maps."""

@@ -28,11 +28,52 @@ def _act_module(name: str) -> nn.Module:
 
 
 class _Planned(nn.Module):
-    """Modules of this tree run only as part of a planned YoloxModule forward."""
+    """Modules of this tree run as parts of a planned YoloxModule forward; standalone, a block's
+    forward (the reference's eager call, e.g. ``module.backbone.backbone.dark3(x)``) runs a
+    one-block HIP plan of it (``plan_block``), cached per input shape.  Eval mode only: the plan
+    folds BatchNorm's running statistics (training-mode batch statistics run only inside
+    YoloxModule.forward(x, targets))."""
 
-    def forward(self, *args, **kwargs):  # pragma: no cover - guard
+    takes_image = False  # plan_block's input: the [B, 3, H, W] image (Focus / CspDarknet) or a map
+
+    def plan_block(self, ctx, x):  # pragma: no cover - every planned block overrides it
+        raise NotImplementedError(f"{type(self).__name__} has no standalone plan")
+
+    def forward(self, x):
+        outs = _block_forward(self, x)
+        return outs[0]
+
+    def _apply(self, fn, *args, **kwargs):
+        self.__dict__.pop("_stage_plans", None)
+        return super()._apply(fn, *args, **kwargs)
+
+
+def _block_forward(block: nn.Module, x: torch.Tensor) -> list:
+    """Standalone forward of one building block (network_blocks.py / darknet.py modules) through
+    a block plan: NCHW in, NCHW out in the parameters' dtype."""
+    from .. import _native as N
+    from ..engine import Plan
+    if block.training:
         raise NotImplementedError(
-            f"{type(self).__name__} is executed by the HIP plan of YoloxModule; call the YoloxModule")
+            f"{type(block).__name__}.forward in training mode (BatchNorm batch statistics) is not planned: "
+            "call .eval() first, or train through YoloxModule.forward(x, targets)")
+    if not isinstance(x, torch.Tensor) or x.dim() != 4:
+        raise ValueError(f"{type(block).__name__} takes one [B, C, H, W] tensor")
+    p = _param0(block)
+    if p.device.type != "cuda":
+        raise RuntimeError(f"{type(block).__name__} runs on a ROCm device only; call .to('cuda') first")
+    B, C, H, W = x.shape
+    if block.takes_image:
+        if C != 3:
+            raise ValueError(f"expected [B, 3, H, W] images, got {tuple(x.shape)}")
+        if x.dtype not in (torch.float32, torch.bfloat16, torch.float16, torch.uint8):
+            x = x.float()
+    else:
+        x = x.to(p.dtype)
+    key = ("block", B, C, H, W, x.dtype, p.dtype, str(p.device))
+    plan = _stage_plan(block, key, lambda: Plan(_StageModel(block), B, H, W, p.dtype, p.device, N.NCHW, x.dtype,
+                                                stage="block", block=block, head_inputs=[(C, H, W)]))
+    return plan.run_block(x)
 
 
 class _StageModel:
@@ -73,6 +114,9 @@ class BaseConv(_Planned):
     def plan(self, ctx, srcs, out=None, residual=None):
         return ctx.conv(self, srcs, out=out, residual=residual)
 
+    def plan_block(self, ctx, x):
+        return self.plan(ctx, [x])
+
 
 class DWConv(_Planned):
     """Depthwise BaseConv (groups = cin) followed by a pointwise BaseConv."""
@@ -85,6 +129,9 @@ class DWConv(_Planned):
     def plan(self, ctx, srcs, out=None, residual=None):
         t = ctx.conv(self.dconv, srcs)
         return ctx.conv(self.pconv, [t], out=out, residual=residual)
+
+    def plan_block(self, ctx, x):
+        return self.plan(ctx, [x])
 
 
 def _conv_cls(depthwise: bool):
@@ -103,6 +150,10 @@ class Bottleneck(_Planned):
         """y = conv2(conv1(x)) (+ x); ``out`` may alias ``x`` (in-place residual)."""
         t = self.conv1.plan(ctx, [x])
         return self.conv2.plan(ctx, [t], out=out, residual=x if self.use_add else None)
+
+    def plan_block(self, ctx, x):
+        out = ctx.buffer(x.lh, x.lw, _out_channels(self.conv2)).full()
+        return self.plan(ctx, x, out)
 
 
 class SPPBottleneck(_Planned):
@@ -123,6 +174,9 @@ class SPPBottleneck(_Planned):
         ctx.spp(cat, hidden)
         return self.conv2.plan(ctx, [cat.full()], out=out)
 
+    def plan_block(self, ctx, x):
+        return self.plan(ctx, [x])
+
 
 class CspLayer(_Planned):
     """CSP bottleneck with 3 convs; the concat buffer [x_1 | x_2] is written in place."""
@@ -135,6 +189,9 @@ class CspLayer(_Planned):
         self.conv2 = BaseConv(in_channels, hidden, 1, stride=1, act=act)
         self.conv3 = BaseConv(2 * hidden, out_channels, 1, stride=1, act=act)
         self.m = nn.Sequential(*[Bottleneck(hidden, hidden, shortcut, 1.0, depthwise, act=act) for _ in range(n)])
+
+    def plan_block(self, ctx, x):
+        return self.plan(ctx, [x])
 
     def plan(self, ctx, srcs, out=None, fused_head=None):
         """``fused_head``: (the [x_1 | x_2] buffer, the first Bottleneck's hidden map) already
@@ -196,6 +253,11 @@ class Focus(_Planned):
         super().__init__()
         self.conv = BaseConv(in_channels * 4, out_channels, ksize, stride, act=act)
 
+    takes_image = True
+
+    def plan_block(self, ctx, image):
+        return self.plan(ctx, image)
+
     def plan(self, ctx, image):
         """Fused into one 6x6 s2 conv on the image (yxh_stem_conv) when the geometry
         allows; otherwise yxh_focus_pack + the 3x3 conv on the packed channels."""
@@ -221,6 +283,19 @@ class CspDarknet(_Planned):
         self.dark5 = nn.Sequential(Conv(bc * 8, bc * 16, 3, 2, act=act),
                                    SPPBottleneck(bc * 16, bc * 16, activation=act),
                                    CspLayer(bc * 16, bc * 16, n=bd, shortcut=False, depthwise=depthwise, act=act))
+
+    takes_image = True
+
+    def forward(self, x):
+        """darknet.py:165-177 standalone: {"dark3", "dark4", "dark5"} feature maps of [B, 3, H, W]
+        images (NCHW, the parameters' dtype) by a backbone-only HIP plan."""
+        if set(self.out_features) - {"dark3", "dark4", "dark5"}:
+            raise NotImplementedError("the planned CspDarknet returns dark3 / dark4 / dark5 only")
+        outs = dict(zip(("dark3", "dark4", "dark5"), _block_forward(self, x)))
+        return {k: v for k, v in outs.items() if k in self.out_features}
+
+    def plan_block(self, ctx, image):
+        return self.plan(ctx, image)
 
     def plan(self, ctx, packed):
         fused = ctx.stem_s2_fusable(self.stem.conv, self.dark2[0])

@@ -274,3 +274,56 @@ def test_submodules_are_callable_like_the_reference(golden):
         m.train()
         m.head(list(feats))
     m.eval()
+
+
+BLOCK_CASES = {  # tests/golden/make_golden.py gen_blocks: the reference's own modules, eval mode
+    "focus": ("Focus", (3, 32), dict(ksize=3)),
+    "conv3s1": ("BaseConv", (32, 48, 3, 1), {}),
+    "conv3s2": ("BaseConv", (32, 64, 3, 2), {}),
+    "conv1": ("BaseConv", (64, 32, 1, 1), {}),
+    "conv1_lrelu": ("BaseConv", (32, 32, 1, 1), dict(act="lrelu")),
+    "conv3_relu": ("BaseConv", (32, 32, 3, 1), dict(act="relu")),
+    "bottleneck": ("Bottleneck", (32, 32, True, 1.0), {}),
+    "spp": ("SPPBottleneck", (64, 64), {}),
+    "csp_short": ("CspLayer", (64, 64), dict(n=2, shortcut=True)),
+    "csp_noshort": ("CspLayer", (128, 64), dict(n=1, shortcut=False)),
+    "dwconv3s1": ("DWConv", (32, 48, 3, 1), {}),
+    "dwconv3s2": ("DWConv", (32, 64, 3, 2), {}),
+}
+
+
+@pytest.mark.parametrize("key", list(BLOCK_CASES))
+def test_building_blocks_callable_standalone(golden, key):
+    """network_blocks.py modules called on their own (Focus, BaseConv incl. lrelu / relu,
+    Bottleneck, SPPBottleneck, CspLayer, DWConv), each a one-block HIP plan, vs the
+    reference modules' own outputs on the same weights (blocks.npz) at the fp32 bar (1e-4 of
+    the output's range; measured ~1e-6)."""
+    from yolox_amd.models import network
+    d = golden("blocks.npz")
+    cls, args, kw = BLOCK_CASES[key]
+    m = getattr(network, cls)(*args, **kw)
+    pre = f"{key}.p."
+    m.load_state_dict({k[len(pre):]: torch.from_numpy(v) for k, v in d.items() if k.startswith(pre)})
+    m = m.cuda().eval()
+    x = torch.from_numpy(d[f"{key}.x"]).cuda()
+    y = m(x)
+    ref = torch.from_numpy(d[f"{key}.y"])
+    assert tuple(y.shape) == tuple(ref.shape) and y.dtype == torch.float32
+    assert (y.cpu() - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
+    assert torch.equal(m(x), y)  # the cached plan again
+    with pytest.raises(NotImplementedError, match="training mode"):
+        m.train()(x)
+
+
+def test_backbone_stages_callable_standalone(golden):
+    """module.backbone.backbone(x) (CspDarknet: {"dark3", "dark4", "dark5"}) and a stage
+    Sequential (dark3 = BaseConv s2 + CspLayer, each a block plan) equal the full plan's maps."""
+    d = golden("fwd_yolox_s_128.npz")
+    m = model("yolox_s", torch.float32).eval()
+    x = torch.from_numpy(d["input_u8"]).permute(0, 3, 1, 2).float().cuda()
+    dark = m.backbone.backbone
+    outs = dark(x)
+    assert list(outs) == ["dark3", "dark4", "dark5"]
+    d3 = dark.dark3(dark.dark2(dark.stem(x)))
+    assert (d3 - outs["dark3"]).abs().max().item() <= 1e-4 * outs["dark3"].abs().max().item()
+    assert tuple(outs["dark5"].shape) == (x.shape[0], 512, 4, 4)

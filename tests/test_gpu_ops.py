@@ -326,6 +326,10 @@ def test_letterbox_resize_cases():
     assert np.abs(out[:, :rh, :rw] - fl).max() <= 1.01
 
 
+# conv_glds (ids 17-25) two-slab staging of the wide tiles spilled to scratch (round 4): not built
+GLDS_K2_WITHDRAWN = {17, 18, 20, 23, 24}
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 def test_every_tile_variant(dtype):
     """All tile configurations x K-slab counts x both kernels (register-staged and
@@ -336,6 +340,10 @@ def test_every_tile_variant(dtype):
     X = nhwc(x, dtype)
     for tid in list(range(1, 10)) + list(range(17, 26)):
         for ks in (1, 2):
+            if ks == 2 and tid in GLDS_K2_WITHDRAWN:
+                with pytest.raises(NotImplementedError, match="spilled"):
+                    run_conv([(X, 0, 64, 0)], conv, bn, dtype, tile=2 * tid + ks - 1)
+                continue
             y = run_conv([(X, 0, 64, 0)], conv, bn, dtype, tile=2 * tid + ks - 1)
             close(y.permute(0, 3, 1, 2), want, dtype)
 

@@ -12,8 +12,10 @@ if [ -n "$TESTS" ]; then
   tail -4 gpurun_out/tests_$TAG.log
   [ $rc -eq 0 ] || { grep -E "^E |Error" gpurun_out/tests_$TAG.log | head -20; exit $rc; }
 fi
+i=0
 for e in ${AB:-DEFAULT=1}; do
-  env $e timeout -k 10 300 python -u bench.py --no-cpu-baseline --layers > gpurun_out/bench_${TAG}_$e.json \
-      2> gpurun_out/bench_${TAG}_$e.err || { tail -5 gpurun_out/bench_${TAG}_$e.err; exit 1; }
-  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], 'img/s fwd', d['roofline']['forward_ms'], 'ms frac', d['roofline']['frac'])" gpurun_out/bench_${TAG}_$e.json $e
+  i=$((i + 1))
+  f=gpurun_out/bench_${TAG}_${i}_${e//\//_}
+  env $e timeout -k 10 300 python -u bench.py --no-cpu-baseline --layers > $f.json 2> $f.err || { tail -5 $f.err; exit 1; }
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], 'img/s fwd', d['roofline']['forward_ms'], 'ms frac', d['roofline']['frac'])" $f.json $e
 done
