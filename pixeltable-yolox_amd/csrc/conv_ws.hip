@@ -94,6 +94,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     constexpr int SMEM = HWOFF + HBYTES_W;
     static_assert(!F1 || (S == 1 && NW % NG == 0), "fused Bottleneck tile");
     constexpr int FCO = (FC + WK - 1) / WK;  // pixel fragments this wave finishes
+    constexpr int NS = WCB * 9;              // K steps per tile (channel block x tap)
     constexpr int PD = FR * FC >= 8 ? 1 : FR * FC >= 4 ? 2 : 3;  // fragment-read distance in K steps
     static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0 && TM % (16 * WM) == 0, "tile");
     // weights must stay in VGPRs: 160 of 256 (2 waves per SIMD), 288 of 512 (one 4-wave block per CU)
@@ -365,17 +366,47 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     };
     constexpr int HPF = (TM / 16 + NW - 1) / NW;  // HP: pixel fragments per wave
     constexpr int NPU = PG ? PF2 * NF2 : HP ? HPF * PGH : 0;  // post pieces per wave per tile
-    auto post_piece = [&](const PostCtx& q, const int u) {
+    // a piece is split in two: its LDS operand reads (post_load) go out one K step before its
+    // MFMAs / decode / stores (post_math), and the pieces are spread SP steps apart over the
+    // tile's K loop, so no MFMA waits on a fresh LDS read and the reads do not bunch up
+    constexpr int KBP = PG ? KB2 : HP ? 2 * (TN / 32) : 1;  // operand registers of one piece
+    // (the head form keeps its pieces in the first steps, reads and MFMAs in one step: spread
+    // out or split, the 288-register weight set spills)
+    constexpr bool SPLIT = PG;
+    constexpr int SP = SPLIT && NS / (NPU + 1) > 1 ? NS / (NPU + 1) : 1;
+    auto post_skip = [&](const int u) -> bool {  // wave-uniform: a head piece with no rows
+        if constexpr (HP) {
+            const int pf = wave + NW * (u / PGH), f = u - PGH * (u / PGH);
+            return pf >= TM / 16 || f >= (hgrp1 ? 1 : PGH);
+        }
+        return false;
+    };
+    auto post_load = [&](const PostCtx& q, const int u, uint4 (&ob)[KBP]) {
+        if constexpr (PG) {
+            const int pf = u / NF2;
+            const int pl = (wm2 * PF2 + pf) * 16 + frow;
+#pragma unroll
+            for (int kb = 0; kb < KB2; ++kb)
+                ob[kb] = kb < TN / 32 ? *(const uint4*)(q.ys + (pl * RS + kb * 4 + fq) * 16)
+                                      : *(const uint4*)(q.xs + (pl * XS + (kb - TN / 32) * 4 + fq) * 16);
+        } else if constexpr (HP) {
+            if (post_skip(u)) return;
+            const int pf = wave + NW * (u / PGH), f = u - PGH * (u / PGH);
+            const char* wl = smem + HWOFF;
+#pragma unroll
+            for (int kb = 0; kb < TN / 32; ++kb) {
+                ob[2 * kb] = *(const uint4*)(q.ys + ((pf * 16 + frow) * RS + kb * 4 + fq) * 16);
+                ob[2 * kb + 1] = *(const uint4*)(wl + ((f * 16 + frow) * RS + kb * 4 + fq) * 16);
+            }
+        }
+    };
+    auto post_math = [&](const PostCtx& q, const int u, const uint4 (&ob)[KBP]) {
         if constexpr (PG) {
             const int pf = u / NF2, f = u - NF2 * (u / NF2);
             const int pl = (wm2 * PF2 + pf) * 16 + frow;
             f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int kb = 0; kb < KB2; ++kb) {
-                const uint4 bv = kb < TN / 32 ? *(const uint4*)(q.ys + (pl * RS + kb * 4 + fq) * 16)
-                                              : *(const uint4*)(q.xs + (pl * XS + (kb - TN / 32) * 4 + fq) * 16);
-                Mma<T>::run(z, a2[f][kb], bv);
-            }
+            for (int kb = 0; kb < KB2; ++kb) Mma<T>::run(z, a2[f][kb], ob[kb]);
             const int ty = pl / TX, tx = pl - ty * TX;
             const int oy = q.c.oy0 + ty, ox = q.c.ox0 + tx;
             const int n = (wn2 * NF2 + f) * 16 + fq * 4;
@@ -387,25 +418,26 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             const int od = oy < OH && ox < OW ? ((oy * OW + ox) * p.pgd_cs + n) * 2 : (int)dma::kOob;
             __builtin_amdgcn_raw_buffer_store_b64(uv, q.srd, od, 0, 0);
         } else if constexpr (HP) {
+            if (post_skip(u)) return;
             const int pf = wave + NW * (u / PGH), f = u - PGH * (u / PGH);
-            if (pf >= TM / 16 || f >= (hgrp1 ? 1 : PGH)) return;  // wave-uniform
-            const char* wl = smem + HWOFF;
-            const float* bl = (const float*)(wl + HROWS * RS * 16);
-            const int pl = pf * 16 + frow;
+            const float* bl = (const float*)(smem + HWOFF + HROWS * RS * 16);
+            // z[pixel][channel] (Y the A operand): lane l holds pixel 4 (l >> 4) + r of the
+            // fragment and channel l & 15, so each dword store writes 16 consecutive channels of
+            // 4 rows (4 x 64 B) instead of 4 channels of 16 rows
             f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int kb = 0; kb < TN / 32; ++kb)
-                Mma<T>::run(z, *(const uint4*)(wl + ((f * 16 + frow) * RS + kb * 4 + fq) * 16),
-                            *(const uint4*)(q.ys + (pl * RS + kb * 4 + fq) * 16));
-            const int ty = pl / TX, tx = pl - ty * TX;
-            const int oy = q.c.oy0 + ty, ox = q.c.ox0 + tx;
-            const bool okp = oy < OH && ox < OW;
-            const int rowo = (oy * OW + ox) * p.pgd_cs + (hgrp1 ? 0 : 5);
+            for (int kb = 0; kb < TN / 32; ++kb) Mma<T>::run(z, ob[2 * kb], ob[2 * kb + 1]);
             const float st = p.pg_stride;
+            const int ch = f * 16 + frow;
+            const float bch = bl[ch];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int ch = f * 16 + fq * 4 + r;
-                float v = z[r] + bl[ch];
+                const int pl = pf * 16 + fq * 4 + r;
+                const int ty = pl / TX, tx = pl - ty * TX;
+                const int oy = q.c.oy0 + ty, ox = q.c.ox0 + tx;
+                const bool okp = oy < OH && ox < OW;
+                const int rowo = (oy * OW + ox) * p.pgd_cs + (hgrp1 ? 0 : 5);
+                float v = z[r] + bch;
                 if (hgrp1) {
                     if (ch < 2) v = (v + (float)(ch == 0 ? ox : oy)) * st;
                     else if (ch < 4) v = __builtin_amdgcn_exp2f(v * 1.4426950408889634f) * st;
@@ -418,13 +450,17 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             }
         }
     };
+    auto post_piece = [&](const PostCtx& q, const int u) {
+        uint4 ob[KBP];
+        post_load(q, u, ob);
+        post_math(q, u, ob);
+    };
     auto post_all = [&](const PostCtx& q) {
 #pragma unroll
         for (int u = 0; u < NPU; ++u) post_piece(q, u);
     };
 
     f32x4 accp[FR][FCO];  // owned fragments of the previous tile, waiting for their epilogue
-    constexpr int NS = WCB * 9;
     constexpr int NP = FR * FCO;  // epilogue pieces, one per K step while they last
 
     // one tile: wait for its halo, start tile k+1's halo (+ residual), MMA of tile k with the
@@ -514,6 +550,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         if constexpr (EPI) e = epi_ctx(prev, k - 1);
         PostCtx pc{};
         if constexpr (POST) pc = post_ctx(prev2, k - 2);
+        uint4 pob[KBP];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             if (s + PD < NS) load_b(s + PD, bf[(s + PD) % (PD + 1)]);
@@ -526,8 +563,14 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             if constexpr (EPI)
                 if (s < NP) epi_piece(e, accp, s / FR, s % FR);
             // ... and piece s of the post work of the tile before that
-            if constexpr (POST)
-                if (s < NPU) post_piece(pc, s);
+            // ... and the post work of the tile before that: piece u's operands are read in step
+            // u * SP, its MFMAs and stores run in the next step
+            if constexpr (POST && SPLIT) {
+                if (s >= 1 && (s - 1) % SP == 0 && (s - 1) / SP < NPU) post_math(pc, (s - 1) / SP, pob);
+                if (s % SP == 0 && s / SP < NPU) post_load(pc, s / SP, pob);
+            } else if constexpr (POST) {
+                if (s % SP == 0 && s / SP < NPU) post_piece(pc, s / SP);
+            }
             // keep the one-step-ahead read distance (the scheduler would otherwise pull each
             // read down next to its first MFMA) and put two VALU ops in each MFMA's shadow
             if (s + PD < NS) __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);  // DS reads
@@ -540,9 +583,11 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         if constexpr (EPI)
 #pragma unroll
             for (int q = NS; q < NP; ++q) epi_piece(e, accp, q / FR, q % FR);
-        if constexpr (POST)
+        if constexpr (POST) {
+            if (SPLIT && (NS - 1) % SP == 0 && (NS - 1) / SP < NPU) post_math(pc, (NS - 1) / SP, pob);
 #pragma unroll
-            for (int u = NS; u < NPU; ++u) post_piece(pc, u);
+            for (int u = (NS + SP - 1) / SP; u < NPU; ++u) post_piece(pc, u);
+        }
 
         // ---- K-split: partial sums of the fragments other waves finish go through LDS
         if constexpr (WK > 1) {
