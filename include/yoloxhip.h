@@ -154,6 +154,10 @@ typedef struct {
  * over its stacked [cls | reg] features (yolo_head.py:160-161) as ONE launch; conv_ws tiles,
  * 16-bit, 3x3 s1 only. */
 #define YXH_CONV_GROUPS2 2
+/* With post_weight (not the head form): ALSO store the conv's output tile to dst (the Bottleneck
+ * chain of a CspLayer, network_blocks.py:95-99 / 160-183: Bottleneck i's 3x3 + shortcut output is
+ * Bottleneck i+1's input and shortcut, and the post conv is Bottleneck i+1's conv1 over it). */
+#define YXH_CONV_POST_STORE 4
 
 int yxh_conv2d(const yxh_conv_desc* d, void* stream);
 

@@ -494,6 +494,7 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     p.dst_bs = d->dst_bstride;
     p.dst_f32 = d->dst_dtype == YXH_F32 && dt != YXH_F32 ? 1 : (dt == YXH_F32 ? 1 : 0);
     YXH_CHECK_ARG(!(d->flags & YXH_CONV_ACCUMULATE) || d->dst_dtype == YXH_F32, "accumulate needs an f32 dst");
+    YXH_CHECK_ARG(!(d->flags & YXH_CONV_POST_STORE) || d->post_weight, "YXH_CONV_POST_STORE needs a post conv");
     p.accum = (d->flags & YXH_CONV_ACCUMULATE) ? 1 : 0;
     p.act = d->act;
     p.dstride = d->decode_stride;
@@ -558,8 +559,14 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         p.pgs_bs = d->post_src.bstride;
         p.pgs_ch = d->post_src.channels;
         p.pg_cout = d->post_cout;
-        if (d->tile == 0)  // default post tile per shape
-            return conv_ws_dispatch(dt, head ? 51 : d->stride == 2 ? 45 : d->cin == 32 ? 41 : 43, p, st);
+        p.pg_store = (d->flags & YXH_CONV_POST_STORE) ? 1 : 0;
+        YXH_CHECK_ARG(!p.pg_store || (!head && d->dst && p.vec_store && d->dst_dtype == dt),
+                      "YXH_CONV_POST_STORE: a 1x1 post conv (not the head form) and a 16-bit dst of 8-byte rows");
+        if (d->tile == 0) {  // default post tile per shape
+            const bool chain = d->post_src.channels == 0 && d->stride == 1;
+            return conv_ws_dispatch(
+                dt, head ? 51 : d->stride == 2 ? 45 : chain ? (d->cin == 64 ? 54 : 55) : d->cin == 32 ? 41 : 43, p, st);
+        }
         if (!((d->tile >> 1) > 220 && (d->tile >> 1) <= 220 + kNumWsPostTiles)) {
             set_error("a post conv runs on the conv_ws post tiles (ids 221-%d) only", 220 + kNumWsPostTiles);
             return YXH_EUNSUPPORTED;

@@ -47,6 +47,7 @@ struct ConvParams {
     const float* pgb2;
     int pg_cout2;
     float pg_stride;
+    int pg_store;  // YXH_CONV_POST_STORE: the conv output tile is stored to dst as well
 };
 
 // Stationary weight fragment (i: 16 output channels from n_first, tap, kb: 32-channel K block)
@@ -304,7 +305,7 @@ int conv_ws_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumWsTiles = 36;  // 31..36: fused Bottleneck (pre_weight)
 // conv_ws tiles with a 1x1 post conv (yxh_conv_desc.post_weight): tile ids 221..220+kNumWsPostTiles
 // (conv_ws_dispatch ids 41..40+kNumWsPostTiles)
-constexpr int kNumWsPostTiles = 13;
+constexpr int kNumWsPostTiles = 16;
 // Weight-stationary persistent 1x1 conv over dense sources (conv_ws1.hip): tile ids 201..200+kNumWs1Tiles
 int conv_ws1_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumWs1Tiles = 10;

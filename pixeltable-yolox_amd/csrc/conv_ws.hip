@@ -169,6 +169,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 
     const bool silu = p.act == YXH_ACT_SILU;
     const bool has_res = p.res != nullptr;
+    const bool pg_store = PG && p.pg_store;
     const uint32_t dbytes = (uint32_t)((long long)ohw * p.dst_cs * 2);
     const uint32_t rbytes = (uint32_t)((long long)ohw * p.res_cs * 2);
     const int dcs = p.dst_cs, rcs = p.res_cs;
@@ -333,8 +334,10 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         u32x2 u;
         __builtin_memcpy(&u, t, 8);
         if constexpr (PGY) {
-            (void)od;  // Y stays in LDS, over this lane's own residual values
+            // Y stays in LDS, over this lane's own residual values (and, YXH_CONV_POST_STORE,
+            // leaves for dst too: the next Bottleneck's input)
             *(u32x2*)(e.rl + (pl * RS + (nl >> 3)) * 16 + (nl & 7) * 2) = u;
+            if (PG && pg_store) __builtin_amdgcn_raw_buffer_store_b64(u, e.dsrd, od, 0, 0);
         } else if (!(YXH_WS_PROBE & 1) || p.act == 12345) {
             __builtin_amdgcn_raw_buffer_store_b64(u, e.dsrd, od, 0, 0);
         }
@@ -677,7 +680,7 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
             set_error("conv_ws head-form tile: two groups of %d channels, %d class fragments", TN, PGH);
             return YXH_EUNSUPPORTED;
         }
-    } else if ((p.pgw != nullptr) != (PGN > 0) || p.pgw2 ||
+    } else if ((p.pgw != nullptr) != (PGN > 0) || p.pgw2 || (p.pg_store && PGN == 0) ||
                (PGN > 0 && (p.pg_cout != PGN || p.pgs_ch != PGC || p.cout != TN))) {
         set_error(PGN > 0 ? "conv_ws post tile built for %d -> %d channels + a %d-channel post_src, post conv %d"
                           : "conv_ws plain tile with a post conv (%d -> %d, %d, %d)",
@@ -785,6 +788,13 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 51: return launch_ws<T, 128, 1, 16, 4, 128, 4, 1, 1, 1, false, 0, 0, 5>(p, st);
         // (id 52, the eight-wave K-split head form, spilled once its post pieces rode the MFMA loop)
         case 53: return launch_ws<T, 128, 1, 16, 2, 128, 4, 1, 1, 1, false, 0, 0, 5>(p, st);
+        // Bottleneck chain (YXH_CONV_POST_STORE): the 3x3 + shortcut output stored AND the next
+        // Bottleneck's conv1 (1x1 C -> C) over it: dark3 (64 @80x80), dark4 (128 @40x40)
+        // (one block of 4 waves per CU: the 2-block / 8-wave forms spill)
+        case 52: return launch_ws<T, 64, 1, 16, 8, 64, 2, 1, 2, 1, false, 64, 0>(p, st);
+        case 54: return launch_ws<T, 64, 1, 16, 4, 64, 2, 1, 2, 1, false, 64, 0>(p, st);
+        case 55: return launch_ws<T, 128, 1, 8, 4, 128, 4, 1, 1, 1, false, 128, 0>(p, st);
+        case 56: return launch_ws<T, 128, 1, 16, 2, 128, 4, 1, 1, 1, false, 128, 0>(p, st);
         default: set_error("conv_ws tile id %d", id); return YXH_EINVAL;
     }
 }

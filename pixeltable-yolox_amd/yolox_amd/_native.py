@@ -56,6 +56,7 @@ class ConvDesc(C.Structure):
 
 CONV_ACCUMULATE = 1
 CONV_GROUPS2 = 2
+CONV_POST_STORE = 4
 
 
 class OptSeg(C.Structure):

@@ -287,7 +287,9 @@ class PlanCtx:
         return out
 
     # (main conv cin, stride, post_src channels, post cout) shapes the conv_ws post tiles are built for
-    POST_SHAPES = {(32, 1, 32, 64), (64, 1, 64, 128), (64, 2, 0, 128)}
+    # (cin, stride, post_src channels, post cout): dark2 / dark3 / C3_p3 conv3 over [y | x_2], a stage's
+    # stride-2 conv + conv1 | conv2, and the Bottleneck chain (3x3 + shortcut, stored, + the next conv1)
+    POST_SHAPES = {(32, 1, 32, 64), (64, 1, 64, 128), (64, 2, 0, 128), (64, 1, 0, 64), (128, 1, 0, 128)}
 
     def post_fusable(self, m, post_ms, post_src_ch: int) -> bool:
         """BaseConv ``m`` (3x3) followed by the 1x1 BaseConvs ``post_ms`` (stacked along cout)
@@ -306,9 +308,10 @@ class PlanCtx:
                         and q.in_channels == k.out_channels + post_src_ch for q in pk))
 
     def conv_post(self, m, srcs: list, post_ms, post_src: Optional[View], post_out: View,
-                  residual: Optional[View] = None) -> View:
+                  residual: Optional[View] = None, out: Optional[View] = None) -> View:
         """conv ``m`` + the 1x1 post conv (``post_ms`` stacked) over [m's output | post_src] as
-        ONE launch (yxh_conv_desc.post_*): m's output never leaves the block's LDS."""
+        ONE launch (yxh_conv_desc.post_*): m's output never leaves the block's LDS -- unless
+        ``out`` is given (YXH_CONV_POST_STORE: the Bottleneck chain), then it is stored there too."""
         k = m.conv
         lh, lw = srcs[0].lh, srcs[0].lw
         s = k.stride[0]
@@ -321,7 +324,7 @@ class PlanCtx:
         self.ops.append(OpRec(N.OP_CONV, dict(
             srcs=list(srcs), out=None, residual=residual, spec=spec, cin=k.in_channels, cout=k.out_channels, k=3,
             stride=s, pad=1, groups=1, in_h=lh, in_w=lw, out_h=oh, out_w=ow, act=N.ACT_CODE["silu"], dst_f32=False,
-            post_spec=pspec, post_src=post_src, post_out=post_out)))
+            post_spec=pspec, post_src=post_src, post_out=post_out, post_store_out=out)))
         self.flops += 2.0 * self.batch * oh * ow * (k.out_channels * 9 * k.in_channels + cout_post * pspec.cin_pad)
         return post_out
 
@@ -445,7 +448,7 @@ class OutBuffer:
 # conv_pwr kernel, 97-104 the dense 1x1 conv_pwf kernel, 113-150 the 3x3 conv_r3 kernel
 # (yoloxhip.h yxh_conv_desc.tile)
 TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
-                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 197)] + [2 * i for i in range(201, 211)] + [2 * i for i in range(221, 234)]
+                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 197)] + [2 * i for i in range(201, 211)] + [2 * i for i in range(221, 237)]
 # 16-bit plans: the families that win on MI355X (profiles/r03/final/tune_r3fa_*.json: yolox_s picks only
 # conv_pwf / conv_ws / conv_ws1; yolox_l fp16 also conv_igemm and conv_r3 once or twice); the LDS-DMA
 # conv_glds, row-tiled conv_rows and the round-1 pointwise kernels never do and are tried only with
@@ -503,6 +506,8 @@ def op_buffers(r: OpRec) -> tuple:
     writes = [a["out"].buf] if a.get("out") is not None else []
     if a.get("post_out") is not None:
         writes.append(a["post_out"].buf)
+    if a.get("post_store_out") is not None:
+        writes.append(a["post_store_out"].buf)
     return reads, writes
 
 
@@ -818,7 +823,11 @@ class Plan:
                     po = a["post_out"]
                     d.post_dst = self._ptr(po, c)
                     d.post_dst_cstride, d.post_dst_bstride = po.buf.c, po.buf.nelem_image
-                    d.dst = d.post_dst
+                    so = a.get("post_store_out")
+                    if so is not None:  # the Bottleneck chain: the 3x3's output is stored as well
+                        d.flags |= N.CONV_POST_STORE
+                        po = so
+                    d.dst = self._ptr(po, c)
                     d.dst_dtype = ctx.dcode
                     d.dst_cstride, d.dst_bstride = po.buf.c, po.buf.nelem_image
                 elif a["dst_f32"]:

@@ -201,12 +201,7 @@ class CspLayer(_Planned):
             cat, t0 = fused_head
             x1 = cat.slice(0, hidden)
             rest = list(self.m)
-            if t0 is not None:  # the first Bottleneck's conv1 already ran
-                b0 = rest.pop(0)
-                if not rest and self._post_fusable(ctx, b0):
-                    return self._plan_post(ctx, b0, t0, x1, cat, out)
-                b0.conv2.plan(ctx, [t0], out=x1, residual=x1 if b0.use_add else None)
-            return self._plan_tail(ctx, rest, x1, cat, out)
+            return self._plan_tail(ctx, rest, x1, cat, out, t=t0)  # t0: the first conv1 already ran
         cat = ctx.buffer(srcs[0].lh, srcs[0].lw, 2 * hidden)
         x1 = cat.slice(0, hidden)
         # conv1 | conv2 read the same input: one conv writes the whole [x_1 | x_2]
@@ -237,13 +232,35 @@ class CspLayer(_Planned):
         return ctx.conv_post(b.conv2, [t], [self.conv3], cat.slice(hidden, hidden), out,
                              residual=x1 if b.use_add else None)
 
-    def _plan_tail(self, ctx, bottlenecks, x1, cat, out):
+    def _plan_tail(self, ctx, bottlenecks, x1, cat, out, t=None):
+        """The Bottlenecks in place on x_1, then conv3.  ``t``: the first Bottleneck's conv1 output
+        when an earlier launch computed it.  Fused where the tiles exist: Bottleneck i's 3x3 +
+        shortcut with Bottleneck i+1's conv1 as its post conv (the chain: its output stored too),
+        and the last one's 3x3 with conv3 over [y | x_2] (the output never stored)."""
+        hidden = self.conv1.conv.out_channels
         for i, b in enumerate(bottlenecks):
-            if i == len(bottlenecks) - 1 and self._post_fusable(ctx, b):
+            last = i == len(bottlenecks) - 1
+            if t is None and not (last and self._post_fusable(ctx, b)) and not self._chain_fusable(ctx, bottlenecks, i):
+                b.plan(ctx, x1, out=x1)
+                continue
+            if t is None:
                 t = b.conv1.plan(ctx, [x1])
+            if last and self._post_fusable(ctx, b):
                 return self._plan_post(ctx, b, t, x1, cat, out)
-            b.plan(ctx, x1, out=x1)
+            res = x1 if b.use_add else None
+            if self._chain_fusable(ctx, bottlenecks, i):
+                t_next = ctx.buffer(x1.lh, x1.lw, hidden).full()
+                ctx.conv_post(b.conv2, [t], [bottlenecks[i + 1].conv1], None, t_next, residual=res, out=x1)
+                t = t_next
+            else:
+                b.conv2.plan(ctx, [t], out=x1, residual=res)
+                t = None
         return self.conv3.plan(ctx, [cat.full()], out=out)
+
+    @staticmethod
+    def _chain_fusable(ctx, bottlenecks, i) -> bool:
+        return (i + 1 < len(bottlenecks) and hasattr(ctx, "post_fusable")
+                and ctx.post_fusable(bottlenecks[i].conv2, [bottlenecks[i + 1].conv1], 0))
 
 
 class Focus(_Planned):

@@ -139,9 +139,12 @@ def test_planner_topology_and_flops(name, hw, gflop, anchors):
     n_stem_csp = sum(1 for o in ctx.ops if o.kind == 5 and o.args.get("dst") is None)
     assert n_stem_csp == (1 if name == "yolox_s" else 0)
     # ... and 16-bit convs followed by a 1x1 that fits a conv_ws post tile (a Bottleneck 3x3 +
-    # CspLayer.conv3, a stride-2 stage conv + its CspLayer conv1 | conv2) are one op each
+    # CspLayer.conv3, a stride-2 stage conv + its CspLayer conv1 | conv2, a Bottleneck 3x3 + the
+    # next Bottleneck's conv1: dark3's and dark4's chains of three) are one op each
     n_post = sum(1 for o in ctx.ops if o.args.get("post_spec") is not None)
-    assert n_post == (4 if name == "yolox_s" else n_post)
+    n_chain = sum(1 for o in ctx.ops if o.args.get("post_store_out") is not None)
+    assert n_post == (8 if name == "yolox_s" else n_post)
+    assert n_chain == (4 if name == "yolox_s" else n_chain)
     assert (kinds.count(0) == n_bn_convs - n_csp - fused_head + 2 * (3 - heads - n_head_post) - 1 - n_fused_bneck
             - n_grouped
             - s2 - 2 * n_stem_csp - n_post)

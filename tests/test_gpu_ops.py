@@ -842,6 +842,39 @@ def test_conv_ws_post_conv_bit_exact_vs_two_launches(geom):
     assert torch.equal(Z, z), (Z.float() - z.float()).abs().max().item()
 
 
+@pytest.mark.parametrize("cin,plain,chain,H,W,B", [
+    (64, 165, 232, 40, 36, 3), (64, 165, 234, 21, 19, 2), (128, 187, 235, 20, 20, 4), (128, 186, 236, 13, 22, 2)])
+def test_conv_ws_bottleneck_chain_bit_exact_vs_two_launches(cin, plain, chain, H, W, B):
+    """Chain tiles (ids 232 / 234-236, YXH_CONV_POST_STORE, round 4): Bottleneck i's 3x3 + shortcut
+    with Bottleneck i+1's conv1 as the post conv (network_blocks.py:95-99 in a CspLayer's chain)
+    store the 3x3's output AND the 1x1 over it, bit for bit what the plain conv_ws tile (same
+    K order) + a dense 1x1 (conv_pwf) compute; in place over the shortcut buffer, as planned."""
+    n = N()
+    dtype = torch.bfloat16
+    conv, bn = make_conv(cin, cin, 3, 1, seed=cin + H)
+    pconv, pbn = make_conv(cin, cin, 1, 1, seed=cin + W)
+    g = torch.Generator().manual_seed(H * W + cin)
+    T = nhwc(torch.randn(B, cin, H, W, generator=g), dtype)
+    X1 = nhwc(torch.randn(B, cin, H, W, generator=g), dtype)
+    pw, pb = pack(pconv, pbn, dtype)
+    y_ref = run_conv([(T, 0, cin, 0)], conv, bn, dtype, residual=(X1, 0), out=torch.zeros_like(X1), tile=2 * plain)
+    z_ref = run_conv([(y_ref, 0, cin, 0)], pconv, pbn, dtype, tile=2 * 97)
+    Y = X1.clone()  # the chain runs in place over its shortcut
+    Z = torch.zeros_like(X1)
+    run_conv([(T, 0, cin, 0)], conv, bn, dtype, residual=(Y, 0), out=Y, tile=2 * chain, flags=n.CONV_POST_STORE,
+             post=(pw, pb, None, Z, 0, cin))
+    assert torch.equal(Y, y_ref), (Y.float() - y_ref.float()).abs().max().item()
+    assert torch.equal(Z, z_ref), (Z.float() - z_ref.float()).abs().max().item()
+    # default chain tile (tile 0) and the flag's argument checks
+    Z0 = torch.zeros_like(X1)
+    Y0 = X1.clone()
+    run_conv([(T, 0, cin, 0)], conv, bn, dtype, residual=(Y0, 0), out=Y0, flags=n.CONV_POST_STORE,
+             post=(pw, pb, None, Z0, 0, cin))
+    assert torch.equal(Y0, y_ref) and torch.equal(Z0, z_ref)
+    with pytest.raises(ValueError, match="POST_STORE"):
+        run_conv([(T, 0, cin, 0)], conv, bn, dtype, flags=n.CONV_POST_STORE)
+
+
 @pytest.mark.parametrize("hw", [(80, 80), (20, 22), (13, 8)])
 def test_conv_ws_head_form_bit_exact_vs_two_launches(hw):
     """Head-form tiles (ids 231 / 233, round 4): a level's cls_convs[k][1] | reg_convs[k][1]

@@ -25,4 +25,12 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_I
     -d gpurun_out/pmc_${TAG}_SQ -o run --output-format csv \
     -- python bench.py $ARGS --steps 4 --warmup 1 --no-cpu-baseline --tune-file $TUNE \
     > gpurun_out/pmc_${TAG}_SQ.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS \
+    SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
+    -d gpurun_out/pmc_${TAG}_SQ2 -o run --output-format csv \
+    -- python bench.py $ARGS --steps 4 --warmup 1 --no-cpu-baseline --tune-file $TUNE \
+    > gpurun_out/pmc_${TAG}_SQ2.log 2>&1 || exit 1
+python tools/mfma_util.py gpurun_out/pmc_${TAG}_SQ/run_counter_collection.csv --last 3 \
+    --stalls gpurun_out/pmc_${TAG}_SQ2/run_counter_collection.csv --json gpurun_out/mfma_util_$TAG.json \
+    > gpurun_out/mfma_util_$TAG.txt || exit 1
 echo "profile $TAG done"

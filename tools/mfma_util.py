@@ -34,6 +34,14 @@ for (_, name), d in disp.items():
     for k, v in d.items():
         f[k] += v
     f["n"] += 1
+# optional second pass (--stalls CSV: SQ_WAVE_CYCLES, SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY,
+# SQ_INSTS_LDS, ...): where the waves' cycles go, per kernel template (dispatch ids of another run
+# differ, so it is matched by name; the whole pass is averaged per dispatch)
+stall = defaultdict(lambda: defaultdict(float))
+if "--stalls" in sys.argv:
+    for r in csv.DictReader(open(sys.argv[sys.argv.index("--stalls") + 1])):
+        if any(k in r["Kernel_Name"] for k in FWD):
+            stall[r["Kernel_Name"]][r["Counter_Name"]] += float(r["Counter_Value"])
 rows = []
 for name, f in fam.items():
     cyc = f["GRBM_GUI_ACTIVE"] / 8
@@ -42,15 +50,25 @@ for name, f in fam.items():
     rows.append({"kernel": name[:110], "dispatches": int(f["n"]), "time_us": f["ns"] / 1e3 / last, "mfma_util": util,
                  "clock_ghz": clk, "mfma_insts": f["SQ_INSTS_MFMA"], "valu_insts": f["SQ_INSTS_VALU"],
                  "valu_per_mfma": f["SQ_INSTS_VALU"] / max(f["SQ_INSTS_MFMA"], 1)})
+    st = stall.get(name)
+    if st and st.get("SQ_WAVE_CYCLES"):
+        wc = st["SQ_WAVE_CYCLES"]
+        rows[-1].update({"wait_any": st["SQ_WAIT_ANY"] / wc, "wait_inst_any": st["SQ_WAIT_INST_ANY"] / wc,
+                         "active_inst_any": st["SQ_ACTIVE_INST_ANY"] / wc,
+                         "wait_inst_lds": st.get("SQ_WAIT_INST_LDS", 0.0) / wc,
+                         "lds_bank_conflict_cycles": st.get("SQ_LDS_BANK_CONFLICT", 0.0)})
 rows.sort(key=lambda r: -r["time_us"])
 tot_t = sum(r["time_us"] for r in rows)
 tot_busy = sum(fam[n]["SQ_VALU_MFMA_BUSY_CYCLES"] for n in fam)
 tot_cyc = sum(fam[n]["GRBM_GUI_ACTIVE"] / 8 for n in fam)
 print(f"last {last} forwards; time per forward")
-print(f"{'time us':>9} {'share':>6} {'util':>6} {'GHz':>5} {'VALU/MFMA':>9}  kernel")
+print(f"{'time us':>9} {'share':>6} {'util':>6} {'GHz':>5} {'VALU/MFMA':>9} {'wait':>5} {'stall':>5} {'issue':>5}  kernel"
+      "   (wait / stall / issue: SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES)")
 for r in rows:
+    w = (f"{r['wait_any']:5.0%} {r['wait_inst_any']:5.0%} {r['active_inst_any']:5.0%}" if "wait_any" in r
+         else f"{'-':>5} {'-':>5} {'-':>5}")
     print(f"{r['time_us']:9.1f} {r['time_us'] / tot_t:6.1%} {r['mfma_util']:6.1%} {r['clock_ghz']:5.2f} "
-          f"{r['valu_per_mfma']:9.1f}  {r['kernel'][:80]}")
+          f"{r['valu_per_mfma']:9.1f} {w}  {r['kernel'][:80]}")
 print(f"all forward kernels: MFMA utilisation {tot_busy / (tot_cyc * 1024):.1%} (time-weighted)")
 if "--json" in sys.argv:
     json.dump({"source": path, "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)",

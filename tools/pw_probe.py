@@ -1,6 +1,6 @@
 """Probe: 1x1-conv time vs a plain copy of the same bytes, SiLU vs no activation,
 MALL-resident (same buffers) vs rotating buffers (> 256 MB Infinity Cache).
-Run on the GPU box: python tools/pw_probe.py"""
+Run on the GPU box: python tools/pw_probe.py [tile codes]"""
 import ctypes as C
 import os
 import sys
@@ -14,7 +14,7 @@ L = N.lib()
 dev = torch.device("cuda:0")
 st = N.stream_ptr(dev)
 SHAPES = [(204800, 64, 64), (51200, 128, 128), (819200, 64, 64), (12800, 512, 512), (51200, 256, 256)]
-TILES = [6 * 2, 9 * 2, 81 * 2, 82 * 2, 6 * 2 + 1]
+TILES = [int(t) for t in sys.argv[1:]] or [97 * 2, 99 * 2, 203 * 2, 205 * 2, 206 * 2, 207 * 2]
 
 
 def timeit(fn, nbuf, reps=24):
