@@ -617,13 +617,15 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
                           (tile > 112 && tile <= 112 + kNumR3Tiles) || (tile > 160 && tile <= 160 + kNumWsTiles) ||
                           (tile > 200 && tile <= 200 + kNumWs1Tiles) || (tile > 210 && tile <= 210 + kNumPw1fTiles) ||
                           (tile > 214 && tile <= 214 + kNumDgradS2Tiles) ||
-                          (tile > 220 && tile <= 220 + kNumWsPostTiles),
+                          (tile > 220 && tile <= 220 + kNumWsPostTiles) ||
+                          (tile > 240 && tile <= 240 + kNumWs1DeepTiles),
                       "tile %d", d->tile);
         YXH_CHECK_ARG(want_ks == 1 || ks == 2, "2-slab staging not possible for this conv");
         ks = want_ks;
     }
     const int kstage = 4 * ks * epc;
     p.ncb = (d->cin + kstage - 1) / kstage;
+    if (tile > 240) return conv_ws1_dispatch(dt, tile - 240 + kNumWs1Tiles, p, st);
     if (tile > 220) return conv_ws_dispatch(dt, tile - 220 + 40, p, st);
     if (tile > 214) return dgrad_s2f_dispatch(dt, tile - 214, p, st);
     if (dilated && tile > 16) {

@@ -259,15 +259,19 @@ __device__ __forceinline__ void pwf_epilogue(const ConvParams& p, const f32x4 (&
         for (int i = 0; i < FR; ++i) {
             const int n = n0 + wr * 64 + i * 16 + fq * 4;
             if (n >= p.cout) continue;
-            float v[4];
+            const float* lb = lbias + wr * 64 + i * 16 + fq * 4;
+            f32x4 v = acc[i][j] + f32x4{lb[0], lb[1], lb[2], lb[3]};
+            if constexpr (ACT == YXH_ACT_SILU) {
+                v = silu4(v);  // packed pairs, bit-identical to apply_act's silu
+            } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = apply_act<false>(acc[i][j][r] + lbias[wr * 64 + i * 16 + fq * 4 + r], ACT);
+                for (int r = 0; r < 4; ++r) v[r] = apply_act<false>(v[r], ACT);
+            }
             if (rrow) {
                 const uint2 u = *(const uint2*)(rrow + n);
                 T t[4];
                 __builtin_memcpy(t, &u, 8);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] += to_f32(t[r]);
+                v = v + f32x4{to_f32(t[0]), to_f32(t[1]), to_f32(t[2]), to_f32(t[3])};
             }
             T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
             uint2 u;

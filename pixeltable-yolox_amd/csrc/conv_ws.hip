@@ -323,13 +323,9 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         if constexpr (GR > 0) rv = *(const u32x2*)(e.rl + (pl * RS + (nl >> 3)) * 16 + (nl & 7) * 2);
         T rt[4];
         __builtin_memcpy(rt, &rv, 8);
-        float v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float x = ap[i][o][q] + bias[i][q];
-            const float y = silu ? yxh::silu<false>(x) : x;
-            v[q] = has_res ? y + to_f32(rt[q]) : y;
-        }
+        const f32x4 x = ap[i][o] + f32x4{bias[i][0], bias[i][1], bias[i][2], bias[i][3]};
+        f32x4 v = silu ? yxh::silu4(x) : x;
+        if (has_res) v = v + f32x4{to_f32(rt[0]), to_f32(rt[1]), to_f32(rt[2]), to_f32(rt[3])};
         T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
         u32x2 u;
         __builtin_memcpy(&u, t, 8);
@@ -413,9 +409,8 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             const int ty = pl / TX, tx = pl - ty * TX;
             const int oy = q.c.oy0 + ty, ox = q.c.ox0 + tx;
             const int n = (wn2 * NF2 + f) * 16 + fq * 4;
-            T t[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) t[r] = from_f32<T>(yxh::silu<false>(z[r] + b2[f][r]));
+            const f32x4 zs = yxh::silu4(z + f32x4{b2[f][0], b2[f][1], b2[f][2], b2[f][3]});
+            T t[4] = {from_f32<T>(zs[0]), from_f32<T>(zs[1]), from_f32<T>(zs[2]), from_f32<T>(zs[3])};
             u32x2 uv;
             __builtin_memcpy(&uv, t, 8);
             const int od = oy < OH && ox < OW ? ((oy * OW + ox) * p.pgd_cs + n) * 2 : (int)dma::kOob;

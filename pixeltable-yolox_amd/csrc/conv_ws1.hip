@@ -14,7 +14,7 @@
 
 namespace yxh {
 
-template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC>
+template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC, int NBUF>
 __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p, int ntiles, int ntn, int nwork,
                                                                     int ps, int l0, int l1) {
     static_assert(sizeof(T) == 2, "16-bit operands");
@@ -24,10 +24,14 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
     constexpr int WTM = TM / WM, FC = WTM / 16;
     constexpr int C16 = CIN / 8;
     // LDS image bound: two regions of TM pixels x ps 16-byte slots (ps padded up to 2 x odd,
-    // at most 3 slots per region), each rounded up to whole 1 KiB wave-loads
-    constexpr int LMAX = (TM * (C16 + 6) + 63) / 64 + 2, GB = (LMAX + NW - 1) / NW, HBYTES = LMAX * 1024;
+    // at most 3 slots per region), each rounded up to whole 1 KiB wave-loads; a buffer holds
+    // GB wave-loads of every wave (the ones past the image land zeros in the padding), so each
+    // wave issues exactly GB DMAs per tile and the pipeline's vmcnt waits are constants.
+    // NBUF buffers: NBUF - 1 tiles' rows in flight while one computes
+    constexpr int LMAX = (TM * (C16 + 6) + 63) / 64 + 2, GB = (LMAX + NW - 1) / NW, HBYTES = GB * NW * 1024;
     constexpr int RBYTES = WK > 1 ? WN * WM * FR * FC * (WK - 1) * 1024 : 0;
-    constexpr int SMEM = 2 * HBYTES + RBYTES;
+    constexpr int SMEM = NBUF * HBYTES + RBYTES;
+    static_assert(NBUF >= 2 && (NBUF - 1) * GB <= 63, "DMA pipeline depth");
     constexpr int FCO = (FC + WK - 1) / WK;
     constexpr int PD = FR * FC >= 8 ? 1 : FR * FC >= 4 ? 2 : 3;  // fragment-read distance in K steps
     static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0, "tile");
@@ -69,12 +73,14 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
                                      (uint32_t)((long long)M * (p.nsrc > 1 ? p.scs[1] : p.scs[0]) * 2));
     const int scs0 = p.scs[0], scs1 = p.nsrc > 1 ? p.scs[1] : 0;
 
+    // tile t's rows into buffer kb; a tile past the end (t >= ntiles) loads zeros, so the count
+    // of DMAs per wave and tile is always GB
     auto issue = [&](int t, int kb) {
         const int m0 = t * TM;
 #pragma unroll
         for (int i = 0; i < GB; ++i) {
             const int L = wave + NW * i;
-            if (L < l0 + l1) {
+            {
                 const int g = geo[i];
                 const int m = m0 + (g & 0xffff);
                 const bool ok = g >= 0 && m < M;
@@ -91,10 +97,10 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
         }
     };
 
-    // prologue: the first two tiles' rows go out before the weights, which then load in the
-    // order the first tile's K steps consume them (tile_step's FIRST waits for the rows only)
-    issue(tile, 0);
-    if (tile + nwork < ntiles) issue(tile + nwork, 1);
+    // prologue: the first NBUF tiles' rows go out before the weights, which then load in the
+    // order the first tile's K steps consume them (tile_step's FIRST waits for tile 0 only)
+#pragma unroll
+    for (int q = 0; q < NBUF; ++q) issue(tile + q * nwork, q);
     uint4 a[FR][WCB];
 #pragma unroll
     for (int c = 0; c < WCB; ++c)
@@ -118,12 +124,9 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
         const int n = n0 + wn * WTN + i * 16 + fq * 4;
         const bool ok = j < FC && m < M && n < cout;
         const int od = ok ? (m * dcs + n) * 2 : (int)dma::kOob;
-        T t[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float x = ap[i][o][q] + bias[i][q];
-            t[q] = from_f32<T>(silu ? yxh::silu<false>(x) : x);
-        }
+        const f32x4 x = ap[i][o] + f32x4{bias[i][0], bias[i][1], bias[i][2], bias[i][3]};
+        const f32x4 v = silu ? yxh::silu4(x) : x;
+        T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
         u32x2 u;
         __builtin_memcpy(&u, t, 8);
         __builtin_amdgcn_raw_buffer_store_b64(u, dsrd, od, 0, 0);
@@ -134,13 +137,19 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
     auto tile_step = [&](const int t, const int k, const int tprev, auto epi, auto first) -> int {
         constexpr bool EPI = decltype(epi)::value;
         constexpr bool FIRST = decltype(first)::value;
-        const int kb = k & 1;
+        const int kb = k % NBUF;
         const int next = t + nwork;
-        // FIRST: vmcnt retires in issue order and the rows went out before the weight loads
-        if constexpr (FIRST) dma::wait_vm<(FR * WCB < 63 ? FR * WCB : 63)>();
-        else dma::wait_vm<0>();
+        // vmcnt retires in issue order.  FIRST: tiles 1 .. NBUF-1 and the weights went out after
+        // tile 0's rows; later steps: at least tiles k+1 .. k+NBUF-2 did (GB DMAs each)
+        if constexpr (FIRST) {
+            constexpr int younger = (NBUF - 1) * GB + FR * WCB;
+            dma::wait_vm<(younger < 63 ? younger : 63)>();
+        } else {
+            dma::wait_vm<(NBUF - 2) * GB>();
+        }
         dma::barrier();
-        if (!FIRST && next < ntiles) issue(next, kb ^ 1);
+        // the buffer of tile k-1 is free: tile k + NBUF - 1 into it (the prologue issued tile NBUF-1)
+        if (!FIRST) issue(t + (NBUF - 1) * nwork, (k + NBUF - 1) % NBUF);
 
         f32x4 acc[FR][FC];
 #pragma unroll
@@ -226,9 +235,10 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
     for (int o = 0; o < FCO; ++o)
 #pragma unroll
         for (int i = 0; i < FR; ++i) epi_piece(cur, accp, o, i);
+    dma::wait_vm<0>();  // the zero-filling DMAs of tiles past the end land before the LDS is released
 }
 
-template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC = 1>
+template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC = 1, int NBUF = 2>
 static int launch_ws1(const ConvParams& p, hipStream_t st) {
     if (p.cin != CIN) {
         set_error("conv_ws1 variant built for %d input channels", CIN);
@@ -259,7 +269,7 @@ static int launch_ws1(const ConvParams& p, hipStream_t st) {
     const long long ntiles = (M + TM - 1) / TM;
     const int ntn = (p.cout + TN - 1) / TN;
     const int nwork = (int)std::min<long long>(ntiles, std::max(1, p.cus * BPC / ntn));
-    hipLaunchKernelGGL((conv_ws1<T, CIN, TM, TN, WN, WK, WM, BPC>), dim3((unsigned)(nwork * ntn)),
+    hipLaunchKernelGGL((conv_ws1<T, CIN, TM, TN, WN, WK, WM, BPC, NBUF>), dim3((unsigned)(nwork * ntn)),
                        dim3(64 * WN * WK * WM), 0, st, p, (int)ntiles, ntn, nwork, ps, l0, l1);
     YXH_CHECK_LAUNCH("conv_ws1 launch");
     return YXH_OK;
@@ -279,6 +289,16 @@ static int ws1_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 8: return launch_ws1<T, 512, 64, 64, 2, 2, 2, 1>(p, st);
         case 9: return launch_ws1<T, 1024, 32, 64, 2, 2, 2, 1>(p, st);
         case 10: return launch_ws1<T, 256, 128, 128, 4, 1, 2, 1>(p, st);
+        // deeper row pipelines (3-4 buffers: 2-3 tiles in flight), smaller tiles: the 1x1s were
+        // latency-bound at one tile in flight (2-5x a copy of the same bytes, tools/pw_probe.py)
+        case 11: return launch_ws1<T, 64, 64, 64, 2, 1, 2, 2, 4>(p, st);
+        case 12: return launch_ws1<T, 128, 64, 128, 4, 1, 1, 1, 4>(p, st);
+        case 13: return launch_ws1<T, 256, 32, 128, 4, 1, 1, 1, 4>(p, st);
+        case 14: return launch_ws1<T, 256, 64, 128, 4, 1, 1, 1, 3>(p, st);
+        case 15: return launch_ws1<T, 512, 32, 128, 4, 1, 1, 1, 3>(p, st);
+        case 16: return launch_ws1<T, 512, 32, 64, 2, 2, 2, 1, 3>(p, st);
+        case 17: return launch_ws1<T, 1024, 16, 64, 4, 1, 1, 1, 4>(p, st);
+        case 18: return launch_ws1<T, 64, 128, 64, 2, 1, 2, 1, 3>(p, st);
         default: set_error("conv_ws1 tile id %d", id); return YXH_EINVAL;
     }
 }

@@ -291,12 +291,11 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
                 const bool valid = interior || ((unsigned)gy < (unsigned)p.OH1 && (unsigned)gx < (unsigned)p.OW1);
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
+                    const f32x4 y =
+                        yxh::silu4(acc[i][jj] + f32x4{bias1[i][0], bias1[i][1], bias1[i][2], bias1[i][3]});
                     T t[4];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float y = yxh::silu<false>(acc[i][jj][r] + bias1[i][r]);
-                        t[r] = from_f32<T>(valid ? y : 0.0f);
-                    }
+                    for (int r = 0; r < 4; ++r) t[r] = from_f32<T>(valid ? y[r] : 0.0f);
                     uint2 u;
                     __builtin_memcpy(&u, t, 8);
                     if (pix < kS2NSP) *(uint2*)(simg + (sy * HXP + sx) * PSB + (i * 16 + fq * 4) * 2) = u;
@@ -339,12 +338,9 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
 #pragma unroll
                 for (int i = 0; i < FR2; ++i) {
                     const int n = wn * 32 + i * 16 + fq * 4;
-                    T t[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float x = acc2[i][j][r] + bias2[i][r];
-                        t[r] = from_f32<T>(yxh::silu<false>(x));
-                    }
+                    const f32x4 y =
+                        yxh::silu4(acc2[i][j] + f32x4{bias2[i][0], bias2[i][1], bias2[i][2], bias2[i][3]});
+                    T t[4] = {from_f32<T>(y[0]), from_f32<T>(y[1]), from_f32<T>(y[2]), from_f32<T>(y[3])};
                     uint2 u;
                     __builtin_memcpy(&u, t, 8);
                     *(uint2*)(dst + (long long)(oy * p.OW + ox) * p.dst_cs + n) = u;
@@ -358,9 +354,9 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
 #pragma unroll
                 for (int i = 0; i < FR2; ++i) {
                     const int n = wn * 32 + i * 16 + fq * 4;
-                    T t[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) t[r] = from_f32<T>(yxh::silu<false>(acc2[i][j][r] + bias2[i][r]));
+                    const f32x4 y =
+                        yxh::silu4(acc2[i][j] + f32x4{bias2[i][0], bias2[i][1], bias2[i][2], bias2[i][3]});
+                    T t[4] = {from_f32<T>(y[0]), from_f32<T>(y[1]), from_f32<T>(y[2]), from_f32<T>(y[3])};
                     uint2 u;
                     __builtin_memcpy(&u, t, 8);
                     *(uint2*)(ybuf + pl * ZRS + n * 2) = u;
@@ -386,10 +382,9 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
                 }
 #pragma unroll
                 for (int g = 0; g < 2; ++g) {
-                    T t[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        t[r] = from_f32<T>(yxh::silu<false>(acc3[g][r] + b3l[wave * 16 + fq * 4 + r]));
+                    const float* bb = b3l + wave * 16 + fq * 4;
+                    const f32x4 y = yxh::silu4(acc3[g] + f32x4{bb[0], bb[1], bb[2], bb[3]});
+                    T t[4] = {from_f32<T>(y[0]), from_f32<T>(y[1]), from_f32<T>(y[2]), from_f32<T>(y[3])};
                     uint2 u;
                     __builtin_memcpy(&u, t, 8);
                     *(uint2*)(zbuf + ((f0 + g) * 16 + frow) * ZRS + (wave * 16 + fq * 4) * 2) = u;
@@ -427,10 +422,9 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
                     f32x4 acc4 = f32x4{0.f, 0.f, 0.f, 0.f};
                     Mma<T>::run(acc4, a4, *(const uint4*)(zbuf + pl * ZRS + fq * 16));
                     const int oy = cur.oy0 + f, ox = cur.ox0 + fr;
-                    T t[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        t[r] = from_f32<T>(yxh::silu<false>(acc4[r] + b4l[(wave & 1) * 16 + fq * 4 + r]));
+                    const float* bb = b4l + (wave & 1) * 16 + fq * 4;
+                    const f32x4 y = yxh::silu4(acc4 + f32x4{bb[0], bb[1], bb[2], bb[3]});
+                    T t[4] = {from_f32<T>(y[0]), from_f32<T>(y[1]), from_f32<T>(y[2]), from_f32<T>(y[3])};
                     uint2 u;
                     __builtin_memcpy(&u, t, 8);
                     if (oy < p.OH && ox < p.OW)

@@ -34,6 +34,19 @@ __device__ __forceinline__ float silu(float v) {
     return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.4426950408889634f));
 }
 
+// SiLU of 4 values: the operations of silu<false> (so bit-identical results) on a vector, which
+// gfx950 issues as packed-fp32 pairs (v_pk_mul_f32 / v_pk_add_f32): half the non-transcendental
+// issue slots of four scalar silu calls -- the epilogues of the 1x1 / stem kernels are VALU-heavy
+__device__ __forceinline__ f32x4 silu4(f32x4 v) {
+    const f32x4 t = v * -1.4426950408889634f;
+    f32x4 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y), __builtin_amdgcn_exp2f(t.z),
+               __builtin_amdgcn_exp2f(t.w)};
+    e = e + 1.0f;
+    const f32x4 r = {__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y), __builtin_amdgcn_rcpf(e.z),
+                     __builtin_amdgcn_rcpf(e.w)};
+    return v * r;
+}
+
 template <bool PRECISE = false>
 __device__ __forceinline__ float apply_act(float v, int act) {
     switch (act) {

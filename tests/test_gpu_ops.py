@@ -1005,9 +1005,10 @@ WS1_GEOMS = [  # sources (channels, buffer channels, channel offset), cout, H, W
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("geom", WS1_GEOMS)
 def test_conv_ws1_1x1(dtype, geom):
-    """conv_ws1 (ids 201-210): weight-stationary persistent 1x1 conv over one or two dense
-    sources (channel slices of wider buffers), output into a channel slice, every variant
-    built for this cin vs torch fp32; partial last pixel tile, cout tails of the block."""
+    """conv_ws1 (ids 201-210, and 241-248: 3-4 row buffers in flight): weight-stationary
+    persistent 1x1 conv over one or two dense sources (channel slices of wider buffers), output
+    into a channel slice, every variant built for this cin vs torch fp32; partial last pixel
+    tile, cout tails of the block."""
     srcs, cout, H, W, B = geom
     cin = sum(c for c, _, _ in srcs)
     conv, bn = make_conv(cin, cout, 1, 1, seed=cin + cout)
@@ -1022,7 +1023,7 @@ def test_conv_ws1_1x1(dtype, geom):
     want = ref_conv(torch.cat(parts, 1), conv, bn, "silu")
     out = torch.zeros(B, H, W, cout + 16, dtype=dtype, device=DEV)
     ran = 0
-    for tid in range(201, 211):
+    for tid in list(range(201, 211)) + list(range(241, 249)):
         try:
             y = run_conv(bufs, conv, bn, dtype, out=out, out_coff=8, tile=2 * tid)
         except NotImplementedError as e:
