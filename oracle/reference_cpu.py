@@ -80,7 +80,8 @@ def _act(x: Tensor, act: str) -> Tensor:
 # ``stored_as(dtype)`` every BaseConv uses its BN-folded weight rounded to ``dtype`` (fp32 bias),
 # sums in fp32, and rounds its output (after the activation and any Bottleneck shortcut) to
 # ``dtype``, as the device stores every map; the head preds use rounded weights on the rounded
-# features and stay fp32.
+# features and stay fp32.  In train mode (batch-statistics BN, forward_train) it rounds the
+# input image, each conv's weight and output and each block output instead (the --fp16 step).
 _STORE: Optional[torch.dtype] = None
 
 
@@ -112,11 +113,14 @@ def base_conv(sd: SD, p: str, x: Tensor, k: int, s: int, act: str, eps: float,
                             sd[p + ".bn.running_mean"], sd[p + ".bn.running_var"], eps)
         y = _act(F.conv2d(x, _rnd(w), b, s, (k - 1) // 2, 1, groups), act)
         return _rnd(y + residual if residual is not None else y)
-    y = F.conv2d(x, sd[p + ".conv.weight"], None, s, (k - 1) // 2, 1, groups)
-    y = F.batch_norm(y, sd[p + ".bn.running_mean"], sd[p + ".bn.running_var"],
+    # train mode under stored_as (the --fp16 step): 16-bit conv operands with an fp32 sum, the
+    # conv output and the block output stored in 16 bits, BN batch statistics in fp32; autograd
+    # then differentiates through the roundings as identities (the backward itself stays fp32)
+    y = F.conv2d(x, _rnd(sd[p + ".conv.weight"]), None, s, (k - 1) // 2, 1, groups)
+    y = F.batch_norm(_rnd(y), sd[p + ".bn.running_mean"], sd[p + ".bn.running_var"],
                      sd[p + ".bn.weight"], sd[p + ".bn.bias"], bn_train, 0.03, eps)
     y = _act(y, act)
-    return y + residual if residual is not None else y
+    return _rnd(y + residual if residual is not None else y)
 
 
 def conv(sd: SD, p: str, x: Tensor, k: int, s: int, arch: Arch, bn_train: bool,
@@ -333,7 +337,7 @@ def train_outputs(sd: SD, arch: Arch, x: Tensor):
     """Train-mode head outputs (yolo_head.py:161-182, get_output_and_grid :213-231):
     (outputs [B, A, 5+C] with decoded boxes and raw logits, origin reg [B, A, 4],
     level sizes [(h, w)])."""
-    levels = head_raw(sd, arch, backbone(sd, arch, x, bn_train=True), bn_train=True)
+    levels = head_raw(sd, arch, backbone(sd, arch, _rnd(x), bn_train=True), bn_train=True)
     C = arch.num_classes
     outs, origin, hw = [], [], []
     for (reg, obj, cls), s in zip(levels, (8, 16, 32)):

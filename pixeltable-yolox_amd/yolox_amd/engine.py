@@ -110,6 +110,9 @@ class OpRec:
 _FUSE_BOTTLENECK = os.environ.get("YOLOX_AMD_FUSE_BOTTLENECK", "0") == "1"
 # 1x1 convs folded into the launch that produces their input (YOLOX_AMD_CSP_FUSION=0: separate launches)
 _CSP_FUSION = os.environ.get("YOLOX_AMD_CSP_FUSION", "1") != "0"
+# head levels whose preds ride in the cls_convs[k][1] | reg_convs[k][1] launch (conv_ws head form):
+# "0,1,2" (default) / "" (none) -- YOLOX_AMD_HEAD_FUSION
+_HEAD_FUSION = {int(v) for v in os.environ.get("YOLOX_AMD_HEAD_FUSION", "0,1,2").split(",") if v.strip()}
 # fragment-major weight copies for the weight-stationary tiles (YOLOX_AMD_WFRAG=0: row layout only)
 _WFRAG = os.environ.get("YOLOX_AMD_WFRAG", "1") != "0"
 
@@ -381,12 +384,12 @@ class PlanCtx:
         self.flops += 2.0 * self.batch * src.lh * src.lw * 2 * half * 9 * cin
         return out
 
-    def grouped2_head_fusable(self, head, src: View, train: bool) -> bool:
+    def grouped2_head_fusable(self, head, src: View, train: bool, level: int = 0) -> bool:
         """cls_convs[k][1] | reg_convs[k][1] + the level's preds + decode as ONE conv_ws head-form
         launch (yxh_conv_desc.post_weight / post_weight2): eval, 16-bit, 128 channels per group,
         65-80 classes, 16-byte level rows."""
         return (self.csp_fusion and not train and self.dtype != torch.float32 and src.ch == 256
-                and 65 <= head.num_classes <= 80)
+                and 65 <= head.num_classes <= 80 and level in _HEAD_FUSION)
 
     def conv_grouped2_head(self, ms, src: View, head, k: int, out: "OutBuffer", a_off: int, stride: int) -> None:
         """The two-group 3x3 (cls | reg, yolo_head.py:160-161) whose blocks keep their 128-channel

@@ -497,7 +497,7 @@ class YoloxHead(_Planned):
             c1, r1 = self.cls_convs[k][1], self.reg_convs[k][1]
             two = (c.buf is r.buf and c.coff == 0 and r.coff == c.ch and c.buf.c == 2 * c.ch
                    and ctx.grouped2_fusable(c1, r1, c.buf.full()))
-            if two and hasattr(ctx, "grouped2_head_fusable") and ctx.grouped2_head_fusable(self, c.buf.full(), train):
+            if two and hasattr(ctx, "grouped2_head_fusable") and ctx.grouped2_head_fusable(self, c.buf.full(), train, k):
                 # ... with the level's preds + decode riding in the same launch
                 ctx.conv_grouped2_head([c1, r1], c.buf.full(), self, k, out, a_off, self.strides[k])
                 for rec in ctx.ops[n0:]:

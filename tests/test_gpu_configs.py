@@ -17,10 +17,10 @@ configs[3]  yolox_l 640 fp16 batch 16 (bench plan): all 16 images vs the oracle'
             same output.
 configs[4]  yolox_x 1280 --fp16 train: on-device SimOTA at A = 33600 anchors with up to
             120 GTs exact vs the oracle (fg mask, matched GT, num_fg; IoUs to fp32
-            rounding) plus the loss values; a yolox_x 1280 batch-1 train step in fp32 whose six
-            losses (rel 1e-3) and named parameter gradients (1e-3 of the tensor's max) match
-            the oracle's autograd; and the same step under fp16 autocast against the same
-            oracle with the fp16 bound stated in the test.
+            rounding) plus the loss values; a yolox_x 1280 train step at the per-GPU batch of
+            -d 8 -b 64 (8 images) in fp32 whose losses (rel 1e-3) and named parameter gradients
+            (1e-3 of the tensor's max) match the oracle's autograd; and the --fp16 step (batch 2)
+            against the same oracle within bounds derived from the oracle run with fp16 storage.
 """
 import os
 
@@ -276,39 +276,73 @@ GRAD_NAMES = ("backbone.backbone.stem.conv.conv.weight", "backbone.backbone.dark
               "head.reg_preds.1.weight", "head.obj_preds.2.bias", "head.stems.2.bn.weight")
 
 
-def test_configs4_yolox_x_1280_train_step_vs_oracle(oracle, monkeypatch):
-    """configs[4]'s model and image size (yolox_x, 1280x1280, up to 120 labels), batch 1:
-    fp32 losses within 1e-3 of the oracle (north_star tolerance) and named gradients within
-    1e-3 of each tensor's max; then the --fp16 (autocast) step against the same oracle:
-    losses within 2e-2 relative, gradients within 0.15 of each tensor's max (fp16 operands
-    with fp32 accumulation through ~100 layers; bound measured, not derived: the stem
-    weight's gradient, at the end of the reverse pass, is the worst at 0.091)."""
+def test_configs4_yolox_x_1280_train_step_fp32_batch8_vs_oracle(oracle, monkeypatch):
+    """configs[4]'s model and image size (yolox_x, 1280x1280, up to 120 labels) at its per-GPU
+    batch (-d 8 -b 64: 8 images per rank; the loss is per rank, trainer.py:168-169): fp32 losses
+    within 1e-3 of the oracle (north_star tolerance) and named gradients within 1e-3 of each
+    tensor's max.  The oracle's fp32 autograd at batch 8 holds ~25 GB of host memory and runs
+    ~1 min on the box's 16 threads."""
     from yolox_amd.models import YoloxModule
     from yolox_amd.weights import synthetic_images, synthetic_labels
+    B = 8
     m = YoloxModule.synthetic("yolox_x", seed=0, device="cuda").train()
-    x = torch.from_numpy(synthetic_images(1, 1280, 1280, seed=5)).permute(0, 3, 1, 2).float()
-    labels = torch.from_numpy(synthetic_labels(1, 1280, 1280, max_gt=120, seed=6))
+    x = torch.from_numpy(synthetic_images(B, 1280, 1280, seed=5)).permute(0, 3, 1, 2).float()
+    labels = torch.from_numpy(synthetic_labels(B, 1280, 1280, max_gt=120, seed=6))
+    labels[0, :120, 0] = torch.arange(120) % 80  # image 0 at the 120-label cap
+    g = torch.Generator().manual_seed(7)
+    labels[0, :120, 1:3] = torch.rand(120, 2, generator=g) * 1080 + 100
+    labels[0, :120, 3:5] = torch.rand(120, 2, generator=g) * 300 + 20
     out, spp_in = _device_train_step(monkeypatch, m, x, labels)
     grads = {n: p.grad.cpu().clone() for n, p in m.named_parameters() if n in GRAD_NAMES}
     ref, sdo = _oracle_train_step(oracle, monkeypatch, m, "yolox_x", x, labels, spp_in)
     for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss", "num_fg"):
         assert float(out[k]) == pytest.approx(float(ref[k]), rel=1e-3, abs=1e-6), k
     assert float(out["num_fg"]) > 0
+    worst = []
     for name in GRAD_NAMES:
         g, gr = grads[name], sdo[name].grad
         e = float((g - gr).abs().max() / (gr.abs().max() + 1e-12))
+        worst.append((e, name))
         assert e < 1e-3, (name, e)
-    # --fp16: same module, autocast selects fp16 compute (trainer.py:100-104)
-    out16, _ = _device_train_step(monkeypatch, m, x, labels, torch.float16)
+    print("configs4 fp32 batch 8: worst gradient rel err", max(worst))
+
+
+def test_configs4_yolox_x_1280_train_step_fp16_derived_bound(oracle, monkeypatch):
+    """The --fp16 (autocast) step of configs[4] (yolox_x 1280, batch 2) against the oracle's fp32
+    autograd, within bounds DERIVED from the oracle itself run with 16-bit storage
+    (oracle.stored_as(float16) in train mode: fp16 image, conv weights, conv outputs and block
+    outputs, fp32 sums and BN statistics): each loss and each named gradient may be off the fp32
+    oracle by at most FACTOR x the emulation's own distance from it (+ 1e-3 of the tensor's max,
+    the fp32 noise floor).  The factor covers what the emulation does not model -- 16-bit
+    backward maps and the device's summation order; measured on MI355X (round 4, printed with
+    -s): see the assertion message."""
+    from yolox_amd.models import YoloxModule
+    from yolox_amd.weights import synthetic_images, synthetic_labels
+    FACTOR = 3.0
+    m = YoloxModule.synthetic("yolox_x", seed=0, device="cuda").train()
+    x = torch.from_numpy(synthetic_images(2, 1280, 1280, seed=5)).permute(0, 3, 1, 2).float()
+    labels = torch.from_numpy(synthetic_labels(2, 1280, 1280, max_gt=120, seed=6))
+    out16, spp_in = _device_train_step(monkeypatch, m, x, labels, torch.float16)
+    grads = {n: p.grad.cpu().float().clone() for n, p in m.named_parameters() if n in GRAD_NAMES}
+    for n, p in m.named_parameters():
+        assert torch.isfinite(p.grad).all(), n
+    ref, sdo = _oracle_train_step(oracle, monkeypatch, m, "yolox_x", x, labels, spp_in)
+    ref_grads = {n: sdo[n].grad.clone() for n in GRAD_NAMES}
+    with oracle.stored_as(torch.float16):
+        emu, sde = _oracle_train_step(oracle, monkeypatch, m, "yolox_x", x, labels, spp_in)
+    stats = {}
     for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss"):
-        v = float(out16[k])
-        assert np.isfinite(v) and v == pytest.approx(float(ref[k]), rel=2e-2), k
-    for name, p in m.named_parameters():
-        assert torch.isfinite(p.grad).all(), name
-        if name in GRAD_NAMES:
-            gr = sdo[name].grad
-            e = float((p.grad.cpu().float() - gr).abs().max() / (gr.abs().max() + 1e-12))
-            assert e < 0.15, (name, e)
+        r, d_dev, d_emu = float(ref[k]), abs(float(out16[k]) - float(ref[k])), abs(float(emu[k]) - float(ref[k]))
+        stats[k] = (d_dev / abs(r), d_emu / abs(r))
+        assert d_dev <= FACTOR * d_emu + 1e-3 * abs(r), (k, stats[k])
+    for name in GRAD_NAMES:
+        gr = ref_grads[name]
+        scale = float(gr.abs().max()) + 1e-12
+        d_dev = float((grads[name] - gr).abs().max()) / scale
+        d_emu = float((sde[name].grad - gr).abs().max()) / scale
+        stats[name] = (d_dev, d_emu)
+        assert d_dev <= FACTOR * d_emu + 1e-3, (name, stats[name], stats)
+    print("configs4 fp16 (dev, emulation) distances from the fp32 oracle:", stats)
 
 
 def test_configs0_yolox_tiny_416_single_image(golden, oracle, tmp_path):
