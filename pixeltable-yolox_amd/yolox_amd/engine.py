@@ -110,9 +110,12 @@ class OpRec:
 _FUSE_BOTTLENECK = os.environ.get("YOLOX_AMD_FUSE_BOTTLENECK", "0") == "1"
 # 1x1 convs folded into the launch that produces their input (YOLOX_AMD_CSP_FUSION=0: separate launches)
 _CSP_FUSION = os.environ.get("YOLOX_AMD_CSP_FUSION", "1") != "0"
-# head levels whose preds ride in the cls_convs[k][1] | reg_convs[k][1] launch (conv_ws head form):
-# "0,1,2" (default) / "" (none) -- YOLOX_AMD_HEAD_FUSION
-_HEAD_FUSION = {int(v) for v in os.environ.get("YOLOX_AMD_HEAD_FUSION", "0,1,2").split(",") if v.strip()}
+# head levels whose preds ride in the cls_convs[k][1] | reg_convs[k][1] launch (conv_ws head form),
+# YOLOX_AMD_HEAD_FUSION="0,1,2" / "2" / ...; default none: measured on MI355X (round 4, one box,
+# profiles/r04/head_fusion_ab.txt) the bench forward is 1.693 ms with all three levels fused,
+# 1.681 with levels 0 + 2, 1.679 with level 2 and 1.678 with none -- the head-form tile runs its
+# conv ~45 us slower at level 0 than the plain two-group tile, which eats the head_pred launch
+_HEAD_FUSION = {int(v) for v in os.environ.get("YOLOX_AMD_HEAD_FUSION", "").split(",") if v.strip()}
 # fragment-major weight copies for the weight-stationary tiles (YOLOX_AMD_WFRAG=0: row layout only)
 _WFRAG = os.environ.get("YOLOX_AMD_WFRAG", "1") != "0"
 

@@ -123,7 +123,8 @@ def test_planner_topology_and_flops(name, hw, gflop, anchors):
     # ... and with 128-channel head convs (yolox_s) each level's preds ride in its two-group
     # cls_convs[k][1] | reg_convs[k][1] launch instead (conv_ws head form)
     n_head_post = sum(1 for o in ctx.ops if o.args.get("head_post") is not None)
-    assert n_head_post == (3 if name == "yolox_s" else 0)
+    from yolox_amd import engine as E  # YOLOX_AMD_HEAD_FUSION: the levels planned in the head form
+    assert n_head_post == (len(E._HEAD_FUSION & {0, 1, 2}) if name == "yolox_s" else 0)
     if name in ("yolox_s", "yolox_l"):  # head widths 128 / 256 (yolox_x: 320, unfused)
         assert heads + n_head_post == 3
     # ... and a 16-bit plan folds each fusable Bottleneck's conv1 into its 3x3 (one op)

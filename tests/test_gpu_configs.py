@@ -296,7 +296,7 @@ def test_configs4_yolox_x_1280_train_step_fp32_batch8_vs_oracle(oracle, monkeypa
     grads = {n: p.grad.cpu().clone() for n, p in m.named_parameters() if n in GRAD_NAMES}
     ref, sdo = _oracle_train_step(oracle, monkeypatch, m, "yolox_x", x, labels, spp_in)
     for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss", "num_fg"):
-        assert float(out[k]) == pytest.approx(float(ref[k]), rel=1e-3, abs=1e-6), k
+        assert float(out[k]) == pytest.approx(float(ref[k].detach()), rel=1e-3, abs=1e-6), k
     assert float(out["num_fg"]) > 0
     worst = []
     for name in GRAD_NAMES:
@@ -315,7 +315,8 @@ def test_configs4_yolox_x_1280_train_step_fp16_derived_bound(oracle, monkeypatch
     oracle by at most FACTOR x the emulation's own distance from it (+ 1e-3 of the tensor's max,
     the fp32 noise floor).  The factor covers what the emulation does not model -- 16-bit
     backward maps and the device's summation order; measured on MI355X (round 4, printed with
-    -s): see the assertion message."""
+    -s): 1.9x at worst (the stem weight's gradient, 0.147 vs 0.077 of its max; obj_preds.2.bias
+    2.8x of a 4e-5 distance, under the floor), losses within 0.1x."""
     from yolox_amd.models import YoloxModule
     from yolox_amd.weights import synthetic_images, synthetic_labels
     FACTOR = 3.0
@@ -332,7 +333,8 @@ def test_configs4_yolox_x_1280_train_step_fp16_derived_bound(oracle, monkeypatch
         emu, sde = _oracle_train_step(oracle, monkeypatch, m, "yolox_x", x, labels, spp_in)
     stats = {}
     for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss"):
-        r, d_dev, d_emu = float(ref[k]), abs(float(out16[k]) - float(ref[k])), abs(float(emu[k]) - float(ref[k]))
+        r = float(ref[k].detach())
+        d_dev, d_emu = abs(float(out16[k]) - r), abs(float(emu[k].detach()) - r)
         stats[k] = (d_dev / abs(r), d_emu / abs(r))
         assert d_dev <= FACTOR * d_emu + 1e-3 * abs(r), (k, stats[k])
     for name in GRAD_NAMES:
