@@ -168,6 +168,37 @@ class YoloxConfig:
         sampler = InfiniteSampler(len(ds), seed=seed)
         return MosaicBatches(ds, sampler, batch_size)
 
+    def get_eval_loader(self, batch_size: int, is_distributed: bool, dataset=None, **kwargs):
+        """config.py:363-382 over any ``pull_item`` detection dataset with ``.coco`` (the ground
+        truth: a COCO json dict or pycocotools COCO) and ``.class_ids``: (imgs, targets, info_imgs,
+        ids) batches letterboxed to test_size on the device (ValTransform = yxh_letterbox_batch);
+        distributed: batch_size // world per rank over the rank's contiguous-strided shard (the
+        DistributedSampler without its padding duplicates).  COCO dataset readers are out of scope
+        (no datasets offline): ``dataset`` is required."""
+        from .evaluators.coco_evaluator import EvalLoader
+        if dataset is None:
+            raise NotImplementedError("COCO dataset readers are out of scope: pass dataset= (pull_item, coco, "
+                                      "class_ids)")
+        rank, world = 0, 1
+        if is_distributed:
+            import torch.distributed as dist
+            rank, world = dist.get_rank(), dist.get_world_size()
+            batch_size = batch_size // world
+        return EvalLoader(dataset, batch_size, self.test_size, rank, world)
+
+    def get_evaluator(self, batch_size: int, is_distributed: bool, testdev: bool = False, legacy: bool = False,
+                      dataset=None):
+        """config.py:384-395."""
+        from .evaluators import CocoEvaluator
+        return CocoEvaluator(dataloader=self.get_eval_loader(batch_size, is_distributed, dataset=dataset,
+                                                             testdev=testdev, legacy=legacy),
+                             img_size=self.test_size, confthre=self.test_conf, nmsthre=self.nmsthre,
+                             num_classes=self.num_classes, testdev=testdev)
+
+    def eval(self, model, evaluator, is_distributed: bool, half: bool = False, return_outputs: bool = False):
+        """config.py:403-404."""
+        return evaluator.evaluate(model, is_distributed, half, return_outputs=return_outputs)
+
     def random_resize(self, data_loader, epoch: int, rank: int, is_distributed: bool):
         """config.py:275-294: rank 0 draws the next multiscale input size (multiples of 32
         around input_size) and broadcasts it; every rank returns the same (h, w)."""
