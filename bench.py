@@ -166,14 +166,17 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def load_traffic(model, batch, size, dtype):
+def load_traffic(model, batch, size, dtype, workload="infer"):
+    """The latest committed PMC traffic record (profiles/traffic_*.json, by file name) of this
+    workload: tools/traffic.py (forward) or tools/traffic_train.py (training step)."""
     best = None
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "traffic_*.json"))):
         try:
             d = json.load(open(path))
         except Exception:
             continue
-        if (d.get("model"), d.get("batch"), d.get("size"), d.get("dtype")) == (model, batch, size, dtype):
+        if (d.get("workload", "infer"), d.get("model"), d.get("batch"), d.get("size"), d.get("dtype")) == \
+                (workload, model, batch, size, dtype):
             best = d
     return best
 
@@ -357,6 +360,7 @@ def main_train(args, world, rank):
     achieved = flops / (gpu_ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if amp is not None else PEAK_F32_TFLOPS
     idx = config_index(args)
+    ttr = load_traffic(args.model, B, S, args.dtype, workload="train")
     result = {
         "metric": metric_name(args),
         "value": round(world * B * args.steps / dt_max, 2),
@@ -379,9 +383,11 @@ def main_train(args, world, rank):
                    "issue": "hipGraph replay" if cap is not None else "eager"},
         "roofline": {"kernel": "whole step (conv fwd/dgrad/wgrad dominate; HIP events around each step)",
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "frac": round(achieved / peak, 4),
+                     "traffic": None if ttr is None else ttr["hbm_bytes_per_step"],
                      "algorithmic_flops_per_launch": flops, "step_gpu_ms": round(gpu_ms, 3)},
         "last_loss": round(loss, 4),
+        **({"traffic_source": ttr.get("source")} if ttr is not None else {}),
         "host_issue_ms_per_step": round(host_s / args.steps * 1e3, 3),
     }
     if not args.no_cpu_baseline and world == 1:
