@@ -354,9 +354,12 @@ int yxh_graph_create_dag(const yxh_op* ops, int32_t n, const int32_t* dep_off, c
 
 int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, const int32_t* dep_off,
                            const int32_t* deps, int32_t nlanes, void* stream, void** graph_exec) {
-    // proven limit: 4 capture streams (7 segfaulted in the join / end of capture, DESIGN.md
-    // §11); more concurrency goes through yxh_graph_create_dag
-    constexpr int kMaxLanes = 4;
+    // round 2 capped this at 4 after a 7-stream capture segfaulted in its join; round 4 could not
+    // reproduce it: the same capture pattern with plain kernels holds 4-12 lanes, with and
+    // without lanes that carry no op (tools/lane_capture_probe.hip, profiles/r04/lanes_probe.txt),
+    // and a plan with 8 chunk lanes replays bit-exact (tests/test_gpu_model.py); the round-2 op
+    // list still captured hipMemsetAsync nodes, which round 4 showed break captured graphs
+    constexpr int kMaxLanes = 16;
     YXH_CHECK_ARG(graph_exec && (ops || n == 0) && lanes && dep_off, "null argument");
     YXH_CHECK_ARG(nlanes >= 1 && nlanes <= kMaxLanes, "nlanes %d", nlanes);
     YXH_CHECK_ARG(dep_off[0] == 0, "dep_off[0] must be 0");

@@ -1101,7 +1101,7 @@ class Plan:
             off, deps = self._dag_arrays()
             N.check(self.lib.yxh_graph_create_dag(self._ops, len(self._ops), off, deps, N.stream_ptr(self.device),
                                                   C.byref(g)), "graph capture (dag)")
-        elif self.graph_mode == "lanes" and self.parallel_chunks and self.nchunks <= 4:
+        elif self.graph_mode == "lanes" and self.parallel_chunks and self.nchunks <= 16:
             # one capture stream per chunk: independent chains, joined at the end
             lanes = [c for c in range(self.nchunks) for _ in self.ctx.ops]
             off, deps = self._dag_arrays()

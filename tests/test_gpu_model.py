@@ -201,6 +201,23 @@ def test_graph_forms_match_single_stream_graph():
     assert all(torch.equal(o, outs[0]) for o in outs)
 
 
+def test_eight_chunk_lanes_capture_matches_whole_batch():
+    """parallel_chunks with 8 chunks captures 8 lanes (one stream per chunk: yxh_graph_create_lanes
+    beyond round 2's cap of 4, whose 7-stream crash round 4 could not reproduce) and replays the
+    whole-batch output bit for bit, twice."""
+    from yolox_amd import _native as N
+    from yolox_amd.engine import Plan
+    from yolox_amd.weights import synthetic_images
+    m = model("yolox_s", torch.bfloat16)
+    x = torch.from_numpy(synthetic_images(8, 128, 128, seed=8)).cuda()
+    a = Plan(m, 8, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8).run(x).clone()
+    p = Plan(m, 8, 128, 128, torch.bfloat16, "cuda", N.NHWC, torch.uint8, chunk=1, parallel_chunks=True)
+    p.graph_mode = "lanes"
+    p.static_input().copy_(x)
+    assert torch.equal(p.replay().clone(), a)
+    assert torch.equal(p.replay().clone(), a)
+
+
 def test_fused_stem_s2_plan_matches_unfused_plan():
     """The planned forward with Focus stem + dark2[0] as one yxh_stem_s2 launch (uint8 NHWC
     input, the bench / processor form) vs the same plan with the two as separate launches:
