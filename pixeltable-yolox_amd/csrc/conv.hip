@@ -251,6 +251,17 @@ __global__ __launch_bounds__(256) void focus_pack(const TI* img, int layout, int
 // ---------------------------------------------------------------- SPP
 template <typename T>
 __device__ __forceinline__ uint4 vmax(uint4 a, uint4 b) {
+    if constexpr (__is_same(T, bf16)) {
+        // bf16 maps to order-preserving int16 keys (spp_key) in LDS: 4 packed-int16 max per chunk
+        // instead of 8 converts + compares + selects
+        typedef short s2 __attribute__((ext_vector_type(2)));
+        uint4 r;
+        r.x = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2, a.x), __builtin_bit_cast(s2, b.x)));
+        r.y = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2, a.y), __builtin_bit_cast(s2, b.y)));
+        r.z = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2, a.z), __builtin_bit_cast(s2, b.z)));
+        r.w = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2, a.w), __builtin_bit_cast(s2, b.w)));
+        return r;
+    }
     constexpr int EPC = Chunk<T>::N;
     T x[EPC], y[EPC];
     __builtin_memcpy(x, &a, 16);
@@ -260,6 +271,18 @@ __device__ __forceinline__ uint4 vmax(uint4 a, uint4 b) {
     uint4 r;
     __builtin_memcpy(&r, x, 16);
     return r;
+}
+
+// bf16 <-> order-preserving int16 key, both halves of a dword: a negative value (sign set) has its
+// 15 magnitude bits flipped, so signed int16 order = float order (-0 sorts just below +0; NaN
+// payloads sort outside every finite value); the map is its own inverse
+template <typename T>
+__device__ __forceinline__ uint4 spp_key(uint4 v) {
+    if constexpr (__is_same(T, bf16)) {
+        auto k = [](uint32_t d) { return d ^ (((d >> 15) & 0x00010001u) * 0x7fffu); };
+        return make_uint4(k(v.x), k(v.y), k(v.z), k(v.w));
+    }
+    return v;
 }
 
 // One block per (CPB consecutive 16-byte channel chunks, image): horizontal 5/9/13 maxima
@@ -280,7 +303,7 @@ __global__ __launch_bounds__(256) void spp_maxpool(T* buf, int H, int W, int C, 
     T* base = buf + blockIdx.y * bs;
     for (int q = threadIdx.x; q < N; q += blockDim.x) {
         const int px = q / CPB, ch = q - px * CPB;
-        P[q] = *(const uint4*)(base + (long long)px * cs + c0 + ch * EPC);
+        P[q] = spp_key<T>(*(const uint4*)(base + (long long)px * cs + c0 + ch * EPC));
     }
     __syncthreads();
     for (int q = threadIdx.x; q < N; q += blockDim.x) {
@@ -326,9 +349,9 @@ __global__ __launch_bounds__(256) void spp_maxpool(T* buf, int H, int W, int C, 
             if (dn) o13 = vmax<T>(o13, H13[q + d * row]);
         }
         T* pp = base + (long long)px * cs + c0 + ch * EPC;
-        *(uint4*)(pp + C) = o5;
-        *(uint4*)(pp + 2 * C) = o9;
-        *(uint4*)(pp + 3 * C) = o13;
+        *(uint4*)(pp + C) = spp_key<T>(o5);
+        *(uint4*)(pp + 2 * C) = spp_key<T>(o9);
+        *(uint4*)(pp + 3 * C) = spp_key<T>(o13);
     }
 }
 

@@ -218,10 +218,13 @@ def test_depthwise(dtype, s):
 @pytest.mark.parametrize("hw,B,C", [((20, 20), 2, 32), ((13, 7), 2, 32), ((40, 40), 2, 32),
                                     ((20, 20), 32, 256), ((20, 20), 64, 512)])
 def test_spp_maxpool(dtype, hw, B, C):
-    """bit-exact vs torch max_pool2d; the batch-32/64 cases take the 2- and 4-chunk blocks."""
+    """bit-exact vs torch max_pool2d; the batch-32/64 cases take the 2- and 4-chunk blocks; +-inf,
+    zeros and large negatives exercise bf16's order-preserving int16 keys."""
     n = N()
     H, W = hw
     x = torch.randn(B, C, H, W)
+    x[:, :, 0, 0], x[:, :, 1, 2], x[:, :, 2, 1] = float("-inf"), float("inf"), 0.0
+    x[:, ::3, 3, 3] = -3.0e38
     buf = torch.zeros(B, H, W, 4 * C, dtype=dtype, device=DEV)
     buf[..., :C] = nhwc(x, dtype)
     n.check(n.lib().yxh_spp_maxpool(buf.data_ptr(), n.DTYPE_CODE[dtype], B, H, W, C, 4 * C, H * W * 4 * C,
