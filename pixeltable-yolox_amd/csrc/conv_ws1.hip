@@ -14,7 +14,7 @@
 
 namespace yxh {
 
-template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC, int NBUF>
+template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC, int NBUF, bool UP0>
 __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p, int ntiles, int ntn, int nwork,
                                                                     int ps, int l0, int l1) {
     static_assert(sizeof(T) == 2, "16-bit operands");
@@ -68,7 +68,12 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
         geo[i] = st ? (hp | (ch << 16)) : -1;
     }
     const uint32_t lds0 = dma::lds_addr(smem);
-    const dma::u32x4 srd0 = dma::srd(p.sptr[0], (uint32_t)((long long)M * p.scs[0] * 2));
+    // UP0: source 0 is read through a nearest x2 upsample (yxh_src.upsample = 1: the PAFPN's
+    // upsampled lateral / reduce map in C3_p4 / C3_p3's conv1 | conv2, yolo_pafpn.py:98-112)
+    const long long src0_elems = UP0 ? (long long)(M / p.ohw) * p.sbs[0] : (long long)M * p.scs[0];
+    const dma::u32x4 srd0 = dma::srd(p.sptr[0], (uint32_t)(src0_elems * 2));
+    const int ohw = p.ohw, ow = p.out_w, sw0 = p.sw[0];
+    const long long sbs0 = p.sbs[0];
     const dma::u32x4 srd1 = dma::srd(p.nsrc > 1 ? p.sptr[1] : p.sptr[0],
                                      (uint32_t)((long long)M * (p.nsrc > 1 ? p.scs[1] : p.scs[0]) * 2));
     const int scs0 = p.scs[0], scs1 = p.nsrc > 1 ? p.scs[1] : 0;
@@ -91,7 +96,12 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
                 rs.y = __builtin_amdgcn_readfirstlane(rs.y);
                 rs.z = __builtin_amdgcn_readfirstlane(rs.z);
                 rs.w = __builtin_amdgcn_readfirstlane(rs.w);
-                const uint32_t voff = ok ? (uint32_t)((m * (r0 ? scs0 : scs1) + (g >> 16) * 8) * 2) : dma::kOob;
+                long long e = (long long)m * (r0 ? scs0 : scs1);
+                if (UP0 && r0) {  // pixel m = (b, y, x) reads source pixel (b, y / 2, x / 2)
+                    const int b = m / ohw, rr = m - b * ohw, y = rr / ow, x = rr - y * ow;
+                    e = b * sbs0 + ((long long)(y >> 1) * sw0 + (x >> 1)) * scs0;
+                }
+                const uint32_t voff = ok ? (uint32_t)((e + (g >> 16) * 8) * 2) : dma::kOob;
                 dma::load16(rs, voff, 0u, ldsa);
             }
         }
@@ -238,14 +248,19 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
     dma::wait_vm<0>();  // the zero-filling DMAs of tiles past the end land before the LDS is released
 }
 
-template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC = 1, int NBUF = 2>
+template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC = 1, int NBUF = 2, bool UP0 = false>
 static int launch_ws1(const ConvParams& p, hipStream_t st) {
     if (p.cin != CIN) {
         set_error("conv_ws1 variant built for %d input channels", CIN);
         return YXH_EUNSUPPORTED;
     }
     const int c0 = p.src0_ch, c1 = CIN - c0;
-    if (!p.src_dense || !p.dst_dense || p.dst_f32 || p.accum || p.res || p.pw1 || p.grp2 ||
+    // UP0 variants: source 0 upsampled x2 (nearest), source 1 dense; the others: dense sources
+    const bool srcs_ok = UP0 ? (p.nsrc == 2 && p.sup[0] == 1 && p.sup[1] == 0 && p.sw[0] * 2 == p.out_w &&
+                                p.sw[1] == p.out_w && p.sbs[1] == (long long)p.ohw * p.scs[1] &&
+                                (long long)(p.M / p.ohw) * p.sbs[0] * 2 < (1LL << 31))
+                             : (bool)p.src_dense;
+    if (!srcs_ok || !p.dst_dense || p.dst_f32 || p.accum || p.res || p.pw1 || p.grp2 ||
         (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) || p.cout % 8 || c0 % 32 || c1 % 32 ||
         (p.nsrc == 1) != (c1 == 0)) {
         set_error("conv_ws1: dense 1x1 over 32-channel-aligned sources, 16-bit dst, SiLU/no activation, %d input channels",
@@ -269,7 +284,7 @@ static int launch_ws1(const ConvParams& p, hipStream_t st) {
     const long long ntiles = (M + TM - 1) / TM;
     const int ntn = (p.cout + TN - 1) / TN;
     const int nwork = (int)std::min<long long>(ntiles, std::max(1, p.cus * BPC / ntn));
-    hipLaunchKernelGGL((conv_ws1<T, CIN, TM, TN, WN, WK, WM, BPC, NBUF>), dim3((unsigned)(nwork * ntn)),
+    hipLaunchKernelGGL((conv_ws1<T, CIN, TM, TN, WN, WK, WM, BPC, NBUF, UP0>), dim3((unsigned)(nwork * ntn)),
                        dim3(64 * WN * WK * WM), 0, st, p, (int)ntiles, ntn, nwork, ps, l0, l1);
     YXH_CHECK_LAUNCH("conv_ws1 launch");
     return YXH_OK;
@@ -299,6 +314,12 @@ static int ws1_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 16: return launch_ws1<T, 512, 32, 64, 2, 2, 2, 1, 3>(p, st);
         case 17: return launch_ws1<T, 1024, 16, 64, 4, 1, 1, 1, 4>(p, st);
         case 18: return launch_ws1<T, 64, 128, 64, 2, 1, 2, 1, 3>(p, st);
+        // [upsampled x2 | dense] sources: C3_p4's conv1 | conv2 (256 up + 256 @40x40 -> 256) and
+        // C3_p3's (128 up + 128 @80x80 -> 128)
+        case 19: return launch_ws1<T, 512, 32, 128, 4, 1, 1, 1, 3, true>(p, st);
+        case 20: return launch_ws1<T, 512, 64, 64, 2, 2, 2, 1, 2, true>(p, st);
+        case 21: return launch_ws1<T, 256, 64, 128, 4, 1, 1, 2, 2, true>(p, st);
+        case 22: return launch_ws1<T, 256, 32, 128, 4, 1, 1, 1, 4, true>(p, st);
         default: set_error("conv_ws1 tile id %d", id); return YXH_EINVAL;
     }
 }

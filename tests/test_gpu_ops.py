@@ -998,6 +998,35 @@ def test_conv_ws_fused_bottleneck(ch, H, W, B, shortcut, dtype):
         run_conv([(X, 0, ch, 0)], c3, bn3, dtype, tile=2 * 166, pre=(w1, b1))
 
 
+@pytest.mark.parametrize("c0,c1,cout,H,W,B", [(256, 256, 256, 40, 40, 3), (128, 128, 128, 30, 22, 2),
+                                             (256, 256, 256, 14, 10, 5)])
+def test_conv_ws1_upsampled_source(c0, c1, cout, H, W, B):
+    """conv_ws1 tiles 249-252 (round 4): a 1x1 over [nearest-x2 upsample(src0) | src1] -- the
+    PAFPN's C3_p4 / C3_p3 conv1 | conv2 over the upsampled lateral map and the backbone map
+    (yolo_pafpn.py:98-112) -- vs torch fp32; src0 a channel slice of a wider half-resolution
+    buffer."""
+    dtype = torch.bfloat16
+    conv, bn = make_conv(c0 + c1, cout, 1, 1, seed=c0 + H)
+    g = torch.Generator().manual_seed(H * W + c0)
+    x0 = torch.randn(B, c0, H // 2, W // 2, generator=g)
+    x1 = torch.randn(B, c1, H, W, generator=g)
+    buf0 = torch.zeros(B, H // 2, W // 2, c0 + 64, dtype=dtype, device=DEV)
+    buf0[..., 32:32 + c0] = nhwc(x0, dtype)
+    X1 = nhwc(x1, dtype)
+    want = ref_conv(torch.cat([F.interpolate(x0, scale_factor=2, mode="nearest"), x1], 1), conv, bn, "silu")
+    srcs = [(buf0, 32, c0, 1), (X1, 0, c1, 0)]
+    ran = 0
+    for tid in range(249, 253):
+        try:
+            y = run_conv(srcs, conv, bn, dtype, tile=2 * tid)
+        except NotImplementedError as e:
+            assert "input channels" in str(e), e
+            continue
+        close(y.permute(0, 3, 1, 2), want, dtype)
+        ran += 1
+    assert ran >= 1
+
+
 WS1_GEOMS = [  # sources (channels, buffer channels, channel offset), cout, H, W, batch
     ([(64, 64, 0)], 64, 37, 45, 3), ([(32, 64, 0), (32, 32, 0)], 64, 40, 24, 2), ([(128, 160, 16)], 128, 20, 21, 4),
     ([(128, 256, 0), (128, 128, 0)], 256, 20, 20, 2), ([(256, 256, 0)], 128, 23, 17, 3),
