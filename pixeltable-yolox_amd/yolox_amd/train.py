@@ -738,6 +738,7 @@ class CapturedTrainStep:
         # chain on MI355X: profiles/r03/train_graph.txt.)
         self.pool = None  # the first segment's private pool, shared by the later segments (CUDAGraph.pool())
         self.plan: list = []  # ("main" | "side", CUDAGraph)
+        self._empty: list = []  # captured main segments with no launch (kept alive, not replayed)
         self._keep: list = []  # conv-output gradients read by side segments: alive for the whole step
         self.main = torch.cuda.Stream(self.dev)
         self.side_stream = g._wside
@@ -770,10 +771,22 @@ class CapturedTrainStep:
         self._cur.capture_begin(pool=self.pool, capture_error_mode="global" if "global" in self._dbg else "thread_local")
 
     def _end(self) -> None:
-        self._cur.capture_end()
+        # a main segment between two weight-gradient flushes (or after the last one) may hold no
+        # launch at all: torch reports it empty; it is kept only as the pool owner, not replayed
+        import warnings
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            self._cur.capture_end()
+        empty = any("Graph is empty" in str(w.message) for w in caught)
+        for w in caught:
+            if "Graph is empty" not in str(w.message):
+                warnings.warn_explicit(w.message, w.category, w.filename, w.lineno)
         if self.pool is None:
             self.pool = self._cur.pool()
-        self.plan.append(("main", self._cur))
+        if empty:
+            self._empty.append(self._cur)
+        else:
+            self.plan.append(("main", self._cur))
         self._cur = None
 
     def side(self, pending: list) -> None:
@@ -793,7 +806,8 @@ class CapturedTrainStep:
     def _replay(self) -> None:
         caller = torch.cuda.current_stream(self.dev)
         self.main.wait_stream(caller)
-        fork = None
+        fork = torch.cuda.Event()  # a side segment ahead of every (non-empty) main one forks here
+        fork.record(self.main)
         with torch.cuda.stream(self.main):
             for (kind, gr), ev in zip(self.plan, self.events):
                 if kind == "main":
