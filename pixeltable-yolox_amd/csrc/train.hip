@@ -711,12 +711,14 @@ __global__ __launch_bounds__(64 * WN * WC) void conv_wgrad9(WgradParams p, int t
 __global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, int splits, long long ne, float* dw);
 
 // Per-split partials (yxh_wgrad_desc.workspace): the split count a launcher wants, capped so every
-// split's partial dW fits the workspace and 16 MiB (beyond that writing and summing the partials
-// costs more than the extra blocks gain); p.ws is cleared when not even one split fits (atomics).
-static long long ws_cap_splits(WgradParams& p, long long splits) {
+// split's partial dW fits the workspace and `cap_elems` floats (tiles 1-24: 16 MiB, beyond which
+// writing and summing the partials cost more than the extra blocks gained; the nine-tap 16-bit
+// tiles 25-28 hold all nine taps per split and take 64 MiB, or wide 3x3s get ~100 blocks); p.ws is
+// cleared when not even one split fits (atomics).
+static long long ws_cap_splits(WgradParams& p, long long splits, long long cap_elems = 4LL << 20) {
     if (!p.ws) return splits;
     const long long ne = (long long)p.cout * p.cin_store * p.kh * p.kw;
-    const long long cap = std::min<long long>(p.ws_elems, 4LL << 20) / ne;
+    const long long cap = std::min<long long>(p.ws_elems, cap_elems) / ne;
     if (cap < 1) {
         p.ws = nullptr;
         return splits;
@@ -1245,6 +1247,157 @@ __global__ __launch_bounds__(256) void wgrad9t_f32(WgradParams p, int nseg) {
         }
 }
 
+// bf16/f16 3x3 weight gradient with all nine taps per block (tiles 25-28): wgrad9t_f32's
+// staging -- a stage is a row segment of KP output pixels; dY[KP][TN] and the three input rows
+// X[3][(KP - 1) s + 3][TC] it reads are copied once into LDS in their natural pixel-major layout
+// (rows padded by 16 bytes) -- with the 16-bit MFMA operands (8 consecutive pixels of one channel
+// per lane) read out pixel-transposed by ds_read_b64_tr_b16.  Each lane of a transposed read
+// names its own pixel row, so tap (ky, kx)'s B operand is the X row ky * XW + p * s + kx of each
+// pixel p: stride and shift cost nothing, and dY / X are read once per stage instead of once per
+// tap (tiles 1-10 stage both operands per tap: nine reads of each).
+template <typename T, int TN, int TC, int S, int KP>
+__global__ __launch_bounds__(256, (TN * TC <= 64 * 64 && KP == 32 && S == 1) ? 2 : 1) void wgrad9t_h(WgradParams p, int nseg) {
+    constexpr int WTN = TN / 2, WTC = TC / 2, FN = WTN / 16, FC = WTC / 16;
+    // row pitches: the 8 pixel rows one 32-lane half reads (stride S apart) land on distinct
+    // 8-bank windows -- pitch / 4 an odd multiple of 8 banks (mod 64) per S rows
+    constexpr int XW = (KP - 1) * S + 3, RA = TN * 2 + 32, RB = TC * 2 + (S == 1 ? 32 : 16);
+    constexpr int ASZ = KP * RA, BSZ = 3 * XW * RB;
+    constexpr int ACH = KP * TN / 8, BCH = 3 * XW * TC / 8, AL = (ACH + 255) / 256, BL = (BCH + 255) / 256;
+    static_assert(sizeof(T) == 2 && KP % 32 == 0 && FN >= 1 && FC >= 1, "tile");
+    __shared__ __attribute__((aligned(16))) char lds[2][ASZ + BSZ];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wn = wave & 1, wc = wave >> 1;
+    // XCD-aware order: the dispatcher deals linear block ids to the 8 XCDs round-robin; the
+    // ntn x ntc blocks of one split (same pixels, so the same dY / X lines) get consecutive
+    // logical ids on one XCD and share its L2 instead of fetching the lines once per XCD
+    const int nblk = gridDim.x * gridDim.y * gridDim.z;
+    const int bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+    const int tc_ = lid % gridDim.z, tn_ = (lid / gridDim.z) % gridDim.y, split = lid / (gridDim.z * gridDim.y);
+    const int n0 = tn_ * TN, c0 = tc_ * TC;
+    const int st0 = split * p.sps, st1 = min(p.nst, st0 + p.sps);
+    const int oh = p.out_h, ow = p.out_w, cin = p.cin;
+    const T* dy = (const T*)p.dy;
+
+    uint4 ra[AL], rb[BL];
+    auto gload = [&](int st) {
+        const int seg = st % nseg, r = st / nseg;
+        const int b = r / oh, oy = r - b * oh, ox0 = seg * KP;
+#pragma unroll
+        for (int i = 0; i < AL; ++i) {
+            const int q = tid + 256 * i;
+            const int row = q / (TN / 8), col = q - row * (TN / 8);
+            const int ox = ox0 + row, n = n0 + col * 8;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (q < ACH && ox < ow && n < p.dych)
+                v = *(const uint4*)(dy + (long long)b * p.dybs + (long long)(oy * ow + ox) * p.dycs + n);
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BL; ++i) {
+            const int q = tid + 256 * i;
+            const int row = q / (TC / 8), col = q - row * (TC / 8);  // row = ty * XW + xx
+            const int ty = row / XW, xx = row - ty * XW;
+            const int iy = oy * S + ty - 1, ix = ox0 * S + xx - 1, c = c0 + col * 8;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (q < BCH && c < cin && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w) {
+                const int s = (p.nsrc > 1 && c >= p.src0_ch) ? 1 : 0;
+                const int cc = s ? c - p.src0_ch : c;
+                const int spix = p.sup[s] ? (iy >> 1) * p.sw[s] + (ix >> 1) : iy * p.sw[s] + ix;
+                v = *(const uint4*)((const T*)p.sptr[s] + (long long)b * p.sbs[s] + (long long)spix * p.scs[s] + cc);
+            }
+            rb[i] = v;
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < AL; ++i) {
+            const int q = tid + 256 * i;
+            if (q < ACH) *(uint4*)(lds[buf] + (q / (TN / 8)) * RA + (q % (TN / 8)) * 16) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BL; ++i) {
+            const int q = tid + 256 * i;
+            if (q < BCH) *(uint4*)(lds[buf] + ASZ + (q / (TC / 8)) * RB + (q % (TC / 8)) * 16) = rb[i];
+        }
+    };
+
+    f32x4 acc[9][FN][FC];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FC; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // transposed reads: lane 4q + p of a 16-lane group names pixel row q of a 4-row block and
+    // columns 4p .. 4p + 3; it receives its own column (lane % 16) over the four rows.  K slot
+    // 8g + 4h + q of a 32-pixel slab holds pixel 16h + 4g + q (any bijection serves, A and B
+    // alike): a 32-lane half's read then covers 8 consecutive pixel rows
+    const int g4 = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int colA = (wn * WTN + 4 * p4) * 2, colB = (wc * WTC + 4 * p4) * 2;
+    if (st0 < st1) {
+        gload(st0);
+        lstore(0);
+        __syncthreads();
+    }
+    int buf = 0;
+    for (int st = st0; st < st1; ++st) {
+        const bool more = st + 1 < st1;
+        if (more) gload(st + 1);
+        const char* A = lds[buf] + colA;
+        const char* Bm = lds[buf] + ASZ + colB;
+#pragma unroll
+        for (int kk = 0; kk < KP / 32; ++kk) {
+            const int pr0 = 32 * kk + 4 * g4 + q4, pr1 = pr0 + 16;
+            uint4 af[FN];
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const uint2 lo = lds_read_tr16(A + pr0 * RA + 32 * i);
+                const uint2 hi = lds_read_tr16(A + pr1 * RA + 32 * i);
+                af[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            }
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int x0 = (t / 3) * XW + pr0 * S + (t % 3), x1 = x0 + 16 * S;
+                uint4 bf[FC];
+#pragma unroll
+                for (int j = 0; j < FC; ++j) {
+                    const uint2 lo = lds_read_tr16(Bm + x0 * RB + 32 * j);
+                    const uint2 hi = lds_read_tr16(Bm + x1 * RB + 32 * j);
+                    bf[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+                }
+#pragma unroll
+                for (int i = 0; i < FN; ++i)
+#pragma unroll
+                    for (int j = 0; j < FC; ++j) Mma<T>::run(acc[t][i][j], af[i], bf[j]);
+            }
+        }
+        if (more) lstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    float* out = p.ws ? p.ws + (long long)split * p.cout * p.cin_store * 9 : p.dw;
+    const int kr = lane >> 4, kc = lane & 15;
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+            const int c = c0 + wc * WTC + 16 * j + kc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n0 + wn * WTN + 16 * i + 4 * kr + r;
+                if (n >= p.cout || c >= p.cin_store) continue;
+                float* d = out + ((long long)n * p.cin_store + c) * 9;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    if (p.ws) d[t] = acc[t][i][j][r];
+                    else unsafeAtomicAdd(d + t, acc[t][i][j][r]);
+                }
+            }
+        }
+}
+
 // dW[i] += sum over the splits of ws[split][i], in split order (deterministic)
 __global__ __launch_bounds__(256) void wgrad_reduce(const float* ws, int splits, long long ne, float* dw) {
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -1683,6 +1836,39 @@ int launch_wgrad9t_f32(WgradParams p, hipStream_t st) {
     return ws_reduce(p, splits, st);
 }
 
+template <typename T, int TN, int TC, int S, int KP>
+int launch_wgrad9t_h(WgradParams p, hipStream_t st) {
+    if constexpr (sizeof(T) != 2) {
+        set_error("wgrad tiles 25-28 (nine taps per block, transposed LDS reads) are built for bf16/f16 only");
+        return YXH_EUNSUPPORTED;
+    } else {
+        if (p.kh != 3 || p.kw != 3 || p.stride != S || p.pad != 1) {
+            set_error("wgrad tiles 25-28 (nine taps per block) need a 3x3 pad-1 conv of stride %d", S);
+            return YXH_EUNSUPPORTED;
+        }
+        // 16-byte channel chunks everywhere (conv_wgrad_launch checks the views; src0_ch too)
+        if (p.nsrc > 1 && p.src0_ch % 8) {
+            set_error("wgrad tiles 25-28: 16-byte channel chunks");
+            return YXH_EUNSUPPORTED;
+        }
+        const int nseg = (p.out_w + KP - 1) / KP;
+        const int ntn = (p.cout + TN - 1) / TN, ntc = (p.cin + TC - 1) / TC;
+        p.nst = p.B * p.out_h * nseg;
+        const long long tiles = (long long)ntn * ntc;
+        long long splits = (512 + tiles - 1) / tiles;
+        const long long max_splits = (p.nst + 3) / 4;
+        if (splits > max_splits) splits = max_splits;
+        splits = ws_cap_splits(p, splits, 16LL << 20);
+        if (splits < 1) splits = 1;
+        p.sps = (int)((p.nst + splits - 1) / splits);
+        splits = (p.nst + p.sps - 1) / p.sps;
+        YXH_CHECK_ARG(ntn < 65536 && ntc < 65536, "wgrad grid");
+        hipLaunchKernelGGL((wgrad9t_h<T, TN, TC, S, KP>), dim3((unsigned)splits, ntn, ntc), dim3(256), 0, st, p, nseg);
+        YXH_CHECK_LAUNCH("wgrad9t_h");
+        return ws_reduce(p, splits, st);
+    }
+}
+
 template <typename T>
 int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
     // default: 64 x 64 (cout x cin), 2 x 2 waves; 4 slabs (bf16: 128 pixels) per stage
@@ -1742,6 +1928,20 @@ int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
                     default: return s2 ? launch_wgrad9t_f32<64, 32, 2, 16>(p, st) : launch_wgrad9t_f32<64, 32, 1, 16>(p, st);
                 }
             }
+        case 25: case 26: case 27: case 28: {
+            const bool s2 = p.stride == 2;
+            switch (tile) {
+                case 25: return s2 ? launch_wgrad9t_h<T, 64, 64, 2, 32>(p, st) : launch_wgrad9t_h<T, 64, 64, 1, 32>(p, st);
+                case 26: return s2 ? launch_wgrad9t_h<T, 128, 64, 2, 32>(p, st) : launch_wgrad9t_h<T, 128, 64, 1, 32>(p, st);
+                case 27:  // stride 2 would stage 13 chunks per lane beside 288 accumulators: spills
+                    if (s2) {
+                        set_error("wgrad tile 27 is stride-1 only");
+                        return YXH_EUNSUPPORTED;
+                    }
+                    return launch_wgrad9t_h<T, 64, 128, 1, 32>(p, st);
+                default: return s2 ? launch_wgrad9t_h<T, 64, 64, 2, 64>(p, st) : launch_wgrad9t_h<T, 64, 64, 1, 64>(p, st);
+            }
+        }
         default: set_error("wgrad tile %d", tile); return YXH_EINVAL;
     }
 }

@@ -38,7 +38,7 @@ from .models.network import (BaseConv, Bottleneck, CspDarknet, CspLayer, DWConv,
                              YoloPafpn, YoloxHead)
 
 MAX_CHANNELS = 4096  # reduction workspace sizing (yolox_x: 1280)
-WGRAD_WS_BYTES = 16 << 20  # = the launcher's cap on per-split partials (4 Mi floats)
+WGRAD_WS_BYTES = 64 << 20  # = the launchers' largest cap on per-split partials (16 Mi floats, tiles 25-28)
 
 
 class Act:
@@ -138,7 +138,7 @@ _BASE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + lis
 CONV_TUNE_TILES = _BASE_TILES + ([] if os.environ.get("YOLOX_AMD_TRAIN_TILES16") == "base" else
                                  [2 * i for i in list(range(97, 105)) + list(range(161, 191)) + list(range(201, 211))])
 CONV_TUNE_TILES_F32 = _BASE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)] + [2 * i for i in range(211, 217)]
-WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 25))
+WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 25)) + list(range(25, 29))
 _TRAIN_TILES: dict = {}
 # diagnostic (tools/train_shapes.py): every conv / wgrad launch of the training step, in order
 _LAUNCH_LOG: Optional[list] = [] if os.environ.get("YOLOX_AMD_TRAIN_LOG") else None
@@ -175,7 +175,8 @@ class TrainGraph:
         self._wside = (torch.cuda.Stream(self.device) if os.environ.get("YOLOX_AMD_WGRAD_STREAM", "1") != "0"
                        and self.device.type == "cuda" else None)
         # per-split partial weight gradients of the fp32 wgrad tiles (summed in a fixed order); the
-        # launcher uses at most 16 MiB of partials (csrc/train.hip ws_cap_splits; a weight too large
+        # launcher uses at most 16 MiB of partials, 64 MiB for the 16-bit nine-tap tiles 25-28
+        # (csrc/train.hip ws_cap_splits; a weight too large
         # for one split falls back to fp32 atomics).  One workspace per stream that issues
         # weight gradients (head preds: main stream; BaseConvs: the side stream), so work in
         # flight on one stream never shares partials with the other.

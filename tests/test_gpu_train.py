@@ -345,6 +345,45 @@ def test_conv_wgrad9t_fp32_tiles(ws, tile, cin0, cin1, up1, cout, k, s, H, W, B,
     assert rel(dw, wr.grad) < 1e-5
 
 
+@pytest.mark.parametrize("ws", [0, 16 << 20])
+@pytest.mark.parametrize("tile", [25, 26, 27, 28])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("cin0,cin1,up1,cout,k,s,H,W,B,dyc", [c for c in WGF_CASES if c[4] == 3]
+                         + [(64, 64, 1, 64, 3, 1, 12, 10, 2, 64), (128, 0, 0, 128, 3, 1, 40, 40, 2, 136),
+                            (64, 0, 0, 128, 3, 2, 80, 70, 1, 128)])
+def test_conv_wgrad9t_16bit_tiles(ws, tile, dtype, cin0, cin1, up1, cout, k, s, H, W, B, dyc):
+    """bf16/f16 3x3 weight gradient with all nine taps per block (tiles 25-28: one dY row segment
+    and its three input rows staged once, MFMA operands read pixel-transposed by ds_read_b64_tr_b16,
+    each lane naming its tap's shifted / strided pixel row) against torch autograd: stride 1 / 2,
+    row segments past the image edge, cout / cin tails, two sources (the second upsampled), a wide
+    dy view; tile 27 is stride-1 only."""
+    g = torch.Generator().manual_seed(cin0 * 11 + cout + H + tile)
+    oh, ow = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
+    x0 = torch.randn(B, H, W, cin0, generator=g).to(dtype)
+    x1 = torch.randn(B, H >> up1, W >> up1, cin1, generator=g).to(dtype) if cin1 else None
+    dy = torch.randn(B, oh, ow, dyc, generator=g).to(dtype)
+    keep = [x0.cuda(), dy.cuda()] + ([x1.cuda()] if cin1 else [])
+    srcs = [src(keep[0])]
+    if cin1:
+        srcs.append(src(keep[2], up=up1))
+    try:
+        dw = wgrad(dtype, srcs, src(keep[1]), cout, cin0 + cin1, 3, s, 1, (H, W), (oh, ow), B, tile=tile,
+                   ws_bytes=ws)
+    except NotImplementedError as e:
+        assert tile == 27 and s == 2, e
+        return
+    assert not (tile == 27 and s == 2)
+    xin = x0.float().permute(0, 3, 1, 2)
+    if cin1:
+        x1n = x1.float().permute(0, 3, 1, 2)
+        if up1:
+            x1n = F.interpolate(x1n, scale_factor=2, mode="nearest")
+        xin = torch.cat([xin, x1n], 1)
+    wr = torch.zeros(cout, cin0 + cin1, 3, 3, requires_grad=True)
+    F.conv2d(xin, wr, stride=s, padding=1).backward(dy[..., :cout].float().permute(0, 3, 1, 2))
+    assert rel(dw, wr.grad) < 1e-4  # fp32 accumulation of exact products: order-only differences
+
+
 def test_conv_wgrad_fp32_workspace_is_deterministic():
     """With a workspace the split partials are summed in a fixed order: two runs agree bit for bit."""
     g = torch.Generator().manual_seed(11)

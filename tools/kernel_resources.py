@@ -38,22 +38,31 @@ def kernels(lib: str = LIB) -> dict:
                 continue
             notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True,
                                    text=True).stdout
-            cur = None
+            # one YAML map per kernel, its keys sorted: .agpr_count and .group_segment_fixed_size come
+            # BEFORE .name, so a record starts at its "- ." line and is filed under its name at the end
+            rec, name = None, None
+            def flush():
+                if rec is not None and name:
+                    out.setdefault(name, {}).update(rec)
             for line in notes.splitlines():
                 t = line.strip()
-                m = re.match(r"^-?\s*\.(\w+):\s*(.*)$", t)
+                m = re.match(r"^(-?)\s*\.(\w+):\s*(.*)$", t)
                 if not m:
                     continue
-                key, val = m.group(1), m.group(2).strip()
-                if key == "name" and not val.startswith("_ZN") and cur is None:
+                item, key, val = m.group(1), m.group(2), m.group(3).strip()
+                if item and key != "name" and key != "address_space" and (rec is None or key == "agpr_count"):
+                    flush()
+                    rec, name = {}, None
+                if rec is None:
                     continue
                 if key == "name" and val.startswith("_Z"):
-                    cur = out.setdefault(val, {})
-                elif cur is not None and key in ("vgpr_count", "agpr_count", "sgpr_count", "group_segment_fixed_size",
-                                                 "private_segment_fixed_size"):
+                    name = val
+                elif key in ("vgpr_count", "agpr_count", "sgpr_count", "group_segment_fixed_size",
+                             "private_segment_fixed_size"):
                     short = {"vgpr_count": "vgpr", "agpr_count": "agpr", "sgpr_count": "sgpr",
                              "group_segment_fixed_size": "lds", "private_segment_fixed_size": "scratch"}[key]
-                    cur[short] = int(val)
+                    rec[short] = int(val)
+            flush()
     return out
 
 
