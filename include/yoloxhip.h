@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 15
+#define YXH_ABI_VERSION 16
 
 enum yxh_status {
     YXH_OK = 0,
@@ -47,8 +47,10 @@ enum yxh_act {
     YXH_ACT_LRELU = 3,        /* LeakyReLU(0.1)                                            */
     YXH_ACT_DECODE = 4,       /* eval head: ch 0-1 (v+grid)*s, 2-3 exp(v)*s, 4.. sigmoid
                                  (yolo_head.py:185-187, 233-251)                            */
-    YXH_ACT_DECODE_TRAIN = 5  /* train head: ch 0-1, 2-3 decoded, 4.. raw logits
+    YXH_ACT_DECODE_TRAIN = 5, /* train head: ch 0-1, 2-3 decoded, 4.. raw logits
                                  (yolo_head.py:213-231)                                     */
+    YXH_ACT_DECODE_RAW = 6    /* ABI 16, eval head with decode_in_inference = False: ch 0-3 raw,
+                                 4.. sigmoid (yolo_head.py:185-187, 208-211)                */
 };
 
 /* One input operand of a convolution: `channels` channels starting at `ptr`. */
@@ -527,7 +529,9 @@ typedef struct {
  * decode (yolo_head.py:149-160, 185-187, 205-207, 233-251) in one launch: rows
  * [a_off, a_off + h*w) of every image of the fp32 [B, A, 5+C] output (out_bstride =
  * A*(5+C)).  w_reg [5][cin] (reg 4 + obj 1) / w_cls [C][cin] in `dtype`, fp32 biases.
- * train != 0: obj/cls stay logits (get_output_and_grid, :213-231). */
+ * train = 1: obj/cls stay logits (get_output_and_grid, :213-231); train = 2 (ABI 16): the
+ * eval rows without the box decode (decode_in_inference = False, :208-211): reg raw, obj/cls
+ * sigmoid. */
 typedef struct {
     int32_t dtype, batch, h, w, cin, num_classes;
     yxh_src reg, cls;

@@ -459,7 +459,7 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     YXH_CHECK_ARG(d->nsrc == 1 || d->nsrc == 2, "nsrc %d", d->nsrc);
     YXH_CHECK_ARG(d->weight && d->bias && (d->dst || d->post_weight), "null weight/bias/dst");
     YXH_CHECK_ARG(d->dst_dtype == dt || d->dst_dtype == YXH_F32, "dst dtype %d", d->dst_dtype);
-    YXH_CHECK_ARG(d->act >= YXH_ACT_NONE && d->act <= YXH_ACT_DECODE_TRAIN, "act %d", d->act);
+    YXH_CHECK_ARG(d->act >= YXH_ACT_NONE && d->act <= YXH_ACT_DECODE_RAW, "act %d", d->act);
     YXH_CHECK_ARG(d->act < YXH_ACT_DECODE || d->dst_dtype == YXH_F32, "decode needs an f32 dst");
     const bool dw = d->groups != 1;
     YXH_CHECK_ARG(!dw || (d->groups == d->cin && d->cout == d->cin && d->nsrc == 1), "groups %d", d->groups);

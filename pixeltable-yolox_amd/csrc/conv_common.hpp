@@ -100,12 +100,12 @@ __device__ __forceinline__ void finish4(const ConvParams& p, float v[4], int n, 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             int ch = p.dcoff + n + r;
-            if (ch < 2)
-                v[r] = (v[r] + (float)(ch == 0 ? ox : oy)) * p.dstride;
-            else if (ch < 4)
-                v[r] = expf(v[r]) * p.dstride;
-            else if (p.act == YXH_ACT_DECODE)
+            if (ch < 4) {
+                if (p.act != YXH_ACT_DECODE_RAW)
+                    v[r] = ch < 2 ? (v[r] + (float)(ch == 0 ? ox : oy)) * p.dstride : expf(v[r]) * p.dstride;
+            } else if (p.act != YXH_ACT_DECODE_TRAIN) {
                 v[r] = 1.0f / (1.0f + expf(-v[r]));
+            }
         }
     } else {
 #pragma unroll

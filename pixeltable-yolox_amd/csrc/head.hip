@@ -133,16 +133,18 @@ __global__ __launch_bounds__(256) void head_pred(yxh_head_desc d) {
                     if (f == 0) {
                         if (ch < 5) {
                             v += d.b_reg[ch];
-                            if (ch < 2) v = (v + (float)(ch == 0 ? gx : gy)) * st;
-                            else if (ch < 4) v = hd_exp(v) * st;
-                            else v = d.train ? v : hd_sigmoid(v);
+                            if (ch < 4) {
+                                if (d.train != 2) v = ch < 2 ? (v + (float)(ch == 0 ? gx : gy)) * st : hd_exp(v) * st;
+                            } else {
+                                v = d.train == 1 ? v : hd_sigmoid(v);
+                            }
                             row[ch] = v;
                         }
                     } else {
                         const int c = ch - 16;
                         if (c < C) {
                             v += d.b_cls[c];
-                            row[5 + c] = d.train ? v : hd_sigmoid(v);
+                            row[5 + c] = d.train == 1 ? v : hd_sigmoid(v);
                         }
                     }
                 }
@@ -173,6 +175,7 @@ int head_pred_launch(const yxh_head_desc* d, hipStream_t st) {
     YXH_CHECK_ARG(d && d->out && d->cls.ptr && d->reg.ptr && d->w_reg && d->w_cls && d->b_reg && d->b_cls,
                   "head_pred: null pointer");
     YXH_CHECK_ARG(d->batch > 0 && d->h > 0 && d->w > 0, "head_pred: empty level");
+    YXH_CHECK_ARG(d->train >= 0 && d->train <= 2, "head_pred: mode %d", d->train);
     YXH_CHECK_ARG(((long long)d->h * d->w) % 4 == 0 && d->a_off % 4 == 0 && d->out_bstride % 4 == 0 &&
                       ((uintptr_t)d->out & 15) == 0,
                   "head_pred: level rows must be 16-byte aligned (h*w, a_off multiples of 4)");

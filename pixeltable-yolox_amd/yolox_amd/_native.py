@@ -17,12 +17,12 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
 F32, BF16, F16, U8 = 0, 1, 2, 3
-ACT_NONE, ACT_SILU, ACT_RELU, ACT_LRELU, ACT_DECODE, ACT_DECODE_TRAIN = range(6)
+ACT_NONE, ACT_SILU, ACT_RELU, ACT_LRELU, ACT_DECODE, ACT_DECODE_TRAIN, ACT_DECODE_RAW = range(7)
 NCHW, NHWC = 0, 1
 OP_CONV, OP_FOCUS, OP_SPP, OP_STEM, OP_HEAD, OP_STEM2 = 0, 1, 2, 3, 4, 5
 LB_F32_NCHW, LB_U8_NHWC, LB_BF16_NHWC = 0, 1, 2

@@ -168,13 +168,16 @@ class YoloxConfig:
         sampler = InfiniteSampler(len(ds), seed=seed)
         return MosaicBatches(ds, sampler, batch_size)
 
-    def get_eval_loader(self, batch_size: int, is_distributed: bool, dataset=None, **kwargs):
-        """config.py:363-382 over any ``pull_item`` detection dataset with ``.coco`` (the ground
+    def get_eval_loader(self, batch_size: int, is_distributed: bool, dataset=None, testdev: bool = False,
+                        legacy: bool = False):
+        """config.py:350-382 over any ``pull_item`` detection dataset with ``.coco`` (the ground
         truth: a COCO json dict or pycocotools COCO) and ``.class_ids``: (imgs, targets, info_imgs,
-        ids) batches letterboxed to test_size on the device (ValTransform = yxh_letterbox_batch);
+        ids) batches letterboxed to test_size on the device (ValTransform = yxh_letterbox_batch;
+        ``legacy``: ValTransform(legacy=True)'s channel flip + /255 + mean/std, data_augment.py:236-240);
         distributed: batch_size // world per rank over the rank's contiguous-strided shard (the
         DistributedSampler without its padding duplicates).  COCO dataset readers are out of scope
-        (no datasets offline): ``dataset`` is required."""
+        (no datasets offline): ``dataset`` is required -- ``testdev`` picks the reference's
+        annotation file (test_ann), so here it is the caller's choice of ``dataset``."""
         from .evaluators.coco_evaluator import EvalLoader
         if dataset is None:
             raise NotImplementedError("COCO dataset readers are out of scope: pass dataset= (pull_item, coco, "
@@ -184,7 +187,7 @@ class YoloxConfig:
             import torch.distributed as dist
             rank, world = dist.get_rank(), dist.get_world_size()
             batch_size = batch_size // world
-        return EvalLoader(dataset, batch_size, self.test_size, rank, world)
+        return EvalLoader(dataset, batch_size, self.test_size, rank, world, legacy=legacy)
 
     def get_evaluator(self, batch_size: int, is_distributed: bool, testdev: bool = False, legacy: bool = False,
                       dataset=None):

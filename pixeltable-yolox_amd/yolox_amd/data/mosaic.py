@@ -165,8 +165,11 @@ class ResidentImages:
         self.ids: list = []
         images = []
         off = 0
-        # a dataset whose items repeat stored images (source_index) uploads each image once
+        # a dataset whose items repeat stored images (source_index) uploads each image once; the
+        # repeated item's id is the dataset's own (``image_id(i)``, what its pull_item(i) would
+        # return), or the item index when the dataset has no such method
         src_of = getattr(dataset, "source_index", None)
+        id_of = getattr(dataset, "image_id", None)
         first: dict = {}
         for i in range(n):
             src = src_of(i) if src_of is not None else i
@@ -176,7 +179,7 @@ class ResidentImages:
                 lab = dataset.load_anno(i) if hasattr(dataset, "load_anno") else self.labels[j]
                 self.labels.append(np.array(lab, copy=True))
                 self.infos.append(self.infos[j])
-                self.ids.append(np.array([i]))
+                self.ids.append(np.asarray(id_of(i)) if id_of is not None else np.array([i]))
                 continue
             first[src] = i
             img, lab, info, img_id = dataset.pull_item(i)
@@ -526,6 +529,11 @@ class SyntheticDetectionDataset:
     def load_anno(self, i: int) -> np.ndarray:
         return self._item(i)[1]
 
+    def image_id(self, i: int) -> np.ndarray:
+        """The id pull_item(i) returns (the item index, as the reference's COCODataset ids are
+        per item) -- what ResidentImages records for an item it does not pull."""
+        return np.array([i])
+
     def pull_item(self, i: int):
         img, labels = self._item(i)
-        return img, labels.copy(), img.shape[:2], np.array([i])
+        return img, labels.copy(), img.shape[:2], self.image_id(i)

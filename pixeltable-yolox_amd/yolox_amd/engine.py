@@ -391,7 +391,7 @@ class PlanCtx:
         """cls_convs[k][1] | reg_convs[k][1] + the level's preds + decode as ONE conv_ws head-form
         launch (yxh_conv_desc.post_weight / post_weight2): eval, 16-bit, 128 channels per group,
         65-80 classes, 16-byte level rows."""
-        return (self.csp_fusion and not train and self.dtype != torch.float32 and src.ch == 256
+        return (self.csp_fusion and int(train) == self.HEAD_EVAL and self.dtype != torch.float32 and src.ch == 256
                 and 65 <= head.num_classes <= 80 and level in _HEAD_FUSION)
 
     def conv_grouped2_head(self, ms, src: View, head, k: int, out: "OutBuffer", a_off: int, stride: int) -> None:
@@ -415,9 +415,16 @@ class PlanCtx:
     def spp(self, cat: Buffer, hidden: int) -> None:
         self.ops.append(OpRec(N.OP_SPP, dict(buf=cat, c=hidden)))
 
+    # head output modes: eval rows (decode_outputs), train rows (get_output_and_grid), eval rows
+    # without the box decode (decode_in_inference = False, yolo_head.py:208-211)
+    HEAD_EVAL, HEAD_TRAIN, HEAD_RAW = 0, 1, 2
+
     def head_preds(self, k: int, head, cls_feat: View, reg_feat: View, out: "OutBuffer", a_off: int,
-                   stride: int, train: bool) -> None:
-        act = N.ACT_DECODE_TRAIN if train else N.ACT_DECODE
+                   stride: int, train) -> None:
+        """``train``: False / True, or a HEAD_* mode (yxh_head_desc.train)."""
+        mode = int(train)
+        act = (N.ACT_DECODE, N.ACT_DECODE_TRAIN, N.ACT_DECODE_RAW)[mode]
+        train = mode
         h, w = cls_feat.lh, cls_feat.lw
         C = head.num_classes
         if (self.dtype != torch.float32 and cls_feat.ch == reg_feat.ch and cls_feat.ch in (64, 128, 256)
@@ -1101,7 +1108,7 @@ class Plan:
             off, deps = self._dag_arrays()
             N.check(self.lib.yxh_graph_create_dag(self._ops, len(self._ops), off, deps, N.stream_ptr(self.device),
                                                   C.byref(g)), "graph capture (dag)")
-        elif self.graph_mode == "lanes" and self.parallel_chunks and self.nchunks <= 16:
+        elif self.graph_mode == "lanes" and self.parallel_chunks and self.nchunks <= 8:  # yxh_graph_create_lanes cap
             # one capture stream per chunk: independent chains, joined at the end
             lanes = [c for c in range(self.nchunks) for _ in self.ctx.ops]
             off, deps = self._dag_arrays()

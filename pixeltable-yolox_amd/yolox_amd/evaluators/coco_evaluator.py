@@ -82,17 +82,35 @@ def _gather(obj):
     return out
 
 
+_LEGACY_MEAN = (0.485, 0.456, 0.406)
+_LEGACY_STD = (0.229, 0.224, 0.225)
+
+
+def legacy_normalize(imgs: torch.Tensor) -> torch.Tensor:
+    """ValTransform(legacy=True) after the letterbox (data_augment.py:236-240): BGR -> RGB, / 255,
+    - mean, / std over a float32 [B, 3, H, W] batch, rounded as numpy rounds the reference's
+    in-place ops: ``img /= 255.0`` in float32 (a Python scalar), then ``img -= mean`` and
+    ``img /= std`` against float64 arrays, i.e. computed in float64 and stored as float32."""
+    x = imgs.flip(1) / 255.0
+    mean = torch.tensor(_LEGACY_MEAN, dtype=torch.float64, device=x.device).view(1, 3, 1, 1)
+    std = torch.tensor(_LEGACY_STD, dtype=torch.float64, device=x.device).view(1, 3, 1, 1)
+    x = (x.double() - mean).float()
+    return (x.double() / std).float()
+
+
 class EvalLoader:
-    """The evaluation loader (config.py:363-382): batches of ``dataset.pull_item`` images
+    """The evaluation loader (config.py:350-382): batches of ``dataset.pull_item`` images
     letterboxed on the device to ``size`` (yxh_letterbox_batch: preproc / ValTransform,
     data_augment.py:140-156 + 257-264) as (imgs [B, 3, H, W] fp32, targets, (heights, widths),
-    ids); rank ``rank`` of ``world`` reads items rank, rank + world, ..."""
+    ids); rank ``rank`` of ``world`` reads items rank, rank + world, ...  ``legacy``: the
+    ValTransform(legacy=True) normalisation of old checkpoints (``legacy_normalize``)."""
 
-    def __init__(self, dataset, batch_size: int, size, rank: int = 0, world: int = 1):
+    def __init__(self, dataset, batch_size: int, size, rank: int = 0, world: int = 1, legacy: bool = False):
         self.dataset = dataset
         self.batch_size = max(1, int(batch_size))
         self.size = tuple(size)
         self.indices = list(range(rank, len(dataset), world))
+        self.legacy = bool(legacy)
 
     def __len__(self) -> int:
         return (len(self.indices) + self.batch_size - 1) // self.batch_size
@@ -102,6 +120,8 @@ class EvalLoader:
         for k in range(0, len(self.indices), self.batch_size):
             items = [self.dataset.pull_item(i) for i in self.indices[k:k + self.batch_size]]
             imgs = letterbox_batch([it[0] for it in items], self.size)
+            if self.legacy:
+                imgs = legacy_normalize(imgs)
             targets = [it[1] for it in items]
             info = ([int(it[2][0]) for it in items], [int(it[2][1]) for it in items])
             yield imgs, targets, info, [int(it[3]) for it in items]

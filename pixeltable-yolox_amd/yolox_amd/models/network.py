@@ -451,8 +451,6 @@ class YoloxHead(_Planned):
         from ..engine import Plan
         if self.training:
             raise NotImplementedError("YoloxHead.forward in training mode: call YoloxModule.forward(x, targets)")
-        if not self.decode_in_inference:
-            raise NotImplementedError("decode_in_inference=False (raw head outputs) is not planned")
         if len(xin) != 3:
             raise ValueError("YoloxHead takes three feature maps")
         p = _param0(self)
@@ -460,7 +458,7 @@ class YoloxHead(_Planned):
             raise RuntimeError("YoloxHead runs on a ROCm device only; call .to('cuda') first")
         B = xin[0].shape[0]
         shapes = [tuple(int(v) for v in t.shape[1:]) for t in xin]
-        key = ("head", B, tuple(shapes), p.dtype, str(p.device))
+        key = ("head", B, tuple(shapes), p.dtype, str(p.device), bool(self.decode_in_inference))
         owner = self
         plan = _stage_plan(self, key, lambda: Plan(_StageModel(owner, head=owner), B, 32, 32, p.dtype, p.device,
                                                    stage="head", head_inputs=shapes))
@@ -481,7 +479,10 @@ class YoloxHead(_Planned):
 
     def plan(self, ctx, feats, out, train: bool = False):
         """Per level: stem, 2x cls conv, 2x reg conv, then the 1x1 preds write decoded
-        rows straight into ``out`` [B, A, 5+C] (yolo_head.py:140-251)."""
+        rows straight into ``out`` [B, A, 5+C] (yolo_head.py:140-251); eval with
+        ``decode_in_inference = False``: the same rows without the box decode (:208-211)."""
+        if not train and not self.decode_in_inference:
+            train = 2  # PlanCtx.HEAD_RAW
         a_off = 0
         for k, x in enumerate(feats):
             n0 = len(ctx.ops)

@@ -7,7 +7,10 @@ Differences from the reference, all deliberate:
   ``$YOLOX_HOME/weights/<name>.pth`` if present and raises FileNotFoundError
   otherwise; ``YoloxModule.synthetic(name)`` builds seeded weights instead;
 * the compute dtype follows the parameters: float32 by default (numerical parity
-  with the reference), bfloat16 / float16 after ``.to(dtype)`` / ``.half()``.
+  with the reference), bfloat16 / float16 after ``.to(dtype)`` / ``.half()``;
+* ``from_pretrained(..., device=...)`` defaults to the ROCm device (the reference's
+  default is ``'cpu'``, yolox.py:35,103) and refuses a non-ROCm device right there,
+  before anything is loaded, instead of at the first forward.
 """
 from __future__ import annotations
 
@@ -66,7 +69,8 @@ class YoloxModule(nn.Module):
         from ..engine import Plan
 
         dtype = dtype or self.compute_dtype
-        key = (batch, height, width, input_layout, input_dtype, dtype, str(self.device), chunk, parallel_chunks)
+        key = (batch, height, width, input_layout, input_dtype, dtype, str(self.device), chunk, parallel_chunks,
+               bool(self.head.decode_in_inference))
         plan = self._plans.get(key)
         if plan is None:
             if self.device.type != "cuda":
@@ -115,23 +119,42 @@ class YoloxModule(nn.Module):
     @classmethod
     def from_pretrained(cls, pretrained_model_name_or_path: Union[str, os.PathLike],
                         config: Optional[YoloxConfig] = None, device: Optional[str] = None) -> "YoloxModule":
-        path = str(pretrained_model_name_or_path)
+        """yolox.py:100-131 (a local checkpoint, eval mode, on ``device``): the reference's
+        argument errors first, then a non-ROCm device is refused before anything is loaded."""
+        path, config = cls._checkpoint_path(pretrained_model_name_or_path, config)
+        dev = torch.device(device or default_device())
+        if dev.type != "cuda":
+            raise RuntimeError(f"YoloxModule runs on a ROCm device only (device={str(dev)!r}): the HIP path has "
+                               "no CPU execution; pass device='cuda' (the reference's CPU default is not supported)")
+        return cls.load_checkpoint(path, config).to(dev)
+
+    @staticmethod
+    def _checkpoint_path(name_or_path, config):
+        """(checkpoint file, config) as yolox.py:109-127 resolves them -- without the download."""
+        path = str(name_or_path)
         if os.path.isfile(path):
             if config is None:
                 raise ValueError("config must be provided when loading model from a file")
-        else:
-            config = YoloxConfig.get_named_config(path)
-            if config is None:
-                raise ValueError(f"Unknown model: {pretrained_model_name_or_path}")
-            path = str(HOME / "weights" / f"{config.name}.pth")
-            if not os.path.isfile(path):
-                raise FileNotFoundError(
-                    f"{path} not found: pretrained weights are not downloaded by yolox_amd (no network); "
-                    "place the MegVii checkpoint there or use YoloxModule.synthetic()")
+            return path, config
+        config = YoloxConfig.get_named_config(path)
+        if config is None:
+            raise ValueError(f"Unknown model: {name_or_path}")
+        path = str(HOME / "weights" / f"{config.name}.pth")
+        if not os.path.isfile(path):
+            raise FileNotFoundError(
+                f"{path} not found: pretrained weights are not downloaded by yolox_amd (no network); "
+                "place the MegVii checkpoint there or use YoloxModule.synthetic()")
+        return path, config
+
+    @classmethod
+    def load_checkpoint(cls, pretrained_model_name_or_path: Union[str, os.PathLike],
+                        config: Optional[YoloxConfig] = None) -> "YoloxModule":
+        """The loading half of ``from_pretrained``: the model built from ``config`` with the
+        checkpoint's weights (weights_only load), on the host, eval mode."""
+        path, config = cls._checkpoint_path(pretrained_model_name_or_path, config)
         model = config.get_model()
         weights = torch.load(path, map_location="cpu", weights_only=True)
         model.load_state_dict(weights["model"] if "model" in weights else weights)
-        model = model.to(device or default_device())
         model.eval()
         return model
 

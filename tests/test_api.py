@@ -67,7 +67,10 @@ def test_from_pretrained_loads_local_checkpoint(tmp_path):
     cfg = named_config("yolox_nano")
     sd = synthetic_state_dict(cfg.get_model().state_dict(), seed=3)
     torch.save({"model": sd}, tmp_path / "nano.pth")
-    m = YoloxModule.from_pretrained(str(tmp_path / "nano.pth"), named_config("yolox_nano"), device="cpu")
+    # the HIP path has no CPU execution: a CPU device is refused at load, not at the first forward
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        YoloxModule.from_pretrained(str(tmp_path / "nano.pth"), named_config("yolox_nano"), device="cpu")
+    m = YoloxModule.load_checkpoint(str(tmp_path / "nano.pth"), named_config("yolox_nano"))
     assert not m.training
     assert torch.equal(m.state_dict()["head.cls_preds.1.weight"], sd["head.cls_preds.1.weight"])
     with pytest.raises(RuntimeError, match="ROCm device"):

@@ -179,3 +179,32 @@ def test_trainer_closes_mosaic_at_the_reference_epoch():
         for tr.epoch in range(cfg.max_epoch):
             tr.before_epoch()
         assert closed[0] == first_closed and tr.model.head.use_l1
+
+
+def test_resident_images_ids_of_repeated_items():
+    """Items that repeat a stored image (``source_index``) are uploaded once; their ids come from
+    the dataset (``image_id(i)``: what its pull_item(i) returns), not from the item index."""
+
+    class _Repeating:
+        def __len__(self):
+            return 6
+
+        def source_index(self, i):
+            return i % 2
+
+        def image_id(self, i):
+            return np.array([1000 + 7 * i])
+
+        def load_anno(self, i):
+            return np.zeros((1, 5)) + i
+
+        def pull_item(self, i):
+            return np.full((4, 6, 3), i, np.uint8), self.load_anno(i), (4, 6), self.image_id(i)
+
+    ds = _Repeating()
+    res = M.ResidentImages(ds, device="cpu")
+    assert [int(np.asarray(v).reshape(-1)[0]) for v in res.ids] == [1000 + 7 * i for i in range(6)]
+    assert int(res.pool.numel()) >= 2 * 4 * 6 * 3 and res.offsets[2] == res.offsets[0]
+    syn = M.SyntheticDetectionDataset(5, (64, 64), distinct=2)
+    r2 = M.ResidentImages(syn, device="cpu")
+    assert [int(v[0]) for v in r2.ids] == [int(syn.pull_item(i)[3][0]) for i in range(5)]

@@ -169,3 +169,42 @@ def test_summary_text_format():
     assert lines[1] == " Average Precision  (AP) @[ IoU=0.50      | area=   all | maxDets=100 ] = 0.700"
     assert lines[3] == " Average Precision  (AP) @[ IoU=0.50:0.95 | area= small | maxDets=100 ] = -1.000"
     assert lines[6] == " Average Recall     (AR) @[ IoU=0.50:0.95 | area=   all | maxDets=  1 ] = 0.200"
+
+
+def test_eval_loader_legacy_normalisation(monkeypatch):
+    """get_eval_loader(legacy=True) = ValTransform(legacy=True) (data_augment.py:236-240): after the
+    letterbox, BGR -> RGB, /255, - mean, / std, rounded as numpy's in-place float32 ops round; the
+    default (legacy=False) hands the letterboxed batch over untouched.  The device letterbox is
+    stubbed with a seeded float32 batch (its own parity: tests/test_gpu_processor.py)."""
+    from yolox_amd.config import named_config
+    from yolox_amd.models import processor as P
+
+    rng = np.random.default_rng(5)
+    boxed = rng.integers(0, 256, size=(2, 3, IMG, IMG)).astype(np.float32)
+    boxed[0, :, :4, :4] = 114.0  # letterbox padding value
+    monkeypatch.setattr(P, "letterbox_batch", lambda imgs, size: torch.from_numpy(boxed.copy()))
+
+    class _Items:
+        coco, class_ids = {}, [1]
+
+        def __len__(self):
+            return 2
+
+        def pull_item(self, i):
+            return np.zeros((8, 8, 3), np.uint8), np.zeros((1, 5)), (8, 8), i
+
+    cfg = named_config("yolox_s")
+    plain = next(iter(cfg.get_eval_loader(2, False, dataset=_Items())))[0]
+    assert torch.equal(plain, torch.from_numpy(boxed))
+    got = next(iter(cfg.get_eval_loader(2, False, dataset=_Items(), legacy=True)))[0].numpy()
+    want = []
+    for img in boxed:  # data_augment.py:236-240 verbatim semantics, per image
+        img = img[::-1, :, :].copy()
+        img /= 255.0
+        img -= np.array([0.485, 0.456, 0.406]).reshape(3, 1, 1)
+        img /= np.array([0.229, 0.224, 0.225]).reshape(3, 1, 1)
+        want.append(img)
+    want = np.stack(want)
+    assert got.dtype == np.float32 and np.array_equal(got, want)
+    ev = cfg.get_evaluator(2, False, legacy=True, dataset=_Items())
+    assert ev.dataloader.legacy

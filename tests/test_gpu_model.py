@@ -344,3 +344,37 @@ def test_backbone_stages_callable_standalone(golden):
     d3 = dark.dark3(dark.dark2(dark.stem(x)))
     assert (d3 - outs["dark3"]).abs().max().item() <= 1e-4 * outs["dark3"].abs().max().item()
     assert tuple(outs["dark5"].shape) == (x.shape[0], 512, 4, 4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_decode_in_inference_false(golden, dtype):
+    """head.decode_in_inference = False (yolo_head.py:208-211, the deploy/export form): the eval
+    rows without the box decode -- reg raw, obj / cls sigmoid.  Against the decoded rows of the
+    same module: obj / cls bit-identical, (raw_xy + grid) * stride bit-identical (the decode's own
+    fp32 op order), exp(raw_wh) * stride within 1e-5 (device exp vs torch.exp); fp32 also against
+    the reference fixture, un-decoded.  The standalone head (YoloxHead.forward) follows the flag."""
+    from oracle.reference_cpu import anchors_for
+    d = golden("fwd_yolox_s_128.npz")
+    x = torch.from_numpy(d["input_u8"]).permute(0, 3, 1, 2).float()
+    m = model("yolox_s", dtype)
+    dec = m(x).cpu()
+    m.head.decode_in_inference = False
+    raw = m(x).cpu()
+    m.head.decode_in_inference = True
+    assert torch.equal(m(x).cpu(), dec)  # the flag selects a plan of its own
+    gx, gy, st = anchors_for([(16, 16), (8, 8), (4, 4)])
+    grid = torch.stack([gx, gy], 1)[None]
+    st = st[None, :, None]
+    assert torch.equal(raw[..., 4:], dec[..., 4:])
+    assert torch.equal((raw[..., :2] + grid) * st, dec[..., :2])
+    torch.testing.assert_close(torch.exp(raw[..., 2:4]) * st, dec[..., 2:4], rtol=1e-5, atol=1e-5)
+    if dtype == torch.float32:
+        ref = torch.from_numpy(d["output"])
+        assert (raw[..., :2] - (ref[..., :2] / st - grid)).abs().max() < 1e-3
+        assert (raw[..., 2:4] - torch.log(ref[..., 2:4] / st)).abs().max() < 1e-3
+        # standalone head over the PAFPN maps, flag off: the same raw rows
+        feats = m.backbone(x.cuda())
+        m.head.decode_in_inference = False
+        hraw = m.head(list(feats)).cpu()
+        m.head.decode_in_inference = True
+        torch.testing.assert_close(hraw, raw, rtol=1e-4, atol=1e-4)

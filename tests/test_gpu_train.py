@@ -703,6 +703,57 @@ def test_batched_weight_repack_matches_per_conv(monkeypatch, dtype):
         assert float(out[k]) == float(ref[k]), k
 
 
+def test_captured_train_step_fp16_gradscaler_matches_eager(monkeypatch):
+    """The bench's --fp16 configs[4] form: CapturedTrainStep(grad_scale=scaler._scale) +
+    FusedStep.step(scaler) (train_one_iter(captured=...)) against the eager fp16 step with the
+    same GradScaler + FusedStep, bit for bit over five steps: losses, every parameter, the EMA
+    weights, the scale and the growth tracker.  Step 2 forces an overflow (scale 2^60: every
+    replay reads the live scale, so the captured step overflows too) -- a skipped step and a
+    backoff of the scale happen between two replays; growth_interval 2 makes the scale grow
+    again within the five steps."""
+    from yolox_amd.optim import FusedStep
+    from yolox_amd.trainer import ModelEMA, train_one_iter
+    import yolox_amd.train as T
+    monkeypatch.setenv("YOLOX_AMD_TRAIN_TUNE", "0")
+    monkeypatch.setattr(T, "_TRAIN_TILES", {})
+    m1, sd, x, labels, _ = _model_and_batch()
+    m2, _, _, _, _ = _model_and_batch()
+    xs, ls = x.cuda().half(), labels.cuda()
+    runs = []
+    for m in (m1, m2):
+        m = m.cuda().train()
+        opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, nesterov=True)
+        ema = ModelEMA(m, 0.9998)
+        scaler = torch.amp.GradScaler("cuda", growth_interval=2)
+        fused = FusedStep(m, opt, ema)
+        train_one_iter(m, opt, xs, ls, amp_dtype=torch.float16, scaler=scaler, ema=ema, fused=fused)  # warm-up
+        runs.append([m, opt, ema, scaler, fused, None])
+    m, opt, ema, scaler, fused, _ = runs[1]
+    opt.zero_grad(set_to_none=True)
+    runs[1][5] = T.CapturedTrainStep(m, xs, ls, dtype=torch.float16, grad_scale=scaler._scale)
+    scales = []
+    for it in range(5):
+        if it == 2:
+            for r in runs:
+                r[3]._scale.fill_(2.0 ** 60)
+        outs = []
+        for m, opt, ema, scaler, fused, cap in runs:
+            outs.append(train_one_iter(m, opt, xs, ls, amp_dtype=torch.float16, scaler=scaler, ema=ema, fused=fused,
+                                       captured=cap))
+        torch.cuda.synchronize()
+        for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss", "num_fg"):
+            assert float(outs[0][k]) == float(outs[1][k]), (it, k)
+        (a, _, ea, sa, _, _), (b, _, eb, sb, _, _) = runs
+        assert torch.equal(sa._scale, sb._scale) and torch.equal(sa._growth_tracker, sb._growth_tracker), it
+        for (n, p), q in zip(a.named_parameters(), b.parameters()):
+            assert torch.equal(p, q), (it, n)
+        for p, q in zip(ea.ema.parameters(), eb.ema.parameters()):
+            assert torch.equal(p, q), it
+        scales.append(float(sa._scale))
+    assert scales[2] == 2.0 ** 59  # the forced overflow: step skipped, scale backed off
+    assert scales[4] > scales[3] or scales[3] > scales[2]  # and grown again (growth_interval 2)
+
+
 @pytest.mark.parametrize("opt_kind", ["sgd", "fused"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_captured_train_step_matches_eager(monkeypatch, dtype, opt_kind):
