@@ -485,6 +485,35 @@ int yxh_spp_bwd(int32_t dtype, int32_t batch, const yxh_src* cat, int32_t c, con
 int yxh_upsample_bwd(const float* g, int32_t batch, int32_t h, int32_t w, int32_t c, float* dst, void* stream);
 
 /*
+ * ABI 16, depthwise conv gradients (DWConv.dconv of yolox_nano, network_blocks.py:55-74: Conv2d with
+ * groups = channels, 3x3, stride 1 or 2, pad 1; the autograd of F.conv2d(groups=C) in the train step).
+ * yxh_dw_wgrad: dw[c][ky][kx] (fp32, torch's [C][1][3][3]) = sum over the batch's output pixels of
+ *   dy[c] * x[c](tap), WRITTEN (not accumulated); x: the forward's input view, dy: a view at the
+ *   output size.  Per-block partials in `workspace` (yxh_dw_wgrad_workspace_bytes), summed by a
+ *   second launch in a fixed order: deterministic.
+ * yxh_dw_dgrad: dx[b][iy][ix][c] (fp32 view, 16-byte aligned dy rows) = (accumulate ? dx : 0) +
+ *   sum over taps of dy[b][oy][ox][c] * w[c][tap], iy = oy * stride - pad + ky; w: the forward's
+ *   packed weights [C][3][3] in `dtype` (yxh_fold_bn_pack with cin_pad 1).
+ */
+size_t yxh_dw_wgrad_workspace_bytes(int32_t batch, int32_t out_h, int32_t out_w, int32_t channels, int32_t k);
+int yxh_dw_wgrad(int32_t dtype, int32_t batch, const yxh_src* x, const yxh_src* dy, int32_t channels, int32_t k,
+                 int32_t stride, int32_t pad, int32_t out_h, int32_t out_w, float* dw, void* workspace,
+                 size_t workspace_bytes, void* stream);
+int yxh_dw_dgrad(int32_t dtype, int32_t batch, const yxh_src* dy, const void* w, int32_t channels, int32_t k,
+                 int32_t stride, int32_t pad, int32_t in_h, int32_t in_w, float* dx, int32_t dx_cstride,
+                 int64_t dx_bstride, int32_t accumulate, void* stream);
+
+/*
+ * ABI 16, yxh_resize_bilinear: YoloxConfig.preprocess's multiscale resize (config.py:296-305),
+ * F.interpolate(x, size=(out_h, out_w), mode="bilinear", align_corners=False) of a dense NCHW
+ * batch [batch][channels][in_h][in_w] in `dtype` (f32 / bf16 / f16) into [batch][channels][out_h]
+ * [out_w]: ATen's bilinear arithmetic term for term in fp32 (scale = in / out, source index
+ * clamped at 0, the +1 neighbour clamped at the border), one rounding to `dtype`.
+ */
+int yxh_resize_bilinear(int32_t dtype, int32_t batch, int32_t channels, int32_t in_h, int32_t in_w, const void* src,
+                        int32_t out_h, int32_t out_w, void* dst, void* stream);
+
+/*
  * yxh_head_decode_train: YoloxHead.get_output_and_grid (yolo_head.py:213-231) on the
  * raw pred-conv outputs raw[B, A, 5+C] (fp32): out = raw with ch 0-1 -> (v + grid) *
  * stride and ch 2-3 -> exp(v) * stride.

@@ -27,9 +27,22 @@
 #define YXH_WS_PROBE 0
 #endif
 
+#ifndef YXH_WS_NPIN
+#define YXH_WS_NPIN 48
+#endif
+
 namespace yxh {
 
 namespace {
+
+// the value must live in AGPRs here (an empty asm with an "a" operand): the register allocator
+// then keeps it there and the MFMAs read it in place
+__device__ __forceinline__ void pin_agpr(uint4& v) {
+    typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+    u32x4v t = {v.x, v.y, v.z, v.w};
+    asm volatile("" : "+a"(t));
+    v = make_uint4(t.x, t.y, t.z, t.w);
+}
 
 constexpr int ws_ps(int c16, int s) {
     return s == 1 ? c16 + (6 - c16 % 4) % 4 : (c16 % 2 ? c16 : c16 + 1);
@@ -100,6 +113,13 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     // weights must stay in VGPRs: 160 of 256 (2 waves per SIMD), 288 of 512 (one 4-wave block per CU)
     static_assert(FR * 9 * WCB * 4 <= (NW == 4 && BPC == 1 ? 288 : 160), "weights must stay in VGPRs");
     static_assert(SMEM <= 160 * 1024, "LDS");
+    // 288-register weight sets (one 4-wave block per CU): the first NPIN weight fragments are pinned
+    // to AGPRs where the first tile first reads them, and the MFMAs take them from there (gfx950's
+    // MFMA reads A operands from AGPRs).  Left to itself the register allocator parks ~30 % of the
+    // weights in AGPRs anyway and copies each back to VGPRs before every use (4 v_accvgpr_read +
+    // an s_nop per 4 MFMAs in the K loop of the head level-0 tile).  48 fragments = 192 AGPRs
+    // leave room for the accumulators; 56 / 64 made the allocator shuffle again (probe builds).
+    constexpr int NPIN = !F1 && FR * 9 * WCB * 4 > 160 ? YXH_WS_NPIN : 0;  // (fused-Bottleneck tiles: spills)
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -553,6 +573,11 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         for (int s = 0; s < NS; ++s) {
             if (s + PD < NS) load_b(s + PD, bf[(s + PD) % (PD + 1)]);
             const int c = s / 9, tap = s - 9 * (s / 9);
+            if constexpr (FIRST && NPIN > 0) {  // where each pinned fragment is first used
+#pragma unroll
+                for (int i = 0; i < FR; ++i)
+                    if ((c * 9 + tap) * FR + i < NPIN) pin_agpr(a[i][tap][c]);
+            }
 #pragma unroll
             for (int i = 0; i < FR; ++i)
 #pragma unroll

@@ -17,6 +17,10 @@
 //    contiguous output rows (a level's rows of one image are consecutive; a tile
 //    straddles at most one image boundary) -- instead of 4-byte scattered stores of
 //    340-byte rows.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "conv_common.hpp"
 
 namespace yxh {
@@ -171,6 +175,137 @@ __global__ __launch_bounds__(256) void head_pred(yxh_head_desc d) {
     }
 }
 
+// head_pred2 (CIN 64 / 128): every wave an independent worker over 16-pixel groups.  head_pred
+// above spent 68 % of its wave cycles waiting (profiles/r04/mfma_util_r4z.txt): each tile's
+// feature loads were issued and waited for before any MFMA, and two barriers per tile
+// serialised the block.  Here
+//  * a wave's B operands come straight from global memory into registers (lane (r, q) of
+//    step s: pixel r's channels 32 s + 8 q .. + 8 -- 64-byte segments of the pixel rows), the
+//    NEXT group's loads issued before this group's MFMAs, so HBM latency hides behind a whole
+//    group of work;
+//  * the weights of all 6 output fragments live in VGPRs for the wave's life (one LDS copy per
+//    block feeds them), the biases in LDS;
+//  * the decoded [16][5 + C] rows go through a per-wave LDS slot and leave as 16-byte stores of
+//    the contiguous output rows -- no block barrier after the prologue.
+// Same MFMA order and decode arithmetic as head_pred: bit-identical output
+// (tests/test_gpu_ops.py test_head_pred_fused_level runs both).
+template <typename T, int CIN, int NCF>
+__global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
+    constexpr int NW = 8;
+    constexpr int KS = CIN / 32;                 // K steps
+    constexpr int NF = 1 + NCF;                  // output fragments: reg|obj, then cls
+    constexpr int WROWS = NF * 16;
+    constexpr int WRB = CIN * 2 + 16;            // LDS weight row: +16 B (odd 16-B slots: conflict-free)
+    constexpr int STGF = 16 * (5 + NCF * 16);    // per-wave staging floats (>= 16 rows of 5 + C)
+    __shared__ __attribute__((aligned(16))) char wl[WROWS * WRB];
+    __shared__ float bl[WROWS];
+    __shared__ __attribute__((aligned(16))) float stg_all[NW][STGF];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int frow = lane & 15, fq = lane >> 4;
+    const int C = d.num_classes, hw = d.h * d.w, rowf = 5 + C;
+    const long long M = (long long)d.batch * hw;
+    const long long G = (M + 15) / 16;
+    const long long gstride = (long long)gridDim.x * NW;
+    long long g = (long long)blockIdx.x * NW + wave;
+    // ---- weights / biases -> LDS (rows past 5 reg|obj and C cls rows are zero), then VGPRs
+    for (int q = tid; q < WROWS * (CIN / 8); q += 64 * NW) {
+        const int r = q / (CIN / 8), c = q - (CIN / 8) * (q / (CIN / 8));
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (r < 5) v = *(const uint4*)((const T*)d.w_reg + (long long)r * CIN + c * 8);
+        else if (r >= 16 && r - 16 < C) v = *(const uint4*)((const T*)d.w_cls + (long long)(r - 16) * CIN + c * 8);
+        *(uint4*)(wl + r * WRB + c * 16) = v;
+    }
+    for (int q = tid; q < WROWS; q += 64 * NW)
+        bl[q] = q < 5 ? d.b_reg[q] : (q >= 16 && q - 16 < C) ? d.b_cls[q - 16] : 0.0f;
+    __syncthreads();
+    uint4 wr[NF][KS];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) wr[f][s] = *(const uint4*)(wl + (f * 16 + frow) * WRB + (s * 4 + fq) * 16);
+    if (g >= G) return;  // wave-uniform; no block barrier follows
+
+    // B operands of group g: [0..KS) reg features, [KS..2KS) cls features of pixel 16 g + frow
+    auto load_b = [&](long long gg, uint4 (&b)[2 * KS]) {
+        long long m = gg * 16 + frow;
+        m = m < M ? m : M - 1;
+        const int bi = (int)(m / hw), pix = (int)(m - (long long)bi * hw);
+        const T* pr = (const T*)d.reg.ptr + (long long)bi * d.reg.bstride + (long long)pix * d.reg.cstride + fq * 8;
+        const T* pc = (const T*)d.cls.ptr + (long long)bi * d.cls.bstride + (long long)pix * d.cls.cstride + fq * 8;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            b[s] = *(const uint4*)(pr + s * 32);
+            b[KS + s] = *(const uint4*)(pc + s * 32);
+        }
+    };
+    float* stg = stg_all[wave];
+    uint4 bc[2 * KS], bn[2 * KS];
+    load_b(g, bc);
+    const float st = d.stride;
+    for (; g < G; g += gstride) {
+        const bool more = g + gstride < G;
+        if (more) load_b(g + gstride, bn);
+        f32x4 acc[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int f = 0; f < NF; ++f) Mma<T>::run(acc[f], wr[f][s], f == 0 ? bc[s] : bc[KS + s]);
+        // ---- bias + decode -> this wave's staging rows (row = frow, the group's pixel)
+        const long long m0 = g * 16;
+        long long m = m0 + frow;
+        m = m < M ? m : M - 1;
+        const int pix = (int)(m - (m / hw) * hw);
+        const int gy = pix / d.w, gx = pix - gy * d.w;
+        float* row = stg + frow * rowf;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ch = f * 16 + fq * 4 + r;
+                float v = acc[f][r];
+                if (f == 0) {
+                    if (ch < 5) {
+                        v += bl[ch];
+                        if (ch < 4) {
+                            if (d.train != 2) v = ch < 2 ? (v + (float)(ch == 0 ? gx : gy)) * st : hd_exp(v) * st;
+                        } else {
+                            v = d.train == 1 ? v : hd_sigmoid(v);
+                        }
+                        row[ch] = v;
+                    }
+                } else if (ch - 16 < C) {
+                    v += bl[ch];
+                    row[5 + ch - 16] = d.train == 1 ? v : hd_sigmoid(v);
+                }
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): every lane's rows are in LDS
+        __builtin_amdgcn_wave_barrier();
+        // ---- the group's rows are contiguous in the output (split once at an image boundary)
+        const int n = (int)(M - m0 < 16 ? M - m0 : 16);
+        int t0 = 0, bi = (int)(m0 / hw), p0 = (int)(m0 - (long long)bi * hw);
+        while (t0 < n) {
+            const int cnt = min(n - t0, hw - p0);
+            float* dst = d.out + (long long)bi * d.out_bstride + (long long)(d.a_off + p0) * rowf;
+            const float* src = stg + t0 * rowf;
+            const int total4 = cnt * rowf / 4;  // cnt % 4 == 0: 16-byte runs
+            for (int q = lane; q < total4; q += 64) *(float4*)(dst + 4 * q) = *(const float4*)(src + 4 * q);
+            t0 += cnt;
+            ++bi;
+            p0 = 0;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // the staging reads are done before the next group's writes
+        __builtin_amdgcn_wave_barrier();
+        if (more) {
+#pragma unroll
+            for (int q = 0; q < 2 * KS; ++q) bc[q] = bn[q];
+        }
+    }
+}
+
 int head_pred_launch(const yxh_head_desc* d, hipStream_t st) {
     YXH_CHECK_ARG(d && d->out && d->cls.ptr && d->reg.ptr && d->w_reg && d->w_cls && d->b_reg && d->b_cls,
                   "head_pred: null pointer");
@@ -190,6 +325,29 @@ int head_pred_launch(const yxh_head_desc* d, hipStream_t st) {
     if (ncf != 5) {
         set_error("head_pred built for 65-80 classes (got %d)", d->num_classes);
         return YXH_EUNSUPPORTED;
+    }
+    // head_pred2 for 64 / 128 feature channels (YXH_HEAD_V1=1: the tile kernel, for A/B and the
+    // bit-identity test); 16-byte aligned feature rows
+    const char* v1e = getenv("YXH_HEAD_V1");
+    const bool v1 = v1e != nullptr && v1e[0] == '1';
+    const bool rows16 = ((uintptr_t)d->reg.ptr % 16) == 0 && ((uintptr_t)d->cls.ptr % 16) == 0 &&
+                        d->reg.cstride % 8 == 0 && d->cls.cstride % 8 == 0 && d->reg.bstride % 8 == 0 &&
+                        d->cls.bstride % 8 == 0;
+    if (!v1 && rows16 && (d->cin == 64 || d->cin == 128)) {
+        const long long groups = (M + 15) / 16;
+        const unsigned grid2 = (unsigned)std::min<long long>((groups + 7) / 8, 256);  // one 8-wave block per CU
+#define YXH_HEAD2(T, CIN) hipLaunchKernelGGL((head_pred2<T, CIN, 5>), dim3(grid2), dim3(512), 0, st, *d)
+        if (d->dtype == YXH_BF16 && d->cin == 128) YXH_HEAD2(bf16, 128);
+        else if (d->dtype == YXH_BF16) YXH_HEAD2(bf16, 64);
+        else if (d->dtype == YXH_F16 && d->cin == 128) YXH_HEAD2(f16, 128);
+        else if (d->dtype == YXH_F16) YXH_HEAD2(f16, 64);
+        else {
+            set_error("head_pred: dtype %d not built", d->dtype);
+            return YXH_EUNSUPPORTED;
+        }
+#undef YXH_HEAD2
+        YXH_CHECK_LAUNCH("head_pred2 launch");
+        return YXH_OK;
     }
     if (d->dtype == YXH_BF16 && d->cin == 128) YXH_HEAD(bf16, 128, 5);
     else if (d->dtype == YXH_BF16 && d->cin == 64) YXH_HEAD(bf16, 64, 5);

@@ -168,4 +168,67 @@ int letterbox_batch_launch(const uint8_t* pool, const yxh_lb_image* images, int 
     return YXH_OK;
 }
 
+// ---------------------------------------------------------------- multiscale resize
+// YoloxConfig.preprocess (config.py:296-305): F.interpolate(inputs, size=tsize, mode="bilinear",
+// align_corners=False) of the [B, C, H, W] training batch.  The arithmetic is ATen's bilinear
+// kernel term for term, in fp32 whatever the storage type (accscalar_t): scale = in / out,
+// src = max(scale * (dst + 0.5) - 0.5, 0), i0 = (int)src, i1 = i0 + (i0 < in - 1), l1 = src - i0,
+// l0 = 1 - l1, out = l0y * (l0x * a + l1x * b) + l1y * (l0x * c + l1x * d), rounded once to the
+// storage type -- so the device result is bit-identical to the reference's own call on this GPU
+// (tests/test_gpu_augment.py compares with torch's F.interpolate on the device).  Same size: a copy.
+// One thread per output element, x fastest: each wave reads two input rows of one plane.
+template <typename T>
+__global__ __launch_bounds__(256) void resize_bilinear(const T* __restrict__ src, int planes, int ih, int iw,
+                                                       T* __restrict__ dst, int oh, int ow, float rh, float rw) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long total = (long long)planes * oh * ow;
+    if (idx >= total) return;
+    const int ox = (int)(idx % ow);
+    const long long r = idx / ow;
+    const int oy = (int)(r % oh);
+    const long long pl = r / oh;
+    const T* s = src + pl * ih * iw;
+    if (ih == oh && iw == ow) {
+        dst[idx] = s[(long long)oy * iw + ox];
+        return;
+    }
+    float hr = rh * ((float)oy + 0.5f) - 0.5f;
+    hr = hr < 0.0f ? 0.0f : hr;
+    const int h1 = (int)hr;
+    const int h1p = h1 < ih - 1 ? 1 : 0;
+    const float h1l = hr - (float)h1;
+    const float h0l = 1.0f - h1l;
+    float wr = rw * ((float)ox + 0.5f) - 0.5f;
+    wr = wr < 0.0f ? 0.0f : wr;
+    const int w1 = (int)wr;
+    const int w1p = w1 < iw - 1 ? 1 : 0;
+    const float w1l = wr - (float)w1;
+    const float w0l = 1.0f - w1l;
+    const T* r0 = s + (long long)h1 * iw + w1;
+    const T* r1 = r0 + (long long)h1p * iw;
+    const float v = h0l * (w0l * to_f32(r0[0]) + w1l * to_f32(r0[w1p])) +
+                    h1l * (w0l * to_f32(r1[0]) + w1l * to_f32(r1[w1p]));
+    dst[idx] = from_f32<T>(v);
+}
+
+int resize_bilinear_launch(int dt, int B, int C, int ih, int iw, const void* src, int oh, int ow, void* dst,
+                           hipStream_t st) {
+    YXH_CHECK_ARG(src && dst, "resize: null pointer");
+    YXH_CHECK_ARG(B > 0 && C > 0 && ih > 0 && iw > 0 && oh > 0 && ow > 0, "resize sizes");
+    YXH_CHECK_ARG(dt == YXH_F32 || dt == YXH_BF16 || dt == YXH_F16, "resize dtype %d", dt);
+    const long long total = (long long)B * C * oh * ow;
+    YXH_CHECK_ARG(total < (1LL << 40), "resize: too many elements");
+    // area_pixel_compute_scale<float>: (float)input_size / output_size
+    const float rh = (float)ih / (float)oh, rw = (float)iw / (float)ow;
+    dim3 grid((unsigned)((total + 255) / 256));
+#define YXH_RS(T) hipLaunchKernelGGL(resize_bilinear<T>, grid, dim3(256), 0, st, (const T*)src, B * C, ih, iw, (T*)dst, \
+                                     oh, ow, rh, rw)
+    if (dt == YXH_F32) YXH_RS(float);
+    else if (dt == YXH_BF16) YXH_RS(bf16);
+    else YXH_RS(f16);
+#undef YXH_RS
+    YXH_CHECK_LAUNCH("resize_bilinear");
+    return YXH_OK;
+}
+
 }  // namespace yxh

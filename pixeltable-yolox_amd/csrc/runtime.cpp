@@ -59,6 +59,13 @@ int pack_dgrad_launch(const float* w, int cout, int cin, int kh, int kw, int c_b
 int spp_bwd_launch(int dt, int B, const yxh_src* cat, int c, const float* dcat, float* dx, hipStream_t st);
 int pack_batch_launch(const yxh_pack_job* jobs, int njobs, int total_blocks, int dt, hipStream_t st);
 int upsample_bwd_launch(const float* g, int B, int h, int w, int C, float* dst, hipStream_t st);
+size_t dw_wgrad_workspace_bytes(long long pixels, int channels, int k);
+int dw_wgrad_launch(int dt, int B, const yxh_src* x, const yxh_src* dy, int C, int k, int stride, int pad, int out_h,
+                    int out_w, float* dw, void* ws, size_t ws_bytes, hipStream_t st);
+int dw_dgrad_launch(int dt, int B, const yxh_src* dy, const void* w, int C, int k, int stride, int pad, int in_h,
+                    int in_w, float* dx, int dxcs, long long dxbs, int accumulate, hipStream_t st);
+int resize_bilinear_launch(int dt, int B, int C, int ih, int iw, const void* src, int oh, int ow, void* dst,
+                           hipStream_t st);
 int head_decode_train_launch(const float* raw, int B, int A, int C, const int* lhw, const int* strides, int nlev,
                              float* out, hipStream_t st);
 int yolox_loss_bwd(const float* preds, const float* raw, const float* labels, int B, int A, int C, int L,
@@ -230,6 +237,29 @@ int yxh_spp_bwd(int32_t dtype, int32_t batch, const yxh_src* cat, int32_t c, con
 
 int yxh_upsample_bwd(const float* g, int32_t batch, int32_t h, int32_t w, int32_t c, float* dst, void* stream) {
     return upsample_bwd_launch(g, batch, h, w, c, dst, (hipStream_t)stream);
+}
+
+size_t yxh_dw_wgrad_workspace_bytes(int32_t batch, int32_t out_h, int32_t out_w, int32_t channels, int32_t k) {
+    return dw_wgrad_workspace_bytes((long long)batch * out_h * out_w, channels, k);
+}
+
+int yxh_dw_wgrad(int32_t dtype, int32_t batch, const yxh_src* x, const yxh_src* dy, int32_t channels, int32_t k,
+                 int32_t stride, int32_t pad, int32_t out_h, int32_t out_w, float* dw, void* workspace,
+                 size_t workspace_bytes, void* stream) {
+    return dw_wgrad_launch(dtype, batch, x, dy, channels, k, stride, pad, out_h, out_w, dw, workspace, workspace_bytes,
+                           (hipStream_t)stream);
+}
+
+int yxh_dw_dgrad(int32_t dtype, int32_t batch, const yxh_src* dy, const void* w, int32_t channels, int32_t k,
+                 int32_t stride, int32_t pad, int32_t in_h, int32_t in_w, float* dx, int32_t dx_cstride,
+                 int64_t dx_bstride, int32_t accumulate, void* stream) {
+    return dw_dgrad_launch(dtype, batch, dy, w, channels, k, stride, pad, in_h, in_w, dx, dx_cstride, dx_bstride,
+                           accumulate, (hipStream_t)stream);
+}
+
+int yxh_resize_bilinear(int32_t dtype, int32_t batch, int32_t channels, int32_t in_h, int32_t in_w, const void* src,
+                        int32_t out_h, int32_t out_w, void* dst, void* stream) {
+    return resize_bilinear_launch(dtype, batch, channels, in_h, in_w, src, out_h, out_w, dst, (hipStream_t)stream);
 }
 
 int yxh_head_decode_train(const float* raw, int32_t batch, int32_t anchors, int32_t num_classes,

@@ -218,6 +218,12 @@ def lib():
             "yxh_pack_frag": ([vp, i32, i32, i32, i32, vp, vp], C.c_int),
             "yxh_spp_bwd": ([i32, i32, C.POINTER(Src), i32, vp, vp, vp], C.c_int),
             "yxh_upsample_bwd": ([vp, i32, i32, i32, i32, vp, vp], C.c_int),
+            "yxh_dw_wgrad_workspace_bytes": ([i32, i32, i32, i32, i32], sz),
+            "yxh_dw_wgrad": ([i32, i32, C.POINTER(Src), C.POINTER(Src), i32, i32, i32, i32, i32, i32, vp, vp, sz, vp],
+                             C.c_int),
+            "yxh_dw_dgrad": ([i32, i32, C.POINTER(Src), vp, i32, i32, i32, i32, i32, i32, vp, i32, i64, i32, vp],
+                             C.c_int),
+            "yxh_resize_bilinear": ([i32, i32, i32, i32, i32, vp, i32, i32, vp, vp], C.c_int),
             "yxh_head_decode_train": ([vp, i32, i32, i32, vp, vp, i32, vp, vp], C.c_int),
             "yxh_yolox_loss_bwd": ([vp, vp, vp, i32, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, i32, i32, vp,
                                     vp, vp], C.c_int),
@@ -254,7 +260,8 @@ EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_co
             "yxh_postprocess", "yxh_postprocess_ev", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes", "yxh_graph_create_dag",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
             "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_pack_weights_batch", "yxh_pack_frag", "yxh_spp_bwd",
-            "yxh_upsample_bwd", "yxh_head_decode_train", "yxh_yolox_loss_bwd", "yxh_opt_chunk_elems",
+            "yxh_upsample_bwd", "yxh_dw_wgrad_workspace_bytes", "yxh_dw_wgrad", "yxh_dw_dgrad", "yxh_resize_bilinear",
+            "yxh_head_decode_train", "yxh_yolox_loss_bwd", "yxh_opt_chunk_elems",
             "yxh_sgd_ema_step", "yxh_amp_found_inf", "yxh_amp_update_scale", "yxh_coco_eval", "yxh_coco_iou"]
 
 

@@ -7,7 +7,7 @@ configs are module-level singletons, as in the reference (quirk: they cache the
 model they build, config.py:168-172, 466-469).  The training-side factories the
 trainer calls are here too: ``get_optimizer`` (:307-333), ``get_lr_scheduler``
 (:335-348), ``random_resize`` (:275-294, rank-0 draw broadcast to every rank),
-``preprocess`` (:296-305, bilinear multiscale) and ``get_data_loader`` -- the latter
+``preprocess`` (:296-305, bilinear multiscale on the device) and ``get_data_loader`` -- the latter
 over a synthetic COCO-shaped dataset (no datasets offline; COCO files and the
 Mosaic/MixUp CPU pipeline are out of scope).
 """
@@ -225,16 +225,26 @@ class YoloxConfig:
         return (int(tensor[0].item()), int(tensor[1].item()))
 
     def preprocess(self, inputs, targets, tsize):
-        """config.py:296-305: bilinear resize of the batch to ``tsize`` (align_corners
-        False) with the box columns scaled to match."""
-        import torch.nn.functional as F
-        scale_y = tsize[0] / self.input_size[0]
-        scale_x = tsize[1] / self.input_size[1]
+        """config.py:296-305: bilinear resize of the batch to ``tsize`` (align_corners False:
+        yxh_resize_bilinear, one HIP launch, ATen's arithmetic) with the box columns scaled to
+        match (``scale_targets``)."""
+        from .utils.resize import resize_bilinear
+        if self._multiscale(tsize) != (1, 1):
+            inputs = resize_bilinear(inputs, tsize)
+            targets = self.scale_targets(targets, tsize)
+        return inputs, targets
+
+    def _multiscale(self, tsize):
+        return tsize[1] / self.input_size[1], tsize[0] / self.input_size[0]
+
+    def scale_targets(self, targets, tsize):
+        """The label half of ``preprocess`` (config.py:301-304): x columns (1, 3) and y columns
+        (2, 4) of [B, L, 5] targets scaled by tsize / input_size, in place."""
+        scale_x, scale_y = self._multiscale(tsize)
         if scale_x != 1 or scale_y != 1:
-            inputs = F.interpolate(inputs, size=tsize, mode="bilinear", align_corners=False)
             targets[..., 1::2] = targets[..., 1::2] * scale_x
             targets[..., 2::2] = targets[..., 2::2] * scale_y
-        return inputs, targets
+        return targets
 
     def get_trainer(self, args):
         from .trainer import Trainer

@@ -30,9 +30,10 @@ def _act_module(name: str) -> nn.Module:
 class _Planned(nn.Module):
     """Modules of this tree run as parts of a planned YoloxModule forward; standalone, a block's
     forward (the reference's eager call, e.g. ``module.backbone.backbone.dark3(x)``) runs a
-    one-block HIP plan of it (``plan_block``), cached per input shape.  Eval mode only: the plan
-    folds BatchNorm's running statistics (training-mode batch statistics run only inside
-    YoloxModule.forward(x, targets))."""
+    one-block HIP plan of it (``plan_block``, eval mode: BatchNorm's running statistics folded),
+    cached per input shape -- or, in train mode (a freshly built block is), the model train
+    step's kernels: BatchNorm batch statistics, running-statistics update, and autograd through
+    the HIP reverse pass (train.block_train_forward)."""
 
     takes_image = False  # plan_block's input: the [B, 3, H, W] image (Focus / CspDarknet) or a map
 
@@ -53,15 +54,16 @@ def _block_forward(block: nn.Module, x: torch.Tensor) -> list:
     a block plan: NCHW in, NCHW out in the parameters' dtype."""
     from .. import _native as N
     from ..engine import Plan
-    if block.training:
-        raise NotImplementedError(
-            f"{type(block).__name__}.forward in training mode (BatchNorm batch statistics) is not planned: "
-            "call .eval() first, or train through YoloxModule.forward(x, targets)")
     if not isinstance(x, torch.Tensor) or x.dim() != 4:
         raise ValueError(f"{type(block).__name__} takes one [B, C, H, W] tensor")
     p = _param0(block)
     if p.device.type != "cuda":
         raise RuntimeError(f"{type(block).__name__} runs on a ROCm device only; call .to('cuda') first")
+    if block.training:
+        from ..train import block_train_forward
+        if block.takes_image and x.shape[1] != 3:
+            raise ValueError(f"expected [B, 3, H, W] images, got {tuple(x.shape)}")
+        return block_train_forward(block, x)
     B, C, H, W = x.shape
     if block.takes_image:
         if C != 3:
@@ -70,7 +72,7 @@ def _block_forward(block: nn.Module, x: torch.Tensor) -> list:
             x = x.float()
     else:
         x = x.to(p.dtype)
-    key = ("block", B, C, H, W, x.dtype, p.dtype, str(p.device))
+    key = ("block", B, C, H, W, x.dtype, p.dtype, str(p.device), tuple(getattr(block, "out_features", ())))
     plan = _stage_plan(block, key, lambda: Plan(_StageModel(block), B, H, W, p.dtype, p.device, N.NCHW, x.dtype,
                                                 stage="block", block=block, head_inputs=[(C, H, W)]))
     return plan.run_block(x)
@@ -306,15 +308,30 @@ class CspDarknet(_Planned):
     def forward(self, x):
         """darknet.py:165-177 standalone: {"dark3", "dark4", "dark5"} feature maps of [B, 3, H, W]
         images (NCHW, the parameters' dtype) by a backbone-only HIP plan."""
-        if set(self.out_features) - {"dark3", "dark4", "dark5"}:
-            raise NotImplementedError("the planned CspDarknet returns dark3 / dark4 / dark5 only")
-        outs = dict(zip(("dark3", "dark4", "dark5"), _block_forward(self, x)))
-        return {k: v for k, v in outs.items() if k in self.out_features}
+        names = self._names()
+        return dict(zip(names, _block_forward(self, x)))
+
+    FEATURES = ("stem", "dark2", "dark3", "dark4", "dark5")
+
+    def _names(self) -> list:
+        """The requested maps in the reference's output order (darknet.py:165-177)."""
+        if set(self.out_features) - set(self.FEATURES):
+            raise AttributeError(f"unknown out_features {self.out_features}")
+        return [k for k in self.FEATURES if k in self.out_features]
 
     def plan_block(self, ctx, image):
-        return self.plan(ctx, image)
+        names = self._names()
+        if "stem" in names:  # the stem map exists only when Focus + stem run as their own launch
+            ctx.fuse_stem_s2 = False
+        outs = self.plan_all(ctx, image)
+        return [outs[k] for k in names]
 
     def plan(self, ctx, packed):
+        outs = self.plan_all(ctx, packed)
+        return outs["dark3"], outs["dark4"], outs["dark5"]
+
+    def plan_all(self, ctx, packed) -> dict:
+        """{stem (None when fused into the stride-2 launch), dark2 .. dark5} maps."""
         fused = ctx.stem_s2_fusable(self.stem.conv, self.dark2[0])
         csp2 = self.dark2[1]
         head2 = None
@@ -325,6 +342,7 @@ class CspDarknet(_Planned):
             x = None
         else:
             x = ctx.stem_s2(self.stem.conv, self.dark2[0], packed) if fused else self.stem.plan(ctx, packed)
+        stem = None if fused else x
         feats = []
         for stage in (self.dark2, self.dark3, self.dark4, self.dark5):
             blocks = list(stage)[1:]
@@ -347,7 +365,7 @@ class CspDarknet(_Planned):
                 else:
                     x = blk.plan(ctx, [x])
             feats.append(x)
-        return feats[1], feats[2], feats[3]  # dark3, dark4, dark5
+        return {"stem": stem, "dark2": feats[0], "dark3": feats[1], "dark4": feats[2], "dark5": feats[3]}
 
 
 class YoloPafpn(_Planned):

@@ -17,7 +17,9 @@ closures; ``backward`` replays it in reverse:
 * data gradient = a forward conv with transposed, flipped weights
   (yxh_pack_dgrad_weight; stride 2 via a zero-dilated source) accumulating into the
   fp32 gradient of each input view; nearest-x2 sources through yxh_upsample_bwd;
-* SPP max-pool backward (yxh_spp_bwd), residuals as plain adds.
+* SPP max-pool backward (yxh_spp_bwd), residuals as plain adds;
+* DWConv (yolox_nano): the depthwise conv forward on yxh_conv2d (groups = channels), its
+  gradients on yxh_dw_wgrad / yxh_dw_dgrad.
 
 Parameter gradients land in one flat fp32 buffer (``GradBuffer``) whose slices become
 ``param.grad``; a data-parallel reducer (yolox_amd.dp) can all-reduce it in buckets as
@@ -39,6 +41,7 @@ from .models.network import (BaseConv, Bottleneck, CspDarknet, CspLayer, DWConv,
 
 MAX_CHANNELS = 4096  # reduction workspace sizing (yolox_x: 1280)
 WGRAD_WS_BYTES = 64 << 20  # = the launchers' largest cap on per-split partials (16 Mi floats, tiles 25-28)
+DW_WS_BYTES = 16 << 20  # depthwise weight-gradient partials per stream (yolox_nano 640 batch 64: < 1 MiB)
 
 
 class Act:
@@ -267,11 +270,11 @@ class TrainGraph:
 
     def _conv(self, srcs: list, cin: int, cout: int, k: int, stride: int, pad: int, weight: int, bias: int,
               dst: int, dst_f32: bool, dst_cs: int, dst_bs: int, in_h: int, in_w: int, out_h: int, out_w: int,
-              batch: int, accumulate: bool = False) -> None:
+              batch: int, accumulate: bool = False, groups: int = 1) -> None:
         d = N.ConvDesc()
         d.dtype, d.batch = self.dcode, batch
         d.in_h, d.in_w, d.out_h, d.out_w = in_h, in_w, out_h, out_w
-        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.groups = cin, cout, k, k, stride, pad, 1
+        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.groups = cin, cout, k, k, stride, pad, groups
         d.nsrc = len(srcs)
         for j, s in enumerate(srcs):
             d.src[j] = s
@@ -283,8 +286,10 @@ class TrainGraph:
         d.flags = N.CONV_ACCUMULATE if accumulate else 0
         key = ("conv", self.dcode, batch, in_h, in_w, out_h, out_w, cin, cout, k, stride, pad, int(dst_f32),
                dst_cs, d.flags) + tuple(_src_key(q) for q in srcs)
-        d.tile = self._tile(key, d, self.lib.yxh_conv2d, "dst", batch * dst_bs * (4 if dst_f32 else self.esize),
-                            CONV_TUNE_TILES_F32 if self.dtype == torch.float32 else CONV_TUNE_TILES)
+        # depthwise convs have one kernel (dwconv): nothing to tune
+        d.tile = 0 if groups != 1 else self._tile(key, d, self.lib.yxh_conv2d, "dst",
+                                                  batch * dst_bs * (4 if dst_f32 else self.esize),
+                                                  CONV_TUNE_TILES_F32 if self.dtype == torch.float32 else CONV_TUNE_TILES)
         self._chk(self.lib.yxh_conv2d(C.byref(d), self.stream), "conv")
         if _LAUNCH_LOG is not None:
             _LAUNCH_LOG.append(("dgrad" if weight in self._dgrad_ptrs else "conv", k, stride, cin, cout, in_h, in_w,
@@ -311,6 +316,22 @@ class TrainGraph:
         if _LAUNCH_LOG is not None:
             _LAUNCH_LOG.append(("wgrad", k, stride, cin, cout, in_h, in_w, out_h, out_w, batch, d.tile, len(srcs),
                                 int(srcs[0].upsample), 0))
+
+    def _dw_wgrad(self, x: N.Src, dy: N.Src, C_: int, stride: int, out_h: int, out_w: int, batch: int,
+                  dw: torch.Tensor) -> None:
+        """Depthwise weight gradient (yxh_dw_wgrad): written into the gradient buffer; its per-block
+        partials go to a workspace of the issuing stream."""
+        need = int(self.lib.yxh_dw_wgrad_workspace_bytes(batch, out_h, out_w, C_, 3))
+        side = self._wside is not None and torch.cuda.current_stream(self.device) == self._wside
+        name = "_dw_ws_side" if side else "_dw_ws"
+        ws = getattr(self, name, None)
+        if ws is None:  # one fixed workspace per stream (never re-allocated under pending work)
+            ws = torch.empty(DW_WS_BYTES, dtype=torch.uint8, device=self.device)
+            setattr(self, name, ws)
+        if need > ws.numel():
+            raise NotImplementedError(f"depthwise weight gradient needs {need} B of partials (> {DW_WS_BYTES})")
+        self._chk(self.lib.yxh_dw_wgrad(self.dcode, batch, C.byref(x), C.byref(dy), C_, 3, stride, 1, out_h, out_w,
+                                        dw.data_ptr(), ws.data_ptr(), ws.numel(), self.stream), "dw wgrad")
 
     def _side_wgrad(self, launch: Callable[[], None], dy: torch.Tensor, param: nn.Parameter) -> None:
         """A conv's weight gradient on the side stream: it needs only dy and the forward's input
@@ -425,9 +446,11 @@ class TrainGraph:
     def base_conv(self, m: BaseConv, inputs: list, out: Optional[Act] = None, residual: Optional[Act] = None,
                   cin_store: Optional[int] = None) -> Act:
         """BaseConv.forward (network_blocks.py:48-49) in train mode; inputs: [(Act,
-        upsample)] concatenated along channels (torch.cat order)."""
-        if isinstance(m, DWConv) or m.conv.groups != 1:
-            raise NotImplementedError("depthwise (yolox_nano) training is not implemented")
+        upsample)] concatenated along channels (torch.cat order).  A DWConv (:55-74, yolox_nano)
+        is its depthwise BaseConv (groups = channels) then its pointwise one."""
+        if isinstance(m, DWConv):
+            t = self.base_conv(m.dconv, inputs)
+            return self.base_conv(m.pconv, [(t, 0)], out=out, residual=residual)
         conv, bn = m.conv, m.bn
         B = inputs[0][0].t.shape[0]
         cin = sum(a.ch for a, _ in inputs)
@@ -435,11 +458,14 @@ class TrainGraph:
         in_h, in_w = inputs[0][0].h << inputs[0][1], inputs[0][0].w << inputs[0][1]
         oh, ow = (in_h + 2 * p - k) // s + 1, (in_w + 2 * p - k) // s + 1
         cout = conv.out_channels
-        w, _ = self._fwd_weight(conv, cin)
+        dw = conv.groups != 1  # depthwise: groups == cin == cout, one un-upsampled source
+        if dw and not (conv.groups == cin == cout and len(inputs) == 1 and inputs[0][1] == 0 and k == 3 and p == 1):
+            raise NotImplementedError("grouped convs other than a 3x3 depthwise conv over one source")
+        w, _ = self._fwd_weight(conv, 1 if dw else cin)
         srcs = [a.src(up) for a, up in inputs]
         y = torch.empty(B, oh, ow, cout, dtype=self.dtype, device=self.device)
         self._conv(srcs, cin, cout, k, s, p, w.data_ptr(), self.zero_bias.data_ptr(), y.data_ptr(), False, cout,
-                   oh * ow * cout, in_h, in_w, oh, ow, B)
+                   oh * ow * cout, in_h, in_w, oh, ow, B, groups=conv.groups)
         stats = torch.empty(4, cout, dtype=torch.float32, device=self.device)
         ys = dense_src(y)
         self._chk(self.lib.yxh_bn_stats(
@@ -474,6 +500,16 @@ class TrainGraph:
                     residual.grad = out.grad
                 else:
                     residual.grad.add_(out.grad)
+            if dw:  # depthwise gradients: yxh_dw_wgrad (side stream) and yxh_dw_dgrad
+                self._side_wgrad(lambda: self._dw_wgrad(srcs[0], dense_src(dy), cout, s, oh, ow, B,
+                                                        gb.of(conv.weight)), dy, conv.weight)
+                a = inputs[0][0]
+                if a.needs_grad:
+                    g, acc = a.grad_target()
+                    self._chk(self.lib.yxh_dw_dgrad(self.dcode, B, C.byref(dense_src(dy)), w.data_ptr(), cout, k, s, p,
+                                                    in_h, in_w, g.data_ptr(), a.ch, in_h * in_w * a.ch, int(acc),
+                                                    self.stream), "dw dgrad")
+                return
             self._side_wgrad(lambda: self._wgrad(srcs, cin, cin_store, cout, k, s, p, dense_src(dy), gb.of(conv.weight),
                                                  in_h, in_w, oh, ow, B), dy, conv.weight)
             off, ins = 0, []
@@ -531,14 +567,18 @@ class TrainGraph:
 
     def darknet(self, m: CspDarknet, images: torch.Tensor):
         # darknet.py:165-177
+        outs = self.darknet_all(m, images)
+        return outs["dark3"], outs["dark4"], outs["dark5"]
+
+    def darknet_all(self, m: CspDarknet, images: torch.Tensor) -> dict:
         x = self.focus(m.stem, images)
-        feats = []
-        for stage in (m.dark2, m.dark3, m.dark4, m.dark5):
+        outs = {"stem": x}
+        for name, stage in (("dark2", m.dark2), ("dark3", m.dark3), ("dark4", m.dark4), ("dark5", m.dark5)):
             x = self.base_conv(stage[0], [(x, 0)])
             for blk in list(stage)[1:]:
                 x = self.spp(blk, [(x, 0)]) if isinstance(blk, SPPBottleneck) else self.csp(blk, [(x, 0)])
-            feats.append(x)
-        return feats[1], feats[2], feats[3]
+            outs[name] = x
+        return outs
 
     def pafpn(self, m: YoloPafpn, images: torch.Tensor):
         # yolo_pafpn.py:83-116
@@ -876,3 +916,95 @@ def train_forward(model, images: torch.Tensor, targets: torch.Tensor, dtype: Opt
     anchor = torch.zeros((), device=model.device, requires_grad=True)
     out["total_loss"] = _LossFn.apply(anchor, out["total_loss"], g)
     return out
+
+
+# ------------------------------------------------------------------ standalone blocks, train mode
+class _BlockOwner:
+    """What TrainGraph needs of its model for one building block: parameters and device."""
+
+    def __init__(self, block: nn.Module):
+        self.block = block
+
+    def parameters(self):
+        return self.block.parameters()
+
+    @property
+    def device(self) -> torch.device:
+        return next(self.block.parameters()).device
+
+
+class _BlockFn(torch.autograd.Function):
+    """A block's train-mode forward recorded on its TrainGraph tape; backward replays the tape
+    from the output gradients (parameter gradients published as in the model's step) and
+    returns the input's gradient."""
+
+    @staticmethod
+    def forward(ctx, anchor, x, graph, run):
+        outs, acts, in_act = run()
+        ctx.graph, ctx.acts, ctx.in_act, ctx.x_dtype = graph, acts, in_act, x.dtype
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        for a, go in zip(ctx.acts, gouts):
+            if go is not None:
+                a.grad = go.permute(0, 2, 3, 1).to(torch.float32).contiguous()
+        ctx.graph.backward(None)
+        a = ctx.in_act
+        gx = None
+        if a is not None and a.grad is not None:
+            gx = a.grad.permute(0, 3, 1, 2).to(ctx.x_dtype).contiguous()
+        return None, gx, None, None
+
+
+def block_train_forward(block: nn.Module, x: torch.Tensor, dtype: Optional[torch.dtype] = None) -> list:
+    """A building block's forward in training mode (network_blocks.py:27-208, darknet.py:95-177
+    called standalone on a train-mode module, as the reference's eager modules allow): BatchNorm
+    with batch statistics (running statistics and num_batches_tracked updated like torch), the
+    HIP kernels of the model's train step, and autograd through its reverse pass.  Returns the
+    block's output maps as NCHW tensors (CspDarknet: dark3, dark4, dark5)."""
+    from .models.network import BaseConv, Bottleneck, CspDarknet, CspLayer, DWConv, Focus, SPPBottleneck
+    dtype = dtype or compute_dtype_from_autocast()
+    owner = _BlockOwner(block)
+    g = block.__dict__.get("_train_graph_block")
+    if g is None or g.dtype != dtype or g.device != owner.device:
+        g = TrainGraph(owner, dtype)
+        block.__dict__["_train_graph_block"] = g
+    dev = owner.device
+    x = x.to(dev)
+
+    def run():
+        g.tape = []
+        g._bn_counters = []
+        g._pack_all()
+        in_act = None
+        if isinstance(block, (Focus, CspDarknet)):
+            images = x.contiguous() if x.dtype in (torch.float32, torch.bfloat16, torch.float16, torch.uint8) \
+                else x.float().contiguous()
+            g._keep = (images,)
+            if isinstance(block, Focus):
+                outs = [g.focus(block, images)]
+            else:
+                allm = g.darknet_all(block, images)
+                outs = [allm[k] for k in block._names()]
+        else:
+            t = x.detach().to(dtype).permute(0, 2, 3, 1).contiguous()
+            in_act = Act(t, 0, t.shape[3], needs_grad=x.requires_grad)
+            g._keep = (t,)
+            if isinstance(block, (BaseConv, DWConv)):
+                outs = [g.base_conv(block, [(in_act, 0)])]
+            elif isinstance(block, Bottleneck):
+                outs = [g.bottleneck(block, in_act)]
+            elif isinstance(block, CspLayer):
+                outs = [g.csp(block, [(in_act, 0)])]
+            elif isinstance(block, SPPBottleneck):
+                outs = [g.spp(block, [(in_act, 0)])]
+            else:
+                raise NotImplementedError(f"{type(block).__name__} has no train-mode block forward")
+        if g._bn_counters:
+            torch._foreach_add_(g._bn_counters, 1)
+        maps = [a.t[..., a.coff:a.coff + a.ch].permute(0, 3, 1, 2).contiguous() for a in outs]
+        return maps, outs, in_act
+
+    anchor = torch.zeros((), device=dev, requires_grad=True)
+    return list(_BlockFn.apply(anchor, x, g, run))

@@ -575,6 +575,27 @@ def gen_mosaic(ref) -> None:
     save("mosaic_aug.npz", **arrays)
 
 
+def gen_resize(ref) -> None:
+    """The reference's own YoloxConfig.preprocess (config.py:296-305: F.interpolate bilinear,
+    align_corners False, + the label scaling) on CPU over a seeded 160x160 batch (a copy of the
+    yolox_s config with input_size 160, so the fixture stays small) at down / up / non-square
+    sizes; float32.  The device kernel is bit-exact to ATen's bilinear on the GPU
+    (tests/test_gpu_augment.py); against this CPU run it is held to a few ulps (ATen's CPU
+    kernel contracts the same expression differently)."""
+    import copy
+    cfg = copy.copy(ref.config.YoloxConfig.get_named_config("yolox_s"))
+    cfg.input_size = (160, 160)
+    g = torch.Generator().manual_seed(77)
+    x = (torch.rand(2, 3, 160, 160, generator=g) * 255).round()
+    t = torch.rand(2, 6, 5, generator=g) * 150
+    arrays = {"input_u8": x.to(torch.uint8).numpy(), "targets": t.numpy()}
+    for size in ((128, 128), (192, 192), (224, 160), (96, 200)):
+        y, t2 = cfg.preprocess(x.clone(), t.clone(), size)
+        arrays[f"{size[0]}x{size[1]}.image"] = y.numpy()
+        arrays[f"{size[0]}x{size[1]}.targets"] = t2.numpy()
+    save("resize_preprocess.npz", **arrays)
+
+
 def main() -> None:
     if not os.path.isdir(REF):
         sys.exit("reference not present: fixtures can only be generated in the build container")

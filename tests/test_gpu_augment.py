@@ -89,3 +89,47 @@ def test_rejects_bad_output():
     p, _ = ds.draw(0)
     with pytest.raises(ValueError):
         ds.render([p], out=torch.empty((1, 3, H, W + 1), device="cuda"))
+
+
+# ------------------------------------------------------------------ multiscale resize
+def test_preprocess_resize_matches_reference_fixture(golden):
+    """YoloxConfig.preprocess (config.py:296-305) with the HIP resize (yxh_resize_bilinear) vs the
+    reference's own preprocess run on CPU (tests/golden/resize_preprocess.npz): labels exact;
+    pixels within a few fp32 ulps of the CPU run (ATen's CPU kernel contracts the bilinear sum
+    differently from its GPU kernel, to which the device result is bit-exact -- next test)."""
+    from yolox_amd.config import named_config
+    d = golden("resize_preprocess.npz")
+    cfg = named_config("yolox_s")
+    cfg.input_size = (160, 160)
+    x = torch.from_numpy(d["input_u8"]).float().cuda()
+    for key in [k[:-6] for k in d if k.endswith(".image")]:
+        size = tuple(int(v) for v in key.split("x"))
+        y, t = cfg.preprocess(x.clone(), torch.from_numpy(d["targets"]).cuda(), size)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(t.cpu().numpy(), d[f"{key}.targets"])
+        want = d[f"{key}.image"]
+        assert y.shape == want.shape and y.dtype == torch.float32
+        np.testing.assert_allclose(y.cpu().numpy(), want, rtol=0, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+def test_resize_bilinear_bit_exact_vs_aten_on_device(dtype):
+    """The reference's call itself, F.interpolate(bilinear, align_corners=False), on this GPU
+    (ATen's HIP kernel) against yxh_resize_bilinear: bit-identical over the yolox_s multiscale
+    range at the training batch shape (640 -> 480..800 in steps of 32, trainer.py:83 + config.py:
+    275-294), non-square sizes, odd sizes and the same-size copy; fp32, and fp16 / bf16 (--fp16
+    resizes the half batch)."""
+    import torch.nn.functional as F
+    from yolox_amd.utils.resize import resize_bilinear
+    g = torch.Generator().manual_seed(3)
+    x = (torch.rand(2, 3, 640, 640, generator=g) * 255).round().to(dtype).cuda()
+    sizes = [(s, s) for s in range(480, 801, 32)] + [(640, 640), (608, 672), (353, 517), (17, 23), (1, 1)]
+    for size in sizes:
+        got = resize_bilinear(x, size)
+        want = F.interpolate(x, size=size, mode="bilinear", align_corners=False)
+        assert got.shape == want.shape
+        assert torch.equal(got, want), (size, float((got.float() - want.float()).abs().max()))
+    small = torch.rand(1, 5, 7, 9, generator=g).to(dtype).cuda()  # C != 3, upsample from tiny maps
+    for size in [(14, 18), (3, 4), (21, 5)]:
+        assert torch.equal(resize_bilinear(small, size),
+                           F.interpolate(small, size=size, mode="bilinear", align_corners=False)), size

@@ -328,8 +328,94 @@ def test_building_blocks_callable_standalone(golden, key):
     assert tuple(y.shape) == tuple(ref.shape) and y.dtype == torch.float32
     assert (y.cpu() - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
     assert torch.equal(m(x), y)  # the cached plan again
-    with pytest.raises(NotImplementedError, match="training mode"):
-        m.train()(x)
+
+
+def _oracle_block(oracle, cls, args, kw, sd, x):
+    """The oracle's train-mode (batch-statistics BN) form of one BLOCK_CASES module."""
+    A = oracle.Arch(0.33, 0.25, act=kw.get("act", "silu"))
+    if cls == "Focus":
+        return oracle.base_conv(sd, "b.conv", oracle.focus(x), kw.get("ksize", 1), 1, A.act, A.bn_eps, bn_train=True)
+    if cls == "BaseConv":
+        return oracle.base_conv(sd, "b", x, args[2], args[3], A.act, A.bn_eps, bn_train=True)
+    if cls == "DWConv":
+        return oracle.conv(sd, "b", x, args[2], args[3], A, True, depthwise=True)
+    if cls == "Bottleneck":
+        return oracle.bottleneck(sd, "b", x, args[2], A, True)
+    if cls == "SPPBottleneck":
+        return oracle.spp(sd, "b", x, A, True)
+    return oracle.csp(sd, "b", x, kw.get("n", 1), kw.get("shortcut", True), A, True)
+
+
+@pytest.mark.parametrize("key", list(BLOCK_CASES))
+def test_building_blocks_train_mode(golden, oracle, key):
+    """A train-mode building block called on its own (a freshly built network_blocks.py module
+    is in train mode): BatchNorm batch statistics, the running statistics updated (momentum) and
+    num_batches_tracked + 1, and autograd through the HIP reverse pass -- output, input gradient
+    and every parameter gradient vs the oracle's fp32 autograd of the same block (1e-4 / 1e-3)."""
+    from yolox_amd.models import network
+    d = golden("blocks.npz")
+    cls, args, kw = BLOCK_CASES[key]
+    m = getattr(network, cls)(*args, **kw)
+    pre = f"{key}.p."
+    sd0 = {k[len(pre):]: torch.from_numpy(v) for k, v in d.items() if k.startswith(pre)}
+    m.load_state_dict(sd0)
+    for b in m.modules():
+        if isinstance(b, torch.nn.BatchNorm2d):
+            b.eps, b.momentum = 1e-3, 0.03  # the oracle's BN (config.py:162-166)
+    m = m.cuda().train()
+    x = torch.from_numpy(d[f"{key}.x"]).cuda().requires_grad_(cls != "Focus")
+    y = m(x)
+    g = torch.Generator().manual_seed(11)
+    r = torch.randn(tuple(y.shape), generator=g)
+    (y * r.cuda()).sum().backward()
+    torch.cuda.synchronize()
+    sdo = {f"b.{k}": v.clone().float().requires_grad_(v.is_floating_point() and "running" not in k
+                                                      and "num_batches" not in k) for k, v in sd0.items()}
+    xo = x.detach().cpu().clone().requires_grad_(cls != "Focus")
+    yo = _oracle_block(oracle, cls, args, kw, sdo, xo)
+    (yo * r).sum().backward()
+    assert tuple(y.shape) == tuple(yo.shape) and y.dtype == torch.float32
+    assert (y.detach().cpu() - yo.detach()).abs().max().item() <= 1e-4 * yo.abs().max().item()
+    if cls != "Focus":
+        assert (x.grad.cpu() - xo.grad).abs().max().item() <= 1e-3 * xo.grad.abs().max().item()
+    for name, prm in m.named_parameters():
+        gr = sdo[f"b.{name}"].grad
+        assert (prm.grad.cpu() - gr).abs().max().item() <= 1e-3 * (gr.abs().max().item() + 1e-12), name
+    for name, buf in m.named_buffers():  # running statistics: the oracle updated its copies in place
+        want = sdo[f"b.{name}"]
+        if name.endswith("num_batches_tracked"):
+            assert int(buf) == int(sd0[name]) + 1, name
+        else:
+            assert (buf.cpu() - want).abs().max().item() <= 1e-5 * (want.abs().max().item() + 1.0), name
+
+
+def test_cspdarknet_out_features_and_train_mode(golden):
+    """CspDarknet with the reference's other out_features (darknet.py:165-177: "stem", "dark2"):
+    eval -- a block plan that keeps the stem map (the fused stem launch is planned out), the shared
+    maps equal to the default plan's; train mode -- the same keys, finite gradients everywhere."""
+    from yolox_amd.models.network import CspDarknet
+    from yolox_amd.weights import synthetic_state_dict
+    d = golden("fwd_yolox_s_128.npz")
+    x = torch.from_numpy(d["input_u8"]).permute(0, 3, 1, 2).float().cuda()
+    full = CspDarknet(0.33, 0.5).cuda()
+    full.load_state_dict(synthetic_state_dict(full.state_dict(), seed=4))
+    every = CspDarknet(0.33, 0.5, out_features=("stem", "dark2", "dark3", "dark4", "dark5")).cuda()
+    every.load_state_dict(full.state_dict())
+    full.eval()
+    every.eval()
+    a, b = full(x), every(x)
+    assert list(b) == ["stem", "dark2", "dark3", "dark4", "dark5"]
+    assert tuple(b["stem"].shape) == (2, 32, 64, 64) and tuple(b["dark2"].shape) == (2, 64, 32, 32)
+    for k in ("dark3", "dark4", "dark5"):
+        assert (a[k] - b[k]).abs().max().item() <= 1e-4 * a[k].abs().max().item(), k
+    with pytest.raises(AttributeError):
+        CspDarknet(0.33, 0.5, out_features=("dark9",)).cuda().eval()(x)
+    every.train()
+    outs = every(x)
+    assert list(outs) == ["stem", "dark2", "dark3", "dark4", "dark5"]
+    sum(v.float().mean() for v in outs.values()).backward()
+    torch.cuda.synchronize()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in every.parameters())
 
 
 def test_backbone_stages_callable_standalone(golden):

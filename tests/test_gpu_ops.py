@@ -1118,11 +1118,15 @@ def test_conv_ws_residual_and_strided_dst():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("cin,h,w,train", [(128, 8, 12, 0), (64, 20, 20, 0), (256, 4, 8, 1), (128, 10, 10, 1)])
-def test_head_pred_fused_level(dtype, cin, h, w, train):
+@pytest.mark.parametrize("cin,h,w,train", [(128, 8, 12, 0), (64, 20, 20, 0), (256, 4, 8, 1), (128, 10, 10, 1),
+                                           (128, 6, 6, 2), (64, 12, 8, 1)])
+def test_head_pred_fused_level(dtype, cin, h, w, train, monkeypatch):
     """yxh_head_pred: reg/obj/cls 1x1 preds + cat + sigmoid + decode of one level into
     rows [a_off, a_off + h*w) of a [B, A, 85] output, vs torch fp32 on the same (rounded)
-    operands; other rows untouched.  Features are channel slices of wider buffers."""
+    operands; other rows untouched.  Features are channel slices of wider buffers.  train = 2:
+    decode_in_inference = False (reg raw, obj / cls sigmoid).  For 64 / 128 channels the
+    per-wave head_pred2 runs, bit-identical to the tile kernel (YXH_HEAD_V1=1) -- 10 x 10 and
+    6 x 6 levels put 16-pixel groups across image boundaries."""
     import ctypes as Cc
     n = N()
     B, C, A, a_off, stride = 3, 80, 4 * 7 + h * w + 12, 28, 16.0
@@ -1146,14 +1150,20 @@ def test_head_pred_fused_level(dtype, cin, h, w, train):
     d.out, d.out_bstride, d.a_off, d.stride, d.train = outd.data_ptr(), A * (5 + C), a_off, stride, train
     n.check(n.lib().yxh_head_pred(Cc.byref(d), n.stream_ptr()), "head_pred")
     got = outd.cpu()
+    monkeypatch.setenv("YXH_HEAD_V1", "1")
+    outd.fill_(-7.0)
+    n.check(n.lib().yxh_head_pred(Cc.byref(d), n.stream_ptr()), "head_pred (v1)")
+    assert torch.equal(outd.cpu(), got)
+    monkeypatch.delenv("YXH_HEAD_V1")
     ro = reg.float().reshape(B, h * w, cin) @ w_ro.float().T + b_ro
     cl = cls.float().reshape(B, h * w, cin) @ w_cl.float().T + b_cl
     gy, gx = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
     want = torch.cat([ro, cl], -1)
-    want[..., 0] = (want[..., 0] + gx.reshape(-1)) * stride
-    want[..., 1] = (want[..., 1] + gy.reshape(-1)) * stride
-    want[..., 2:4] = torch.exp(want[..., 2:4]) * stride
-    if not train:
+    if train != 2:
+        want[..., 0] = (want[..., 0] + gx.reshape(-1)) * stride
+        want[..., 1] = (want[..., 1] + gy.reshape(-1)) * stride
+        want[..., 2:4] = torch.exp(want[..., 2:4]) * stride
+    if train != 1:
         want[..., 4:] = torch.sigmoid(want[..., 4:])
     lvl = got[:, a_off:a_off + h * w]
     torch.testing.assert_close(lvl, want, rtol=1e-4, atol=1e-4)

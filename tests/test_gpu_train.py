@@ -556,12 +556,54 @@ def test_train_step_fp32_matches_oracle(oracle, use_l1):
             break
 
 
-@pytest.mark.parametrize("name", ["yolox_m", "yolox_x"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H,W,Cc,s", [(2, 16, 16, 16, 1), (2, 17, 13, 32, 2), (1, 9, 10, 64, 1), (3, 8, 8, 256, 2),
+                                        (2, 40, 40, 24, 2)])
+def test_depthwise_gradients(dtype, B, H, W, Cc, s):
+    """yxh_dw_wgrad / yxh_dw_dgrad (DWConv.dconv's gradients: F.conv2d(groups=C), 3x3, pad 1,
+    stride 1 / 2) against torch fp32 autograd on the same rounded operands; the weight gradient
+    twice bit-identical (fixed-order partial sums), the data gradient written or accumulated."""
+    from yolox_amd import _native as N
+    from yolox_amd.train import dense_src
+    g = torch.Generator().manual_seed(B * 1000 + Cc + s)
+    x = torch.randn(B, H, W, Cc, generator=g).to(dtype)
+    oh, ow = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
+    dy = torch.randn(B, oh, ow, Cc, generator=g).to(dtype)
+    wt = (torch.randn(Cc, 1, 3, 3, generator=g) * 0.3).to(dtype).float()
+    xd, dyd = x.cuda(), dy.cuda()
+    wpk = wt.reshape(Cc, 9).to(dtype).cuda().contiguous()
+    ws = torch.empty(int(lib().yxh_dw_wgrad_workspace_bytes(B, oh, ow, Cc, 3)), dtype=torch.uint8, device="cuda")
+    dws = []
+    for _ in range(2):
+        dw = torch.full((Cc, 1, 3, 3), float("nan"), device="cuda")
+        chk(lib().yxh_dw_wgrad(DT[dtype], B, C.byref(dense_src(xd)), C.byref(dense_src(dyd)), Cc, 3, s, 1, oh, ow,
+                               dw.data_ptr(), ws.data_ptr(), ws.numel(), stream()))
+        dws.append(dw)
+    prev = torch.randn(B, H, W, Cc, generator=g)
+    dx = prev.clone().cuda()
+    chk(lib().yxh_dw_dgrad(DT[dtype], B, C.byref(dense_src(dyd)), wpk.data_ptr(), Cc, 3, s, 1, H, W, dx.data_ptr(),
+                           Cc, H * W * Cc, 1, stream()))
+    dx0 = torch.full((B, H, W, Cc), float("nan"), device="cuda")
+    chk(lib().yxh_dw_dgrad(DT[dtype], B, C.byref(dense_src(dyd)), wpk.data_ptr(), Cc, 3, s, 1, H, W, dx0.data_ptr(),
+                           Cc, H * W * Cc, 0, stream()))
+    torch.cuda.synchronize()
+    xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_()
+    wr = wt.clone().requires_grad_()
+    F.conv2d(xr, wr, None, s, 1, 1, Cc).backward(dy.float().permute(0, 3, 1, 2))
+    assert torch.equal(dws[0], dws[1])
+    assert rel(dws[0], wr.grad) < 1e-5
+    want = xr.grad.permute(0, 2, 3, 1)
+    assert rel(dx0, want) < 1e-5
+    assert rel(dx, want + prev) < 1e-5
+
+
+@pytest.mark.parametrize("name", ["yolox_m", "yolox_x", "yolox_nano"])
 def test_train_step_other_widths_match_oracle(oracle, name):
     """yolox_m / yolox_x widths (48/80-channel CSP halves: concat splits that are not
-    K-stage aligned) train through the HIP path: fp32 losses and every parameter
-    gradient vs the oracle's autograd (1e-3), and an fp16 autocast step (the --fp16 of
-    BASELINE configs[4]) gives a finite loss close to the fp32 one."""
+    K-stage aligned) and yolox_nano (DWConv everywhere: the depthwise convs' gradients on
+    yxh_dw_wgrad / yxh_dw_dgrad, network_blocks.py:55-74) train through the HIP path: fp32
+    losses and every parameter gradient vs the oracle's autograd (1e-3), and an fp16 autocast
+    step (the --fp16 of BASELINE configs[4]) gives a finite loss close to the fp32 one."""
     from yolox_amd.config import named_config
     from yolox_amd.weights import synthetic_images, synthetic_labels, synthetic_state_dict
     m = named_config(name).get_model()
@@ -709,8 +751,8 @@ def test_captured_train_step_fp16_gradscaler_matches_eager(monkeypatch):
     same GradScaler + FusedStep, bit for bit over five steps: losses, every parameter, the EMA
     weights, the scale and the growth tracker.  Step 2 forces an overflow (scale 2^60: every
     replay reads the live scale, so the captured step overflows too) -- a skipped step and a
-    backoff of the scale happen between two replays; growth_interval 2 makes the scale grow
-    again within the five steps."""
+    backoff of the scale happen between two replays; from step 3 on a scale of 2^10 with
+    growth_interval 2 makes it grow after steps 3 and 4."""
     from yolox_amd.optim import FusedStep
     from yolox_amd.trainer import ModelEMA, train_one_iter
     import yolox_amd.train as T
@@ -733,9 +775,10 @@ def test_captured_train_step_fp16_gradscaler_matches_eager(monkeypatch):
     runs[1][5] = T.CapturedTrainStep(m, xs, ls, dtype=torch.float16, grad_scale=scaler._scale)
     scales = []
     for it in range(5):
-        if it == 2:
+        if it in (2, 3):  # step 2: forced overflow; step 3: a scale that does not overflow
             for r in runs:
-                r[3]._scale.fill_(2.0 ** 60)
+                r[3]._scale.fill_(2.0 ** 60 if it == 2 else 2.0 ** 10)
+                r[3]._growth_tracker.zero_()
         outs = []
         for m, opt, ema, scaler, fused, cap in runs:
             outs.append(train_one_iter(m, opt, xs, ls, amp_dtype=torch.float16, scaler=scaler, ema=ema, fused=fused,
@@ -751,7 +794,7 @@ def test_captured_train_step_fp16_gradscaler_matches_eager(monkeypatch):
             assert torch.equal(p, q), it
         scales.append(float(sa._scale))
     assert scales[2] == 2.0 ** 59  # the forced overflow: step skipped, scale backed off
-    assert scales[4] > scales[3] or scales[3] > scales[2]  # and grown again (growth_interval 2)
+    assert scales[3] == 2.0 ** 10 and scales[4] == 2.0 ** 11  # two good steps: grown (growth_interval 2)
 
 
 @pytest.mark.parametrize("opt_kind", ["sgd", "fused"])

@@ -32,7 +32,6 @@ def test_launch_world2_broadcast_and_rank_batches(tmp_path):
         assert r[0]["batches"][k] == stream[0::2][8 * k:8 * k + 8]
         assert r[1]["batches"][k] == stream[1::2][8 * k:8 * k + 8]
     assert not set(sum(r[0]["batches"], [])) & set(sum(r[1]["batches"], []))
-    assert r[0]["pre_shape"] == [1, 3, 96, 128]
     assert r[0]["pre_t"] == [1.0, 64.0, 24.0, 16.0, 6.0]  # x cols * 2, y cols * 1.5
 
 
