@@ -18,6 +18,10 @@
 
 namespace yxh {
 
+// conv_ws tiles for 80 / 160 / 320 / 512 input channels (yolox_x, yolox_l) and the fp32-gradient
+// forms (tiles 281-288): tile ids 261..260+kNumWsWideTiles (conv_ws_dispatch ids 61..)
+constexpr int kNumWsWideTiles = 28;
+
 // ---------------------------------------------------------------- implicit GEMM
 // Block: 256 threads = 4 waves on a WR x WC grid; tile TN output channels x TM
 // output pixels; KS 64-byte K slabs per pipeline stage.  LDS holds two stages; a
@@ -474,7 +478,12 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
         YXH_CHECK_ARG(q.upsample >= 0 && q.upsample <= 2, "upsample %d", q.upsample);
         YXH_CHECK_ARG(q.upsample != 2 || !dw, "dilated source on a depthwise conv");
         const int ush = q.upsample ? 1 : 0;
-        YXH_CHECK_ARG((q.h << ush) == d->in_h && (q.w << ush) == d->in_w,
+        // a zero-dilated source (a stride-2 conv's data gradient) of an odd-sized input: the
+        // dilated map's last row / column is odd, i.e. zero, so it may be cut off (logical size
+        // 2h - 1): reads past in_h / in_w are the conv's zero padding either way
+        const bool odd_ok = q.upsample == 2 && ((q.h << 1) - d->in_h) >= 0 && ((q.h << 1) - d->in_h) <= 1 &&
+                            ((q.w << 1) - d->in_w) >= 0 && ((q.w << 1) - d->in_w) <= 1;
+        YXH_CHECK_ARG(odd_ok || ((q.h << ush) == d->in_h && (q.w << ush) == d->in_w),
                       "src%d spatial %dx%d (up %d) vs input %dx%d", s, q.h, q.w, q.upsample, d->in_h, d->in_w);
         dilated |= q.upsample == 2;
         chs += q.channels;
@@ -641,13 +650,15 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
                           (tile > 200 && tile <= 200 + kNumWs1Tiles) || (tile > 210 && tile <= 210 + kNumPw1fTiles) ||
                           (tile > 214 && tile <= 214 + kNumDgradS2Tiles) ||
                           (tile > 220 && tile <= 220 + kNumWsPostTiles) ||
-                          (tile > 240 && tile <= 240 + kNumWs1DeepTiles),
+                          (tile > 240 && tile <= 240 + kNumWs1DeepTiles) ||
+                          (tile > 260 && tile <= 260 + kNumWsWideTiles),
                       "tile %d", d->tile);
         YXH_CHECK_ARG(want_ks == 1 || ks == 2, "2-slab staging not possible for this conv");
         ks = want_ks;
     }
     const int kstage = 4 * ks * epc;
     p.ncb = (d->cin + kstage - 1) / kstage;
+    if (tile > 260) return conv_ws_dispatch(dt, tile - 260 + 60, p, st);
     if (tile > 240) return conv_ws1_dispatch(dt, tile - 240 + kNumWs1Tiles, p, st);
     if (tile > 220) return conv_ws_dispatch(dt, tile - 220 + 40, p, st);
     if (tile > 214) return dgrad_s2f_dispatch(dt, tile - 214, p, st);

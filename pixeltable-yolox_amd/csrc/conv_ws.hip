@@ -37,6 +37,17 @@ namespace {
 
 // the value must live in AGPRs here (an empty asm with an "a" operand): the register allocator
 // then keeps it there and the MFMAs read it in place
+// a stationary weight fragment of a conv whose CR input channels are not a multiple of 32: row
+// pieces of the [cout][9][CR] weights, zero past CR (the halo holds zeros there too)
+template <typename T, int CR>
+__device__ __forceinline__ uint4 ws_weight_padk(const ConvParams& p, int n_first, int tap, int kb, int lane) {
+    const int frow = lane & 15, fq = lane >> 4;
+    const int ch = kb * 32 + fq * 8;
+    if (ch >= CR) return make_uint4(0, 0, 0, 0);
+    const int n = min(n_first + frow, p.cout - 1);
+    return *(const uint4*)((const T*)p.w + ((long long)n * 9 + tap) * CR + ch);
+}
+
 __device__ __forceinline__ void pin_agpr(uint4& v) {
     typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
     u32x4v t = {v.x, v.y, v.z, v.w};
@@ -57,8 +68,14 @@ constexpr int ws_hxp(int tx, int s) {
 
 }  // namespace
 
+// CR: the conv's real input channels when CIN (the K of the tile, a multiple of 32) pads them
+// (yolox_x's 80-channel stage: CIN 96) -- the halo DMA zero-fills chunks past CR, the weight
+// fragments past CR are zero
+// A32: fp32 destination, written or (YXH_CONV_ACCUMULATE) added to -- the data gradient of a
+// stride-1 3x3 conv in the training step (yolox_amd/train.py _dgrad: dy with the transposed,
+// flipped weights into the input's fp32 gradient), no bias / activation / residual
 template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC, bool F1, int PGN = 0,
-          int PGC = 0, int PGH = 0>
+          int PGC = 0, int PGH = 0, int CR = CIN, bool A32 = false>
 __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, int tiles_x, int tiles_y,
                                                                  int ntiles, int ntn, int nwork) {
     static_assert(sizeof(T) == 2, "16-bit operands");
@@ -112,7 +129,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0 && TM % (16 * WM) == 0, "tile");
     // weights must stay in VGPRs: 160 of 256 (2 waves per SIMD), 288 of 512 (one 4-wave block per CU)
     static_assert(FR * 9 * WCB * 4 <= (NW == 4 && BPC == 1 ? 288 : 160), "weights must stay in VGPRs");
-    static_assert(SMEM <= 160 * 1024, "LDS");
+    static_assert(SMEM <= 160 * 1024 && SMEM * BPC <= 160 * 1024, "LDS (BPC blocks per CU must fit)");
     // 288-register weight sets (one 4-wave block per CU): the first NPIN weight fragments are pinned
     // to AGPRs where the first tile first reads them, and the MFMAs take them from there (gfx950's
     // MFMA reads A operands from AGPRs).  Left to itself the register allocator parks ~30 % of the
@@ -147,7 +164,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 
     const uint32_t lds0 = dma::lds_addr(smem);
     const uint32_t bytes = (uint32_t)((long long)in_h * in_w * scs * 2);
-    const int gsrc = p.grp2 && n0 >= cout / 2 ? CIN : 0;  // YXH_CONV_GROUPS2: this half's source channels
+    const int gsrc = p.grp2 && n0 >= cout / 2 ? CR : 0;  // YXH_CONV_GROUPS2: this half's source channels
 
     // per-lane halo slot geometry, fixed for the block's life: the slot's pixel (hy, hx)
     // in the halo and its source byte offset relative to the halo's top-left pixel
@@ -158,7 +175,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         const int s = 64 * L + lane;
         const int hp = s / PS, c16 = s - hp * PS;
         const int hy = hp / HXP, hx = hp - hy * HXP;
-        const bool st = L < LOADS && s < SLOTS && c16 < C16 && hx < HX;
+        const bool st = L < LOADS && s < SLOTS && c16 < CR / 8 && hx < HX;
         hyx[i] = st ? (hy | (hx << 16)) : 0x7fff7fff;  // 0x7fff fails every range check
         hrel[i] = ((hy * in_w + hx) * scs + c16 * 8) * 2;
     }
@@ -190,7 +207,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     const bool silu = p.act == YXH_ACT_SILU;
     const bool has_res = p.res != nullptr;
     const bool pg_store = PG && p.pg_store;
-    const uint32_t dbytes = (uint32_t)((long long)ohw * p.dst_cs * 2);
+    const uint32_t dbytes = (uint32_t)((long long)ohw * p.dst_cs * (A32 ? 4 : 2));
     const uint32_t rbytes = (uint32_t)((long long)ohw * p.res_cs * 2);
     const int dcs = p.dst_cs, rcs = p.res_cs;
     const uint32_t res_lds = lds0 + (uint32_t)(2 * HBYTES + RBYTES);
@@ -292,7 +309,8 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
             for (int i = 0; i < FR; ++i)
-                a[i][tap][c] = ws_weight<T>(p, n0 + wn * WTN + i * 16, tap, 9, CIN, wk * WCB + c, lane);
+                a[i][tap][c] = CR == CIN ? ws_weight<T>(p, n0 + wn * WTN + i * 16, tap, 9, CIN, wk * WCB + c, lane)
+                                         : ws_weight_padk<T, CR>(p, n0 + wn * WTN + i * 16, tap, wk * WCB + c, lane);
     float bias[FR][4];
 #pragma unroll
     for (int i = 0; i < FR; ++i) {
@@ -326,8 +344,8 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     struct EpiCtx { __amdgpu_buffer_rsrc_t dsrd; const char* rl; TileC c; };
     auto epi_ctx = [&](const TileC c, const int k) -> EpiCtx {
-        return EpiCtx{__builtin_amdgcn_make_buffer_rsrc((void*)((T*)p.dst + (long long)c.b * p.dst_bs), (short)0,
-                                                        (int)dbytes, 0x00020000),
+        char* db = (char*)p.dst + (long long)c.b * p.dst_bs * (A32 ? 4 : 2);
+        return EpiCtx{__builtin_amdgcn_make_buffer_rsrc((void*)db, (short)0, (int)dbytes, 0x00020000),
                       smem + 2 * HBYTES + RBYTES + (k % NRING) * RTB, c};
     };
     // one (pixel fragment o, channel fragment i) piece of the epilogue
@@ -338,6 +356,14 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         const int oy = e.c.oy0 + ty, ox = e.c.ox0 + tx;
         const int nl = wn * WTN + i * 16 + fq * 4, n = n0 + nl;
         const bool ok = j < FC && oy < OH && ox < OW && n < cout;
+        if constexpr (A32) {  // fp32 data gradient: 16-byte read-add-store of 4 channels
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const int od4 = ok ? ((oy * OW + ox) * dcs + n) * 4 : (int)dma::kOob;
+            f32x4 v = ap[i][o] + f32x4{bias[i][0], bias[i][1], bias[i][2], bias[i][3]};
+            if (p.accum) v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(e.dsrd, od4, 0, 0));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), e.dsrd, od4, 0, 0);
+            return;
+        }
         const int od = ok ? ((oy * OW + ox) * dcs + n) * 2 : (int)dma::kOob;
         u32x2 rv = {0u, 0u};
         if constexpr (GR > 0) rv = *(const u32x2*)(e.rl + (pl * RS + (nl >> 3)) * 16 + (nl & 7) * 2);
@@ -689,10 +715,14 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 }
 
 template <typename T, int CIN, int S, int TX, int TY, int TN, int WN, int WK, int WM, int BPC = 1, bool F1 = false,
-          int PGN = 0, int PGC = 0, int PGH = 0>
+          int PGN = 0, int PGC = 0, int PGH = 0, int CR = CIN, bool A32 = false>
 static int launch_ws(const ConvParams& p, hipStream_t st) {
-    if (p.stride != S || p.cin != CIN) {
-        set_error("conv_ws variant built for stride %d, %d input channels", S, CIN);
+    if (p.stride != S || p.cin != CR) {
+        set_error("conv_ws variant built for stride %d, %d input channels", S, CR);
+        return YXH_EUNSUPPORTED;
+    }
+    if (CR != CIN && (p.grp2 || PGN > 0 || PGH > 0 || F1 || p.scs[0] % 8 || (uintptr_t)p.sptr[0] % 16)) {
+        set_error("conv_ws padded-K variant (%d -> %d channels): plain conv over 16-byte pixel rows only", CR, CIN);
         return YXH_EUNSUPPORTED;
     }
     if (PGH > 0) {
@@ -717,7 +747,13 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
                   CIN);
         return YXH_EUNSUPPORTED;
     }
-    if (p.dst_f32 || p.accum || (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) ||
+    if (A32) {
+        if (!p.dst_f32 || p.act != YXH_ACT_NONE || p.res || p.grp2 || p.cout % 4 || ((uintptr_t)p.dst % 16) ||
+            p.dst_cs % 4 || p.dst_bs % 4 || (long long)p.ohw * p.dst_cs * 4 >= (1LL << 31)) {
+            set_error("conv_ws fp32-gradient tile: fp32 dst of 16-byte rows, no activation / residual");
+            return YXH_EUNSUPPORTED;
+        }
+    } else if (p.dst_f32 || p.accum || (p.act != YXH_ACT_SILU && p.act != YXH_ACT_NONE) ||
         (!p.vec_store && PGN == 0 && PGH == 0) ||
         p.cout % 8 || (p.res && (S != 1 || ((uintptr_t)p.res % 16) || p.res_cs % 8 || p.res_bs % 8))) {
         set_error("conv_ws: 16-bit dst, SiLU/no activation, 8-byte aligned dst rows, 16-byte residual rows "
@@ -732,7 +768,7 @@ static int launch_ws(const ConvParams& p, hipStream_t st) {
         return YXH_EINVAL;
     }
     const int nwork = (int)std::min<long long>(ntiles, std::max(1, p.cus * BPC / ntn));
-    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM, BPC, F1, PGN, PGC, PGH>), dim3((unsigned)(nwork * ntn)),
+    hipLaunchKernelGGL((conv_ws<T, CIN, S, TX, TY, TN, WN, WK, WM, BPC, F1, PGN, PGC, PGH, CR, A32>), dim3((unsigned)(nwork * ntn)),
                        dim3(64 * WN * WK * WM), 0, st, p, tiles_x, tiles_y, (int)ntiles, ntn, nwork);
     YXH_CHECK_LAUNCH("conv_ws launch");
     return YXH_OK;
@@ -815,6 +851,37 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 54: return launch_ws<T, 64, 1, 16, 4, 64, 2, 1, 2, 1, false, 64, 0>(p, st);
         case 55: return launch_ws<T, 128, 1, 8, 4, 128, 4, 1, 1, 1, false, 128, 0>(p, st);
         case 56: return launch_ws<T, 128, 1, 16, 2, 128, 4, 1, 1, 1, false, 128, 0>(p, st);
+        // wide / odd input channels (ids 61-80 = tiles 261-280): yolox_x (80 / 160 / 320, widths x1.25)
+        // and yolox_l (512) 3x3s.  Register budget per wave: <= 160 weight registers at two waves per SIMD,
+        // <= 288 at one; LDS: two halo buffers of CIN / 8 + 2 16-byte slots per pixel (the big-CIN tiles
+        // are one or two pixel rows high).  80 input channels run as K = 96 (zero chunks).  Withdrawn:
+        // ids 70, 73, 75, 77, 78 (10- / 16-wave blocks: 168 / 128 registers per wave, they spilled) --
+        // 640 input channels have no form that fits (K = 20 blocks: 180 weight registers at WK 4)
+        case 61: return launch_ws<T, 96, 1, 16, 4, 80, 5, 1, 1, 1, false, 0, 0, 0, 80>(p, st);
+        case 62: return launch_ws<T, 96, 1, 16, 4, 32, 2, 1, 2, 2, false, 0, 0, 0, 80>(p, st);
+        case 63: return launch_ws<T, 96, 2, 16, 4, 80, 5, 1, 1, 1, false, 0, 0, 0, 80>(p, st);
+        case 64: return launch_ws<T, 96, 2, 16, 4, 32, 2, 1, 2, 1, false, 0, 0, 0, 80>(p, st);
+        case 65: return launch_ws<T, 160, 1, 16, 4, 64, 4, 1, 1>(p, st);
+        case 66: return launch_ws<T, 160, 1, 16, 4, 32, 2, 1, 2>(p, st);
+        case 67: return launch_ws<T, 160, 2, 16, 2, 64, 4, 1, 1>(p, st);
+        case 68: return launch_ws<T, 160, 2, 16, 2, 32, 2, 1, 2>(p, st);
+        case 69: return launch_ws<T, 320, 1, 8, 4, 32, 2, 2, 1>(p, st);
+        case 71: return launch_ws<T, 320, 1, 16, 2, 32, 2, 2, 1>(p, st);
+        case 72: return launch_ws<T, 320, 2, 16, 1, 32, 2, 2, 1>(p, st);
+        case 74: return launch_ws<T, 512, 1, 8, 2, 32, 2, 4, 1>(p, st);
+        case 76: return launch_ws<T, 512, 1, 16, 1, 32, 2, 4, 1>(p, st);
+        case 79: return launch_ws<T, 160, 1, 16, 2, 64, 4, 1, 1>(p, st);
+        case 80: return launch_ws<T, 96, 1, 8, 4, 32, 2, 1, 2, 2, false, 0, 0, 0, 80>(p, st);
+        // fp32-gradient forms (ids 81-88 = tiles 281-288): the stride-1 3x3 data gradients of the training
+        // step (yolox_x's 80 / 160 / 320-channel maps; yolox_s / yolox_l's 64 / 128 / 256)
+        case 81: return launch_ws<T, 96, 1, 16, 4, 32, 2, 1, 2, 2, false, 0, 0, 0, 80, true>(p, st);
+        case 82: return launch_ws<T, 160, 1, 16, 4, 64, 4, 1, 1, 1, false, 0, 0, 0, 160, true>(p, st);
+        case 83: return launch_ws<T, 160, 1, 16, 4, 32, 2, 1, 2, 1, false, 0, 0, 0, 160, true>(p, st);
+        case 84: return launch_ws<T, 320, 1, 8, 4, 32, 2, 2, 1, 1, false, 0, 0, 0, 320, true>(p, st);
+        case 85: return launch_ws<T, 320, 1, 16, 2, 32, 2, 2, 1, 1, false, 0, 0, 0, 320, true>(p, st);
+        case 86: return launch_ws<T, 64, 1, 16, 4, 64, 2, 1, 2, 2, false, 0, 0, 0, 64, true>(p, st);
+        case 87: return launch_ws<T, 128, 1, 16, 4, 128, 4, 1, 1, 1, false, 0, 0, 0, 128, true>(p, st);
+        case 88: return launch_ws<T, 256, 1, 8, 4, 64, 2, 4, 1, 1, false, 0, 0, 0, 256, true>(p, st);
         default: set_error("conv_ws tile id %d", id); return YXH_EINVAL;
     }
 }

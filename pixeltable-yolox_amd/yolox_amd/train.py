@@ -136,10 +136,12 @@ class GradBuffer:
 # tiles 1-10.  YOLOX_AMD_TRAIN_TUNE=0 keeps the by-shape defaults.
 _BASE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52)) for k in (0, 1)]
 # 16-bit (autocast) steps also try the inference path's 16-bit kernels for the forward convs: dense
-# 1x1 conv_pwf (97-104), weight-stationary 3x3 conv_ws (161-190) and 1x1 conv_ws1 (201-210); they
-# refuse the fp32-accumulating data-gradient form, which stays on the tiles above
+# 1x1 conv_pwf (97-104), weight-stationary 3x3 conv_ws (161-190, 261-280: yolox_x / yolox_l widths) and
+# 1x1 conv_ws1 (201-210); of those only conv_ws's fp32-gradient tiles (281-288) take the data
+# gradient's fp32-accumulating form (stride-1 3x3s), the rest stays on the tiles above
 CONV_TUNE_TILES = _BASE_TILES + ([] if os.environ.get("YOLOX_AMD_TRAIN_TILES16") == "base" else
-                                 [2 * i for i in list(range(97, 105)) + list(range(161, 191)) + list(range(201, 211))])
+                                 [2 * i for i in list(range(97, 105)) + list(range(161, 191)) + list(range(201, 211))
+                                  + list(range(261, 289))])
 CONV_TUNE_TILES_F32 = _BASE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)] + [2 * i for i in range(211, 217)]
 WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 25)) + list(range(25, 29))
 _TRAIN_TILES: dict = {}

@@ -760,6 +760,42 @@ def test_conv_ws_3x3(dtype, geom):
     assert ran >= 1
 
 
+WS_WIDE_WITHDRAWN = {270, 273, 275, 277, 278}  # spilled (10- / 16-wave blocks): EINVAL
+WS_WIDE_GEOMS = [  # cin, cout, s, H, W (input), batch: yolox_x (80 / 160 / 320) and yolox_l (512) 3x3s
+    (80, 80, 1, 35, 41, 2), (80, 160, 2, 66, 70, 2), (160, 160, 1, 40, 38, 2), (160, 320, 2, 42, 38, 2),
+    (320, 320, 1, 20, 22, 2), (320, 320, 2, 20, 20, 2), (320, 640, 2, 21, 19, 2), (512, 512, 1, 12, 14, 2),
+    (320, 96, 1, 9, 7, 3)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("geom", WS_WIDE_GEOMS)
+def test_conv_ws_3x3_wide_channels(dtype, geom):
+    """conv_ws tiles 261-280 (80 -- as K 96 with zero chunks --, 160, 320, 512 input channels: the
+    yolox_x / yolox_l 3x3s) vs the fp32 reference: every variant built for this (cin, stride),
+    channel-slice sources, partial tiles, cout tails, K split over up to ten waves."""
+    cin, cout, s, H, W, B = geom
+    conv, bn = make_conv(cin, cout, 3, s, seed=cin + cout + s)
+    x = torch.randn(B, cin, H, W, generator=torch.Generator().manual_seed(H + W))
+    want = ref_conv(x, conv, bn, "silu")
+    wide = torch.zeros(B, H, W, cin + 32, dtype=dtype, device=DEV)
+    wide[..., 16:16 + cin] = nhwc(x, dtype)
+    ran = 0
+    for tid in range(261, 281):
+        if tid in WS_WIDE_WITHDRAWN:
+            continue
+        try:
+            y = run_conv([(wide, 16, cin, 0)], conv, bn, dtype, tile=2 * tid)
+        except NotImplementedError as e:
+            assert "input channels" in str(e), e
+            continue
+        close(y.permute(0, 3, 1, 2), want, dtype)
+        if cout % 16 == 0 and cin % 32 == 0:  # fragment-major weights: the same values, bit for bit
+            yf = run_conv([(wide, 16, cin, 0)], conv, bn, dtype, tile=2 * tid, frag=True)
+            assert torch.equal(yf, y), tid
+        ran += 1
+    assert ran >= 1, geom
+
+
 POST_GEOMS = [  # cin(=cout), stride, post_src channels, post_cout, H, W (input), batch
     (32, 1, 32, 64, 37, 45, 3), (32, 1, 32, 64, 160, 160, 2), (64, 1, 64, 128, 40, 24, 3),
     (64, 1, 64, 128, 80, 80, 4), (64, 2, 0, 128, 42, 38, 2), (64, 2, 0, 128, 160, 160, 2)]

@@ -201,6 +201,57 @@ def test_conv_wgrad_and_dgrad(dtype, cin0, cin1, up1, cout, k, s, H):
     assert rel(dx0 - 0.5, xin.grad[:, :cin0].permute(0, 2, 3, 1)) < tol
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("cfwd,H,W,B", [(80, 19, 23, 2), (160, 20, 18, 2), (320, 11, 13, 2), (64, 24, 20, 3),
+                                        (128, 17, 15, 2), (256, 9, 10, 2)])
+def test_dgrad_conv_ws_fp32_tiles(dtype, cfwd, H, W, B):
+    """The data gradient of a stride-1 3x3 conv on conv_ws's fp32-gradient tiles (281-288: yolox_x's
+    80 / 160 / 320 channels, yolox_s / yolox_l's 64 / 128 / 256): dy with the transposed, flipped
+    weights written into / added onto an fp32 gradient (YXH_CONV_ACCUMULATE), vs torch fp32 autograd
+    and vs the register-staged conv_igemm tile of the same data gradient."""
+    from yolox_amd import _native as N
+    from yolox_amd.train import dense_src
+    g = torch.Generator().manual_seed(cfwd + H)
+    cin, cout = cfwd, cfwd
+    dy = torch.randn(B, H, W, cout, generator=g).to(dtype)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * 0.05
+    wtd, dyd = wt.cuda(), dy.cuda()
+    pk = torch.empty(cin * 9 * cout, dtype=dtype, device="cuda")
+    chk(lib().yxh_pack_dgrad_weight(wtd.data_ptr(), cout, cin, 3, 3, 0, cin, cout, DT[dtype], pk.data_ptr(), stream()))
+    zb = torch.zeros(cin, device="cuda")
+    xr = torch.zeros(B, cin, H, W, requires_grad=True)
+    F.conv2d(xr, wt.to(dtype).float(), padding=1).backward(dy.float().permute(0, 3, 1, 2))
+    want = xr.grad.permute(0, 2, 3, 1)
+
+    def dgrad(tile, acc):
+        dx = torch.full((B, H, W, cin), 0.5 if acc else float("nan"), device="cuda")
+        d = N.ConvDesc()
+        d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w = DT[dtype], B, H, W, H, W
+        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.groups, d.nsrc = cout, cin, 3, 3, 1, 1, 1, 1
+        d.src[0] = dense_src(dyd)
+        d.weight, d.bias, d.dst, d.dst_dtype = pk.data_ptr(), zb.data_ptr(), dx.data_ptr(), 0
+        d.dst_cstride, d.dst_bstride, d.act = cin, H * W * cin, 0
+        d.flags, d.tile = (N.CONV_ACCUMULATE if acc else 0), tile
+        rc = lib().yxh_conv2d(C.byref(d), stream())
+        if rc == N.EUNSUPPORTED:
+            return None
+        chk(rc)
+        torch.cuda.synchronize()
+        return dx - 0.5 if acc else dx
+
+    base = dgrad(2 * 1, True)  # conv_igemm
+    ran = 0
+    for tid in range(281, 289):
+        for acc in (False, True):
+            got = dgrad(2 * tid, acc)
+            if got is None:
+                continue
+            assert rel(got, want) < 1e-4, (tid, acc)  # same rounded operands: summation order only
+            assert rel(got, base) < 1e-4, (tid, acc)
+            ran += 1
+    assert ran >= 2
+
+
 WG_TILE_CASES = [  # cin0, cin1, up1, cout, k, s, H, B
     (32, 0, 0, 64, 3, 1, 16, 2), (64, 0, 0, 32, 3, 2, 20, 3), (64, 64, 1, 128, 1, 1, 8, 2),
     (128, 0, 0, 128, 3, 1, 9, 2), (16, 0, 0, 24, 3, 1, 12, 1), (256, 0, 0, 192, 1, 1, 23, 2),
