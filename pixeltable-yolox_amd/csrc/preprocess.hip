@@ -173,9 +173,10 @@ int letterbox_batch_launch(const uint8_t* pool, const yxh_lb_image* images, int 
 // align_corners=False) of the [B, C, H, W] training batch.  The arithmetic is ATen's bilinear
 // kernel term for term, in fp32 whatever the storage type (accscalar_t): scale = in / out,
 // src = max(scale * (dst + 0.5) - 0.5, 0), i0 = (int)src, i1 = i0 + (i0 < in - 1), l1 = src - i0,
-// l0 = 1 - l1, out = l0y * (l0x * a + l1x * b) + l1y * (l0x * c + l1x * d), rounded once to the
-// storage type -- so the device result is bit-identical to the reference's own call on this GPU
-// (tests/test_gpu_augment.py compares with torch's F.interpolate on the device).  Same size: a copy.
+// l0 = 1 - l1, out = l0y * (l0x * a + l1x * b) + l1y * (l0x * c + l1x * d) with ATen's fma
+// grouping (measured: tools/resize_probe.hip), rounded once to the storage type -- so the device
+// result is bit-identical to the reference's own call on this GPU (tests/test_gpu_augment.py
+// compares with torch's F.interpolate on the device).  Same size: a copy.
 // One thread per output element, x fastest: each wave reads two input rows of one plane.
 template <typename T>
 __global__ __launch_bounds__(256) void resize_bilinear(const T* __restrict__ src, int planes, int ih, int iw,
@@ -206,8 +207,10 @@ __global__ __launch_bounds__(256) void resize_bilinear(const T* __restrict__ src
     const float w0l = 1.0f - w1l;
     const T* r0 = s + (long long)h1 * iw + w1;
     const T* r1 = r0 + (long long)h1p * iw;
-    const float v = h0l * (w0l * to_f32(r0[0]) + w1l * to_f32(r0[w1p])) +
-                    h1l * (w0l * to_f32(r1[0]) + w1l * to_f32(r1[w1p]));
+    // the contraction ATen's kernel gets from the compiler, spelled out (tools/resize_probe.hip: of
+    // the fma groupings of this sum only this one matches F.interpolate on gfx950 bit for bit)
+    const float v = __builtin_fmaf(h0l, __builtin_fmaf(w0l, to_f32(r0[0]), w1l * to_f32(r0[w1p])),
+                                   h1l * __builtin_fmaf(w0l, to_f32(r1[0]), w1l * to_f32(r1[w1p])));
     dst[idx] = from_f32<T>(v);
 }
 
