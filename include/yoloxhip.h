@@ -598,8 +598,8 @@ int yxh_graph_create(const yxh_op* ops, int32_t n, void* stream, void** graph_ex
  * edges, same-lane order is stream order.  Lane 0 forks the others at the start and
  * joins them at the end.  Used to overlap the three head levels with each other and
  * with the PAFPN bottom-up path (yolo_head.py:140-211 runs the levels independently).
- * At most 16 lanes (EINVAL above; round 2's cap of 4 came from a 7-stream crash that round 4
- * could not reproduce with 4-12 lanes). */
+ * At most 8 lanes (EINVAL above: the most a GPU test replays; round 2's 7-stream crash is
+ * unexplained, runtime.cpp -- past 8 use yxh_graph_create_dag). */
 int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, const int32_t* dep_off,
                            const int32_t* deps, int32_t nlanes, void* stream, void** graph_exec);
 /* yxh_graph_create_dag: the op list as its dataflow DAG -- op i is one graph node (the

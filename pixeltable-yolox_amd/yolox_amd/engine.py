@@ -547,6 +547,35 @@ def dependencies_rw(rw: list) -> list:
     return deps
 
 
+def hoist_lanes(ops) -> list:
+    """The op list reordered so that every graph-lane op (a head level, ``OpRec.lane`` > 0)
+    directly follows the last op it depends on, instead of the whole neck: the op order is the
+    capture order of the lanes graph, and the runtime dispatches a branch's nodes in that order,
+    so a level planned after the neck (yolo_head.py:140-211 runs after yolo_pafpn.py:71-112)
+    otherwise queues behind the other levels' work although its input (the 80x80 PAN output)
+    is ready long before them.  Lane-0 order and each lane's own order are kept; the result is a
+    topological order of the same dataflow DAG (``op_dependencies``)."""
+    deps = op_dependencies(ops)
+    placed = [False] * len(ops)
+    order = []
+    pending = [i for i, r in enumerate(ops) if r.lane != 0]
+    for i, r in enumerate(ops):
+        if r.lane != 0:
+            continue
+        order.append(i)
+        placed[i] = True
+        grew = True
+        while grew:
+            grew = False
+            for j in pending:
+                if not placed[j] and all(placed[k] for k in deps[j]):
+                    order.append(j)
+                    placed[j] = True
+                    grew = True
+    order += [j for j in pending if not placed[j]]
+    return [ops[i] for i in order]
+
+
 def op_dependencies(ops) -> list:
     """Per op, the earlier ops it must wait for, from the buffers it reads and writes
     (read-after-write, write-after-write, write-after-read).  Arena buffers never alias
@@ -634,6 +663,8 @@ class Plan:
         self.anchors = anchors
         # independent head levels run as separate graph branches (YOLOX_AMD_LANES=0: one stream)
         self.nlanes = 1 + max((r.lane for r in ctx.ops), default=0)
+        if self.nlanes > 1 and os.environ.get("YOLOX_AMD_LANE_HOIST", "1") != "0":
+            ctx.ops[:] = hoist_lanes(ctx.ops)
         self._deps = op_dependencies(ctx.ops)
         self.use_lanes = os.environ.get("YOLOX_AMD_LANES", "1") != "0"
         # captured graph form: "lanes" (multi-stream capture: head levels on lanes, or one lane

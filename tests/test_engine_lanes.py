@@ -40,6 +40,32 @@ def test_head_levels_plan_on_their_own_lanes():
         assert [lanes[j] for j in deps[first]] == [0]
 
 
+def test_hoisted_lanes_follow_their_inputs():
+    """engine.hoist_lanes: every head-lane op moves up to just after the last op it depends on
+    (level 0 starts right after the 80x80 PAN output, not after the whole neck), lane 0 and each
+    lane keep their order, and the result is a topological order of the same dataflow DAG."""
+    from yolox_amd.engine import hoist_lanes
+    m = named_config("yolox_s").get_model()
+    ctx = PlanCtx(2, torch.bfloat16, torch.device("cpu"))
+    feats = m.backbone.plan(ctx, ctx.image(128, 128))
+    m.head.plan(ctx, feats, OutBuffer(sum(f.lh * f.lw for f in feats), 85))
+    ops = hoist_lanes(ctx.ops)
+    assert sorted(map(id, ops)) == sorted(map(id, ctx.ops))
+    for k in range(4):
+        assert [o for o in ops if o.lane == k] == [o for o in ctx.ops if o.lane == k]
+    deps = op_dependencies(ops)
+    assert all(j < i for i, d in enumerate(deps) for j in d)
+    lanes = [o.lane for o in ops]
+    for i, o in enumerate(ops):
+        if o.lane and (i == 0 or lanes[i - 1] != o.lane):  # a lane segment starts right after its input
+            assert deps[i] and max(deps[i]) == i - 1 or lanes[i - 1] != 0
+    first = {k: lanes.index(k) for k in (1, 2, 3)}
+    assert first[1] < first[2] < first[3]
+    # level 0 starts before the neck's bottom-up path (its stride-2 convs) has run
+    assert any(l == 0 for l in lanes[first[1]:])
+    assert sum(1 for l in lanes[first[1]:] if l == 0) > 4
+
+
 def test_dag_dependencies_per_chunk_arena():
     """The DAG of a chunked plan: with a shared arena chunk 1's writers wait for chunk 0's
     readers of the same buffers; with arenas of their own the chunks are not ordered."""
