@@ -316,6 +316,6 @@ int conv_pw1f_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumPw1fTiles = 4;
 // fp32 data gradient of a 3x3 s2 conv by output parity class (conv_pw1f.hip): tile ids 215..216
 int dgrad_s2f_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
-constexpr int kNumDgradS2Tiles = 2;
+constexpr int kNumDgradS2Tiles = 6;  // 215-216 fp32 (dgrad_s2f), 217-220 16-bit (dgrad_s2h)
 
 }  // namespace yxh

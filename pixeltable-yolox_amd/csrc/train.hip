@@ -20,6 +20,8 @@
 //                    torch) + the identity branch of SPPBottleneck's concat.
 //  upsample_bwd    : nn.Upsample(nearest x2) backward (2x2 sums), accumulated.
 //  channel_sum     : bias gradients of the head's pred convs.
+#include <cstdlib>
+
 #include "conv_common.hpp"
 
 namespace yxh {
@@ -155,8 +157,10 @@ __global__ __launch_bounds__(256) void chan_reduce(RedArgs a) {
         }
     };
     // U rows in flight per thread: all loads first, then the rows in order (the same
-    // fixed summation order as one row at a time)
-    constexpr int U = 4;
+    // fixed summation order as one row at a time).  BWD holds y, the fp32 gradient and four
+    // coefficient rows per channel: at U = 4 it took 159 VGPRs (3 waves per SIMD, so the
+    // 1024-block grid ran in two rounds: the slowest kernel of the configs[4] step's main stream)
+    constexpr int U = MODE == RED_BWD ? 2 : 4;
     if (rl < rpi) {
         int r = r0 + rl;
         for (; r + (U - 1) * rpi < r1; r += U * rpi) {
@@ -1463,85 +1467,105 @@ __global__ __launch_bounds__(256) void pack_batch(const yxh_pack_job* jobs, int 
 }
 
 // ------------------------------------------------------------------ SPP / upsample backward
-// Block = (kSppCpb channels, image): the plane lives in LDS.  Per pool radius r (2, 4, 6):
-// horizontal pass -> first max column of each row window; vertical pass -> first max
-// row among those = torch's argmax (first maximum in row-major scan, -inf padding);
-// then every input pixel GATHERS the gradients of the outputs whose argmax it is (fixed
-// order, no atomics: deterministic).  dx = dcat[:, :c] + gathered.
-constexpr int kSppCpb = 4;
-
-template <typename T>
-__global__ __launch_bounds__(256) void spp_bwd(TView cat, int H, int W, int c, const float* dcat, float* dx,
-                                               int B) {
+// Block = (CPB channels, image), 1024 threads: the plane lives in LDS.  Per pool radius r (2, 4, 6):
+// horizontal pass -> first max column hcol of each row window; vertical pass -> first max row brow
+// among those = torch's argmax (first maximum in row-major scan, -inf padding): output (oy, ox)
+// routes its gradient to pixel (brow, hcol[brow][ox]).  Every input pixel then GATHERS those
+// gradients separably (fixed order, no atomics: deterministic): G1[y][ox] = the outputs of column
+// ox whose argmax row is y (2r + 1 candidates), then pixel (y, x) sums the G1[y][ox] whose row-window
+// max sits in column x (2r + 1 more) -- 2 (2r + 1) LDS reads per pixel instead of (2r + 1)^2.
+// dx = dcat[:, :c] + the three gathers.  (The round-4 form gathered over the whole square window
+// with one wave per SIMD: 3.4 ms of the configs[4] step's main stream for yolox_x's 40x40x640 SPP.)
+template <typename T, int CPB>
+__global__ __launch_bounds__(1024) void spp_bwd(TView cat, int H, int W, int c, const float* dcat, float* dx,
+                                                int B) {
     extern __shared__ __attribute__((aligned(16))) char sm[];
-    const int HW = H * W, n = HW * kSppCpb;
-    unsigned short* am = (unsigned short*)sm;                 // [3][n] argmax pixel per output
-    float* pl = (float*)(sm + 6 * (size_t)n);                 // plane
-    float* hv = pl + n;                                       // row-window max
-    unsigned short* hc = (unsigned short*)(hv + n);           // its column
-    float* dg = pl;  // [3][n] pooled-output gradients, once the argmax passes are done
-    const int c0 = blockIdx.x * kSppCpb, b = blockIdx.y;
+    const int HW = H * W, n = HW * CPB;
+    unsigned short* brow = (unsigned short*)sm;  // [3][n] argmax row of output q
+    unsigned short* hcol = brow + 3 * n;         // [3][n] first max column of row y's window around x
+    float* pl = (float*)(hcol + 3 * n);          // plane, then the staged output gradients of pool k
+    float* hv = pl + n;                          // row-window max, then G1
+    float* acc = hv + n;                         // the input gradient being gathered
+    const int c0 = blockIdx.x * CPB, b = blockIdx.y, nt = blockDim.x;
     const T* xb = (const T*)cat.ptr + (long long)b * cat.bs;
     const float* db = dcat + (long long)b * HW * 4 * c;
-    for (int q = threadIdx.x; q < n; q += 256) {
-        const int pix = q / kSppCpb, j = q - pix * kSppCpb;
-        pl[q] = c0 + j < c ? to_f32(xb[(long long)pix * cat.cs + c0 + j]) : 0.0f;
+    for (int q = threadIdx.x; q < n; q += nt) {
+        const int pix = q / CPB, j = q - pix * CPB;
+        const bool in = c0 + j < c;
+        pl[q] = in ? to_f32(xb[(long long)pix * cat.cs + c0 + j]) : 0.0f;
+        acc[q] = in ? db[(long long)pix * 4 * c + c0 + j] : 0.0f;
     }
     __syncthreads();
     for (int k = 0; k < 3; ++k) {
         const int r = 2 + 2 * k;
-        for (int q = threadIdx.x; q < n; q += 256) {
-            const int pix = q / kSppCpb, j = q - pix * kSppCpb;
+        for (int q = threadIdx.x; q < n; q += nt) {
+            const int pix = q / CPB, j = q - pix * CPB;
             const int y = pix / W, x = pix - y * W;
             float best = 0.0f;
             int bc = -1;
             for (int xx = max(0, x - r); xx <= min(W - 1, x + r); ++xx) {
-                const float v = pl[(y * W + xx) * kSppCpb + j];
+                const float v = pl[(y * W + xx) * CPB + j];
                 if (bc < 0 || v > best) {
                     best = v;
                     bc = xx;
                 }
             }
             hv[q] = best;
-            hc[q] = (unsigned short)bc;
+            hcol[k * n + q] = (unsigned short)bc;
         }
         __syncthreads();
-        for (int q = threadIdx.x; q < n; q += 256) {
-            const int pix = q / kSppCpb, j = q - pix * kSppCpb;
+        for (int q = threadIdx.x; q < n; q += nt) {
+            const int pix = q / CPB, j = q - pix * CPB;
             const int y = pix / W, x = pix - y * W;
             float best = 0.0f;
             int br = -1;
             for (int yy = max(0, y - r); yy <= min(H - 1, y + r); ++yy) {
-                const float v = hv[(yy * W + x) * kSppCpb + j];
+                const float v = hv[(yy * W + x) * CPB + j];
                 if (br < 0 || v > best) {
                     best = v;
                     br = yy;
                 }
             }
-            am[k * n + q] = (unsigned short)(br * W + hc[(br * W + x) * kSppCpb + j]);
+            brow[k * n + q] = (unsigned short)br;
         }
         __syncthreads();
     }
-    for (int q = threadIdx.x; q < 3 * n; q += 256) {  // the plane is dead: stage the gradients
-        const int k = q / n, r = q - k * n;
-        const int pix = r / kSppCpb, j = r - pix * kSppCpb;
-        dg[q] = c0 + j < c ? db[(long long)pix * 4 * c + (k + 1) * c + c0 + j] : 0.0f;
-    }
-    __syncthreads();
-    for (int q = threadIdx.x; q < n; q += 256) {
-        const int pix = q / kSppCpb, j = q - pix * kSppCpb;
-        if (c0 + j >= c) continue;
-        const int y = pix / W, x = pix - y * W;
-        float g = db[(long long)pix * 4 * c + c0 + j];
-        for (int k = 0; k < 3; ++k) {
-            const int r = 2 + 2 * k;
-            for (int oy = max(0, y - r); oy <= min(H - 1, y + r); ++oy)
-                for (int ox = max(0, x - r); ox <= min(W - 1, x + r); ++ox) {
-                    const int o = k * n + (oy * W + ox) * kSppCpb + j;
-                    if (am[o] == pix) g += dg[o];
-                }
+    // the plane is dead: per pool, stage its output gradients, gather by columns, then by rows
+    for (int k = 0; k < 3; ++k) {
+        const int r = 2 + 2 * k;
+        const unsigned short* bk = brow + k * n;
+        const unsigned short* hk = hcol + k * n;
+        for (int q = threadIdx.x; q < n; q += nt) {
+            const int pix = q / CPB, j = q - pix * CPB;
+            pl[q] = c0 + j < c ? db[(long long)pix * 4 * c + (k + 1) * c + c0 + j] : 0.0f;
         }
-        dx[((long long)b * HW + pix) * c + c0 + j] = g;
+        __syncthreads();
+        for (int q = threadIdx.x; q < n; q += nt) {  // G1[y][ox]
+            const int pix = q / CPB, j = q - pix * CPB;
+            const int y = pix / W, ox = pix - y * W;
+            float g = 0.0f;
+            for (int oy = max(0, y - r); oy <= min(H - 1, y + r); ++oy) {
+                const int o = (oy * W + ox) * CPB + j;
+                if (bk[o] == y) g += pl[o];
+            }
+            hv[q] = g;
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q < n; q += nt) {
+            const int pix = q / CPB, j = q - pix * CPB;
+            const int y = pix / W, x = pix - y * W;
+            float g = 0.0f;
+            for (int ox = max(0, x - r); ox <= min(W - 1, x + r); ++ox) {
+                const int o = (y * W + ox) * CPB + j;
+                if (hk[o] == x) g += hv[o];
+            }
+            acc[q] += g;
+        }
+        __syncthreads();
+    }
+    for (int q = threadIdx.x; q < n; q += nt) {
+        const int pix = q / CPB, j = q - pix * CPB;
+        if (c0 + j < c) dx[((long long)b * HW + pix) * c + c0 + j] = acc[q];
     }
 }
 
@@ -1593,11 +1617,24 @@ int check_view(const yxh_src* s, int dt, const char* what) {
 
 constexpr int kRedMaxBlocks = 1024;
 
+// Reduction blocks: ~8 rows per thread, at most YXH_RED_BLOCKS (default 512: two 4-wave blocks
+// per CU, one round; chan_finalize then reads 512 partials per channel instead of 1024 -- it is
+// latency-bound on the strided partial rows and runs once per BatchNorm per pass)
+int red_cap() {
+    static const int cap = [] {
+        const char* e = getenv("YXH_RED_BLOCKS");
+        const int v = e ? atoi(e) : 512;
+        return v < 1 ? 1 : v > kRedMaxBlocks ? kRedMaxBlocks : v;
+    }();
+    return cap;
+}
+
 int red_blocks(int M, int C, int dt, int* rpb) {
     const int nch = C / (16 / esz(dt));
     const int rpi = nch >= 256 ? 1 : 256 / nch;
     int nblk = (int)(((long long)M + rpi * 8 - 1) / (rpi * 8));  // ~8 rows per thread (4 in flight)
-    nblk = nblk < 1 ? 1 : (nblk > kRedMaxBlocks ? kRedMaxBlocks : nblk);
+    const int cap = red_cap();
+    nblk = nblk < 1 ? 1 : (nblk > cap ? cap : nblk);
     *rpb = (M + nblk - 1) / nblk;
     return (M + *rpb - 1) / *rpb;
 }
@@ -2043,19 +2080,29 @@ int pack_batch_launch(const yxh_pack_job* jobs, int njobs, int total_blocks, int
 int spp_bwd_launch(int dt, int B, const yxh_src* cat, int c, const float* dcat, float* dx, hipStream_t st) {
     YXH_CHECK_ARG(cat && cat->ptr && dcat && dx && B > 0 && c > 0 && cat->cstride >= 4 * c, "spp_bwd arguments");
     const int HW = cat->h * cat->w;
-    const size_t lds = (size_t)HW * kSppCpb * (6 + 12);  // argmax u16 [3], then plane/row max/column or f32 [3]
+    // LDS per channel and pixel: brow + hcol u16 [3] each, plane / row max / gradient f32
+    constexpr size_t kPer = 6 + 6 + 12;
+    const int cpb = (size_t)HW * 4 * kPer <= 160 * 1024 ? 4 : (size_t)HW * 2 * kPer <= 160 * 1024 ? 2 : 1;
+    const size_t lds = (size_t)HW * cpb * kPer;
     YXH_CHECK_ARG(lds <= 160 * 1024 && HW < 65536, "spp_bwd plane %dx%d too large for LDS", cat->h, cat->w);
-    dim3 grid((c + kSppCpb - 1) / kSppCpb, B);
+    dim3 grid((c + cpb - 1) / cpb, B);
     TView v = tview(cat, c);
-#define YXH_SPPB(T)                                                                                        \
+#define YXH_SPPB(T, P)                                                                                     \
     do {                                                                                                   \
-        (void)hipFuncSetAttribute((const void*)spp_bwd<T>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+        (void)hipFuncSetAttribute((const void*)spp_bwd<T, P>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                   (int)lds);                                                               \
-        hipLaunchKernelGGL(spp_bwd<T>, grid, dim3(256), lds, st, v, cat->h, cat->w, c, dcat, dx, B);       \
+        hipLaunchKernelGGL((spp_bwd<T, P>), grid, dim3(1024), lds, st, v, cat->h, cat->w, c, dcat, dx, B); \
     } while (0)
-    if (dt == YXH_BF16) YXH_SPPB(bf16);
-    else if (dt == YXH_F16) YXH_SPPB(f16);
-    else YXH_SPPB(float);
+#define YXH_SPPB_T(T)                 \
+    do {                              \
+        if (cpb == 4) YXH_SPPB(T, 4); \
+        else if (cpb == 2) YXH_SPPB(T, 2); \
+        else YXH_SPPB(T, 1);          \
+    } while (0)
+    if (dt == YXH_BF16) YXH_SPPB_T(bf16);
+    else if (dt == YXH_F16) YXH_SPPB_T(f16);
+    else YXH_SPPB_T(float);
+#undef YXH_SPPB_T
 #undef YXH_SPPB
     YXH_CHECK_LAUNCH("spp_bwd");
     return YXH_OK;

@@ -663,7 +663,11 @@ class Plan:
         self.anchors = anchors
         # independent head levels run as separate graph branches (YOLOX_AMD_LANES=0: one stream)
         self.nlanes = 1 + max((r.lane for r in ctx.ops), default=0)
-        if self.nlanes > 1 and os.environ.get("YOLOX_AMD_LANE_HOIST", "1") != "0":
+        # YOLOX_AMD_LANE_HOIST=1 moves each head level up to its input (engine.hoist_lanes): level 0
+        # then overlaps the PAFPN bottom-up path, but on MI355X the forward got slower (1.635-1.641 vs
+        # 1.629-1.631 ms, profiles/r05/lane_hoist_ab.txt): the level-0 head convs take every CU and
+        # the neck's small layers stretch 3-5x beside them -- the chip is already full, so it stays off
+        if self.nlanes > 1 and os.environ.get("YOLOX_AMD_LANE_HOIST", "0") == "1":
             ctx.ops[:] = hoist_lanes(ctx.ops)
         self._deps = op_dependencies(ctx.ops)
         self.use_lanes = os.environ.get("YOLOX_AMD_LANES", "1") != "0"

@@ -138,10 +138,11 @@ _BASE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + lis
 # 16-bit (autocast) steps also try the inference path's 16-bit kernels for the forward convs: dense
 # 1x1 conv_pwf (97-104), weight-stationary 3x3 conv_ws (161-190, 261-280: yolox_x / yolox_l widths) and
 # 1x1 conv_ws1 (201-210); of those only conv_ws's fp32-gradient tiles (281-288) take the data
-# gradient's fp32-accumulating form (stride-1 3x3s), the rest stays on the tiles above
+# gradient's fp32-accumulating form (stride-1 3x3s); stride-2 3x3 data gradients also try the
+# parity-class tiles (217-220, dgrad_s2h: 1/2/2/4 taps instead of 9 over a zero-dilated dy)
 CONV_TUNE_TILES = _BASE_TILES + ([] if os.environ.get("YOLOX_AMD_TRAIN_TILES16") == "base" else
                                  [2 * i for i in list(range(97, 105)) + list(range(161, 191)) + list(range(201, 211))
-                                  + list(range(261, 289))])
+                                  + list(range(261, 289)) + list(range(217, 221))])
 CONV_TUNE_TILES_F32 = _BASE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)] + [2 * i for i in range(211, 217)]
 WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 25)) + list(range(25, 29))
 _TRAIN_TILES: dict = {}
@@ -783,7 +784,11 @@ class CapturedTrainStep:
         self.plan: list = []  # ("main" | "side", CUDAGraph)
         self._empty: list = []  # captured main segments with no launch (kept alive, not replayed)
         self._keep: list = []  # conv-output gradients read by side segments: alive for the whole step
-        self.main = torch.cuda.Stream(self.dev)
+        # YOLOX_AMD_MAIN_PRIORITY=1: the main segments replay on a high-priority stream, so the
+        # data-gradient chain (the step's critical path) is dispatched ahead of the side stream's
+        # weight gradients when both have workgroups waiting for CUs
+        prio = -1 if os.environ.get("YOLOX_AMD_MAIN_PRIORITY", "0") == "1" else 0
+        self.main = torch.cuda.Stream(self.dev, priority=prio)
         self.side_stream = g._wside
         self._dbg = os.environ.get("YOLOX_AMD_CAP_DEBUG", "")
         if "torch" in self._dbg:  # diagnostic: one torch.cuda.graph capture (side stream forked inside it)

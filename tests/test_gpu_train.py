@@ -252,6 +252,61 @@ def test_dgrad_conv_ws_fp32_tiles(dtype, cfwd, H, W, B):
     assert ran >= 2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("cin,cout,H,W,B", [(80, 160, 19, 23, 2), (160, 320, 20, 18, 2), (64, 128, 24, 20, 2),
+                                            (32, 64, 17, 15, 3), (128, 256, 9, 10, 2), (320, 640, 7, 8, 2)])
+def test_dgrad_s2_parity_class_tiles(dtype, cin, cout, H, W, B):
+    """The data gradient of a stride-2 3x3 conv (darknet.py:148-156 stage convs, yolo_pafpn.py
+    bu_conv1/2) on the 16-bit parity-class tiles (217-220, dgrad_s2h: output pixel (2i+py, 2j+px)
+    meets 1, 2, 2 or 4 taps of the un-dilated dy) written into / added onto an fp32 gradient, vs torch
+    fp32 autograd and vs the zero-dilated form on the register-staged conv_igemm tile; odd and even
+    input sizes (the forward's last row / column of taps may fall outside)."""
+    from yolox_amd import _native as N
+    from yolox_amd.train import dense_src
+    g = torch.Generator().manual_seed(cin + H + W)
+    oh, ow = (H + 1) // 2, (W + 1) // 2
+    dy = torch.randn(B, oh, ow, cout, generator=g).to(dtype)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * 0.05
+    wtd, dyd = wt.cuda(), dy.cuda()
+    pk = torch.empty(cin * 9 * cout, dtype=dtype, device="cuda")
+    chk(lib().yxh_pack_dgrad_weight(wtd.data_ptr(), cout, cin, 3, 3, 0, cin, cout, DT[dtype], pk.data_ptr(), stream()))
+    zb = torch.zeros(cin, device="cuda")
+    xr = torch.zeros(B, cin, H, W, requires_grad=True)
+    y = F.conv2d(xr, wt.to(dtype).float(), stride=2, padding=1)
+    assert tuple(y.shape[2:]) == (oh, ow)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    want = xr.grad.permute(0, 2, 3, 1)
+
+    def dgrad(tile, acc):
+        dx = torch.full((B, H, W, cin), 0.5 if acc else float("nan"), device="cuda")
+        d = N.ConvDesc()
+        d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w = DT[dtype], B, H, W, H, W
+        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.groups, d.nsrc = cout, cin, 3, 3, 1, 1, 1, 1
+        d.src[0] = dense_src(dyd, up=2)
+        d.weight, d.bias, d.dst, d.dst_dtype = pk.data_ptr(), zb.data_ptr(), dx.data_ptr(), 0
+        d.dst_cstride, d.dst_bstride, d.act = cin, H * W * cin, 0
+        d.flags, d.tile = (N.CONV_ACCUMULATE if acc else 0), tile
+        rc = lib().yxh_conv2d(C.byref(d), stream())
+        if rc == N.EUNSUPPORTED:
+            return None
+        chk(rc)
+        torch.cuda.synchronize()
+        return dx - 0.5 if acc else dx
+
+    base = dgrad(2 * 1, True)  # conv_igemm over the zero-dilated dy
+    assert rel(base, want) < 1e-4
+    ran = 0
+    for tid in range(217, 221):
+        for acc in (False, True):
+            got = dgrad(2 * tid, acc)
+            assert got is not None, tid
+            assert rel(got, want) < 1e-4, (tid, acc)  # same rounded operands: summation order only
+            assert rel(got, base) < 1e-4, (tid, acc)
+            ran += 1
+    assert ran == 8
+    assert dgrad(2 * 215, False) is None  # the fp32 tiles refuse 16-bit operands
+
+
 WG_TILE_CASES = [  # cin0, cin1, up1, cout, k, s, H, B
     (32, 0, 0, 64, 3, 1, 16, 2), (64, 0, 0, 32, 3, 2, 20, 3), (64, 64, 1, 128, 1, 1, 8, 2),
     (128, 0, 0, 128, 3, 1, 9, 2), (16, 0, 0, 24, 3, 1, 12, 1), (256, 0, 0, 192, 1, 1, 23, 2),
@@ -464,20 +519,24 @@ def test_wgrad_cin_store_and_strided_dy():
     assert rel(dw.view(5, 12), ref) < 1e-5
 
 
-def test_spp_and_upsample_bwd():
-    g = torch.Generator().manual_seed(11)
-    B, H, W, c = 2, 9, 10, 16
-    x = torch.randn(B, H, W, c, generator=g)
+@pytest.mark.parametrize("B,H,W,c,dtype", [(2, 9, 10, 16, torch.float32), (2, 40, 40, 18, torch.float32),
+                                            (1, 64, 64, 8, torch.float32), (2, 20, 20, 24, torch.float16)])
+def test_spp_and_upsample_bwd(B, H, W, c, dtype):
+    """SPP max-pool backward (separable gather: 4 / 2 / 1 channels per block by plane size; yolox_x
+    @1280 = 40x40) and the nearest-x2 upsample backward vs torch autograd, ties included."""
+    g = torch.Generator().manual_seed(11 + H)
+    x = torch.randn(B, H, W, c, generator=g).to(dtype).float()
     x[0, 1, 1, :] = x[0, 1, 2, :]  # ties: first max in scan order takes the gradient
+    x[-1, H - 2, :, :] = x[-1, H - 1, :, :]
     cat = torch.zeros(B, H, W, 4 * c)
     cat[..., :c] = x
     dcat = torch.randn(B, H, W, 4 * c, generator=g)
-    catd = cat.cuda()
-    chk(lib().yxh_spp_maxpool(catd.data_ptr(), 0, B, H, W, c, 4 * c, H * W * 4 * c, stream()))
+    catd = cat.to(dtype).cuda()
+    chk(lib().yxh_spp_maxpool(catd.data_ptr(), DT[dtype], B, H, W, c, 4 * c, H * W * 4 * c, stream()))
     dx = torch.empty(B, H, W, c, device="cuda")
     cs = src(catd)
     dcd = dcat.cuda()
-    chk(lib().yxh_spp_bwd(0, B, C.byref(cs), c, dcd.data_ptr(), dx.data_ptr(), stream()))
+    chk(lib().yxh_spp_bwd(DT[dtype], B, C.byref(cs), c, dcd.data_ptr(), dx.data_ptr(), stream()))
     up_g = torch.randn(B, 2 * H, 2 * W, c, generator=g)
     acc = torch.ones(B, H, W, c)
     accd, ugd = acc.cuda(), up_g.cuda()
@@ -486,7 +545,7 @@ def test_spp_and_upsample_bwd():
     xr = x.permute(0, 3, 1, 2).clone().requires_grad_()
     outs = torch.cat([xr] + [F.max_pool2d(xr, k, 1, k // 2) for k in (5, 9, 13)], 1)
     outs.backward(dcat.permute(0, 3, 1, 2))
-    assert rel(catd[..., c:], outs.detach().permute(0, 2, 3, 1)[..., c:]) == 0.0
+    assert rel(catd[..., c:].float(), outs.detach().permute(0, 2, 3, 1)[..., c:]) == 0.0
     assert rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-6
     ref = 1 + up_g.view(B, H, 2, W, 2, c).sum((2, 4))
     assert rel(accd, ref) < 1e-6
