@@ -519,8 +519,8 @@ def test_wgrad_cin_store_and_strided_dy():
     assert rel(dw.view(5, 12), ref) < 1e-5
 
 
-@pytest.mark.parametrize("B,H,W,c,dtype", [(2, 9, 10, 16, torch.float32), (2, 40, 40, 18, torch.float32),
-                                            (1, 64, 64, 8, torch.float32), (2, 20, 20, 24, torch.float16)])
+@pytest.mark.parametrize("B,H,W,c,dtype", [(2, 9, 10, 16, torch.float32), (2, 40, 40, 20, torch.float32),
+                                            (1, 48, 48, 8, torch.float32), (2, 20, 20, 24, torch.float16)])
 def test_spp_and_upsample_bwd(B, H, W, c, dtype):
     """SPP max-pool backward (separable gather: 4 / 2 / 1 channels per block by plane size; yolox_x
     @1280 = 40x40) and the nearest-x2 upsample backward vs torch autograd, ties included."""

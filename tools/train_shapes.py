@@ -6,7 +6,8 @@ import json
 import sys
 from collections import defaultdict
 
-FAMILIES = ("conv_igemm", "conv_glds", "conv_rows", "conv_r3", "conv_pw", "conv_ws", "conv_wgrad", "wgrad_f32<", "wgrad9t_f32", "dgrad_s2f")
+FAMILIES = ("conv_igemm", "conv_glds", "conv_rows", "conv_r3", "conv_pw", "conv_ws", "conv_wgrad", "wgrad_f32<", "wgrad9t_f32",
+            "wgrad9t_h", "wgrad1t_h", "dgrad_s2f", "dgrad_s2h")
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 log = json.load(open(sys.argv[2]))
 per_step = len(log["launches"]) // log["steps"]
