@@ -1251,7 +1251,7 @@ __global__ __launch_bounds__(256) void wgrad9t_f32(WgradParams p, int nseg) {
         }
 }
 
-// bf16/f16 3x3 weight gradient with all nine taps per block (tiles 25-28): wgrad9t_f32's
+// bf16/f16 3x3 weight gradient with all nine taps per block (tiles 25-30): wgrad9t_f32's
 // staging -- a stage is a row segment of KP output pixels; dY[KP][TN] and the three input rows
 // X[3][(KP - 1) s + 3][TC] it reads are copied once into LDS in their natural pixel-major layout
 // (rows padded by 16 bytes) -- with the 16-bit MFMA operands (8 consecutive pixels of one channel
@@ -1965,9 +1965,13 @@ int wgrad_tile(int tile, const WgradParams& p, hipStream_t st) {
                     default: return s2 ? launch_wgrad9t_f32<64, 32, 2, 16>(p, st) : launch_wgrad9t_f32<64, 32, 1, 16>(p, st);
                 }
             }
-        case 25: case 26: case 27: case 28: {
+        case 25: case 26: case 27: case 28: case 29: case 30: {
             const bool s2 = p.stride == 2;
             switch (tile) {
+                // 160 x 32 / 32 x 160 (round 5): yolox_x's 160-channel 3x3s in whole tiles (64 x 64 covers
+                // 160 x 160 with 3 x 3 tiles = 1.44x the MFMA work), five 16-row fragments per wave
+                case 29: return s2 ? launch_wgrad9t_h<T, 160, 32, 2, 32>(p, st) : launch_wgrad9t_h<T, 160, 32, 1, 32>(p, st);
+                case 30: return s2 ? launch_wgrad9t_h<T, 32, 160, 2, 32>(p, st) : launch_wgrad9t_h<T, 32, 160, 1, 32>(p, st);
                 case 25: return s2 ? launch_wgrad9t_h<T, 64, 64, 2, 32>(p, st) : launch_wgrad9t_h<T, 64, 64, 1, 32>(p, st);
                 case 26: return s2 ? launch_wgrad9t_h<T, 128, 64, 2, 32>(p, st) : launch_wgrad9t_h<T, 128, 64, 1, 32>(p, st);
                 case 27:  // stride 2 would stage 13 chunks per lane beside 288 accumulators: spills

@@ -144,7 +144,7 @@ CONV_TUNE_TILES = _BASE_TILES + ([] if os.environ.get("YOLOX_AMD_TRAIN_TILES16")
                                  [2 * i for i in list(range(97, 105)) + list(range(161, 191)) + list(range(201, 211))
                                   + list(range(261, 289)) + list(range(217, 221))])
 CONV_TUNE_TILES_F32 = _BASE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)] + [2 * i for i in range(211, 217)]
-WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 25)) + list(range(25, 29))
+WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 25)) + list(range(25, 31))
 _TRAIN_TILES: dict = {}
 # diagnostic (tools/train_shapes.py): every conv / wgrad launch of the training step, in order
 _LAUNCH_LOG: Optional[list] = [] if os.environ.get("YOLOX_AMD_TRAIN_LOG") else None

@@ -452,17 +452,18 @@ def test_conv_wgrad9t_fp32_tiles(ws, tile, cin0, cin1, up1, cout, k, s, H, W, B,
 
 
 @pytest.mark.parametrize("ws", [0, 16 << 20])
-@pytest.mark.parametrize("tile", [25, 26, 27, 28])
+@pytest.mark.parametrize("tile", [25, 26, 27, 28, 29, 30])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("cin0,cin1,up1,cout,k,s,H,W,B,dyc", [c for c in WGF_CASES if c[4] == 3]
                          + [(64, 64, 1, 64, 3, 1, 12, 10, 2, 64), (128, 0, 0, 128, 3, 1, 40, 40, 2, 136),
-                            (64, 0, 0, 128, 3, 2, 80, 70, 1, 128)])
+                            (64, 0, 0, 128, 3, 2, 80, 70, 1, 128), (160, 0, 0, 160, 3, 1, 20, 18, 2, 160),
+                            (80, 80, 0, 160, 3, 2, 24, 22, 2, 160)])
 def test_conv_wgrad9t_16bit_tiles(ws, tile, dtype, cin0, cin1, up1, cout, k, s, H, W, B, dyc):
-    """bf16/f16 3x3 weight gradient with all nine taps per block (tiles 25-28: one dY row segment
+    """bf16/f16 3x3 weight gradient with all nine taps per block (tiles 25-30: one dY row segment
     and its three input rows staged once, MFMA operands read pixel-transposed by ds_read_b64_tr_b16,
     each lane naming its tap's shifted / strided pixel row) against torch autograd: stride 1 / 2,
     row segments past the image edge, cout / cin tails, two sources (the second upsampled), a wide
-    dy view; tile 27 is stride-1 only."""
+    dy view; tile 27 is stride-1 only; 29 / 30 = 160 x 32 / 32 x 160 (yolox_x's 160 channels)."""
     g = torch.Generator().manual_seed(cin0 * 11 + cout + H + tile)
     oh, ow = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
     x0 = torch.randn(B, H, W, cin0, generator=g).to(dtype)
