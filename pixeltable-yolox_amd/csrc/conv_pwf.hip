@@ -249,6 +249,30 @@ template <typename T, int FR, int FC, int WTM, int TN, int ACT>
 __device__ __forceinline__ void pwf_epilogue(const ConvParams& p, const f32x4 (&acc)[FR][FC], const float* lbias,
                                              int m0, int n0, int wr, int wc) {
     const int lane = threadIdx.x & 63, frow = lane & 15, fq = lane >> 4;
+    if constexpr (ACT == YXH_ACT_NONE) {
+        if (p.dst_f32) {  // the 16-bit training step's 1x1 data gradient: fp32 rows, YXH_CONV_ACCUMULATE
+#pragma unroll
+            for (int j = 0; j < FC; ++j) {
+                const int m = m0 + wc * WTM + j * 16 + frow;
+                if (m >= p.M) continue;
+                float* drow = (float*)p.dst + (long long)m * p.dst_cs;
+#pragma unroll
+                for (int i = 0; i < FR; ++i) {
+                    const int n = n0 + wr * 64 + i * 16 + fq * 4;
+                    if (n >= p.cout) continue;
+                    const float* lb = lbias + wr * 64 + i * 16 + fq * 4;
+                    f32x4 v = acc[i][j] + f32x4{lb[0], lb[1], lb[2], lb[3]};
+                    float4* dp = (float4*)(drow + n);
+                    if (p.accum) {
+                        const float4 o = *dp;
+                        v = v + f32x4{o.x, o.y, o.z, o.w};
+                    }
+                    *dp = make_float4(v[0], v[1], v[2], v[3]);
+                }
+            }
+            return;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < FC; ++j) {
         const int m = m0 + wc * WTM + j * 16 + frow;
@@ -324,7 +348,10 @@ static int pwf_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
 }
 
 int conv_pwf_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st) {
-    bool dense = p.taps == 1 && p.stride == 1 && p.pad == 0 && !p.dst_f32 && p.act < YXH_ACT_DECODE && p.dst_dense &&
+    // an fp32 dst (16-bit operands): the training step's 1x1 data gradient -- no activation / residual,
+    // 16-byte rows of whole 4-channel groups (vec_store is the 16-byte test for an fp32 dst)
+    const bool f32ok = !p.dst_f32 || (p.act == YXH_ACT_NONE && !p.res && p.cout % 4 == 0);
+    bool dense = p.taps == 1 && p.stride == 1 && p.pad == 0 && f32ok && p.act < YXH_ACT_DECODE && p.dst_dense &&
                  (!p.res || p.res_dense) && p.vec_store && (!p.res || p.vec_res);
     for (int s = 0; s < p.nsrc; ++s) {
         if (s == 0 && p.sup[0] == 1)  // nearest-x2 upsampled first source: any image stride
@@ -334,7 +361,7 @@ int conv_pwf_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st) {
     }
     if (!dense) {
         set_error("conv_pwf needs a 1x1 s1 conv over dense sources (the first may be x2 upsampled) into a dense "
-                  "16-bit dst");
+                  "16-bit dst (or an fp32 one without activation / residual)");
         return YXH_EUNSUPPORTED;
     }
     const long long img0 = p.sup[0] ? (p.M / p.ohw) * p.sbs[0] : (long long)p.M * p.scs[0];

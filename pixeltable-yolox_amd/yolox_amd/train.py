@@ -137,8 +137,8 @@ class GradBuffer:
 _BASE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52)) for k in (0, 1)]
 # 16-bit (autocast) steps also try the inference path's 16-bit kernels for the forward convs: dense
 # 1x1 conv_pwf (97-104), weight-stationary 3x3 conv_ws (161-190, 261-280: yolox_x / yolox_l widths) and
-# 1x1 conv_ws1 (201-210); of those only conv_ws's fp32-gradient tiles (281-288) take the data
-# gradient's fp32-accumulating form (stride-1 3x3s); stride-2 3x3 data gradients also try the
+# 1x1 conv_ws1 (201-210); of those conv_ws's fp32-gradient tiles (281-288, stride-1 3x3s) and conv_pwf
+# (1x1s, round 5) take the data gradient's fp32-accumulating form; stride-2 3x3 data gradients also try the
 # parity-class tiles (217-220, dgrad_s2h: 1/2/2/4 taps instead of 9 over a zero-dilated dy)
 CONV_TUNE_TILES = _BASE_TILES + ([] if os.environ.get("YOLOX_AMD_TRAIN_TILES16") == "base" else
                                  [2 * i for i in list(range(97, 105)) + list(range(161, 191)) + list(range(201, 211))

@@ -253,6 +253,57 @@ def test_dgrad_conv_ws_fp32_tiles(dtype, cfwd, H, W, B):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("cfwd,coutf,H,W,B", [(160, 160, 20, 18, 2), (320, 640, 9, 10, 2), (64, 128, 17, 15, 3),
+                                              (256, 128, 8, 8, 2), (160, 320, 13, 7, 2)])
+def test_dgrad_1x1_conv_pwf_fp32(dtype, cfwd, coutf, H, W, B):
+    """The data gradient of a 1x1 conv on conv_pwf's fp32-gradient epilogue (tiles 97-104, round 5):
+    dy (the forward's cout channels) with the transposed weights into / onto an fp32 gradient
+    (YXH_CONV_ACCUMULATE), vs torch fp32 autograd and the register-staged conv_igemm tile."""
+    from yolox_amd import _native as N
+    from yolox_amd.train import dense_src
+    g = torch.Generator().manual_seed(cfwd + coutf + H)
+    dy = torch.randn(B, H, W, coutf, generator=g).to(dtype)
+    wt = torch.randn(coutf, cfwd, 1, 1, generator=g) * 0.05
+    wtd, dyd = wt.cuda(), dy.cuda()
+    pk = torch.empty(cfwd * coutf, dtype=dtype, device="cuda")
+    chk(lib().yxh_pack_dgrad_weight(wtd.data_ptr(), coutf, cfwd, 1, 1, 0, cfwd, coutf, DT[dtype], pk.data_ptr(),
+                                    stream()))
+    zb = torch.zeros(cfwd, device="cuda")
+    xr = torch.zeros(B, cfwd, H, W, requires_grad=True)
+    F.conv2d(xr, wt.to(dtype).float()).backward(dy.float().permute(0, 3, 1, 2))
+    want = xr.grad.permute(0, 2, 3, 1)
+
+    def dgrad(tile, acc):
+        dx = torch.full((B, H, W, cfwd), 0.5 if acc else float("nan"), device="cuda")
+        d = N.ConvDesc()
+        d.dtype, d.batch, d.in_h, d.in_w, d.out_h, d.out_w = DT[dtype], B, H, W, H, W
+        d.cin, d.cout, d.kh, d.kw, d.stride, d.pad, d.groups, d.nsrc = coutf, cfwd, 1, 1, 1, 0, 1, 1
+        d.src[0] = dense_src(dyd)
+        d.weight, d.bias, d.dst, d.dst_dtype = pk.data_ptr(), zb.data_ptr(), dx.data_ptr(), 0
+        d.dst_cstride, d.dst_bstride, d.act = cfwd, H * W * cfwd, 0
+        d.flags, d.tile = (N.CONV_ACCUMULATE if acc else 0), tile
+        rc = lib().yxh_conv2d(C.byref(d), stream())
+        if rc == N.EUNSUPPORTED:
+            return None
+        chk(rc)
+        torch.cuda.synchronize()
+        return dx - 0.5 if acc else dx
+
+    base = dgrad(2 * 1, True)  # conv_igemm
+    assert rel(base, want) < 1e-4
+    ran = 0
+    for tid in range(97, 105):
+        for acc in (False, True):
+            got = dgrad(2 * tid, acc)
+            if got is None:
+                continue
+            assert rel(got, want) < 1e-4, (tid, acc)
+            assert rel(got, base) < 1e-4, (tid, acc)
+            ran += 1
+    assert ran >= 6  # the 32-element K-stage tiles (97, 98, 103) take every K here
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("cin,cout,H,W,B", [(80, 160, 19, 23, 2), (160, 320, 20, 18, 2), (64, 128, 24, 20, 2),
                                             (32, 64, 17, 15, 3), (128, 256, 9, 10, 2), (320, 640, 7, 8, 2)])
 def test_dgrad_s2_parity_class_tiles(dtype, cin, cout, H, W, B):
