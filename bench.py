@@ -3,11 +3,12 @@
 configs[1]: batch 32 per GPU, synthetic uniform [0,255] images, seeded weights).
 
 One step = one batch through the hot path: the captured hipGraph of the whole
-forward (Focus -> CSPDarknet -> PAFPN -> decoupled head with fused decode, 63
+forward (Focus -> CSPDarknet -> PAFPN -> decoupled head with fused decode, 53
 kernels) followed by device post-processing (filter, sort, bitmask NMS) at the
 processor defaults (conf 0.5, nms 0.65); a batch's NMS runs on a side stream beside the
-next batch's forward, which waits only for the NMS filter pass (the one reader of the
-forward's output) -- --serial-nms runs them back to back on one stream.  Inputs are resident in HBM (uint8 NHWC, as the
+next batch's forward, which writes the other of two output slots (two captured graphs), so
+it waits only for the filter pass of the batch two back (the one reader of its slot) --
+--serial-nms runs them back to back on one stream.  Inputs are resident in HBM (uint8 NHWC, as the
 processor's letterbox hands them to the forward) before the timed region.  With --gpus N (torchrun, one process per GPU) each rank
 runs an independent replica -- inference has no exchange step, so there is no
 collective in the data path -- and value = all images / max
@@ -86,6 +87,8 @@ def parse():
     ap.add_argument("--nms", type=float, default=0.65)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--one-slot", action="store_true",
+                    help="one output slot: each forward waits for the previous batch's NMS filter (round-4 pipeline)")
     ap.add_argument("--serial-nms", action="store_true",
                     help="NMS behind each forward on one stream (default: beside the next batch's forward)")
     ap.add_argument("--dry-run", action="store_true",
@@ -461,13 +464,16 @@ def main():
     t_tune = time.perf_counter() - t_tune
     if args.tune_file and rank == 0 and not os.path.exists(args.tune_file):
         engine.save_tune_cache(args.tune_file)
-    plan.capture()
+    # Serving pipeline: the NMS of batch k runs on a side stream beside the forward of batch
+    # k+1, and the forward's output rows are double-buffered too (two captured graphs of the same
+    # forward, Plan.capture(slots=2)): forward k+1 writes the other slot, so it never waits for
+    # batch k's NMS; forward k+2 waits for the filter pass of batch k -- the one reader of that
+    # slot (event recorded by yxh_postprocess_ev), long done by then.  Detections are
+    # double-buffered.  --serial-nms puts the NMS back behind each forward on one stream.
+    slots = 1 if args.serial_nms or args.one_slot else 2
+    plan.capture(slots)
     A = plan.anchors
     stream = torch.cuda.current_stream(dev)
-    # Serving pipeline: the NMS of batch k runs on a side stream beside the forward of batch
-    # k+1. Only NMS's filter pass reads the forward's output, so the next replay waits for
-    # that pass alone (event recorded by yxh_postprocess_ev); detections are double-buffered.
-    # --serial-nms puts the NMS back behind each forward on one stream.
     side = torch.cuda.Stream(dev) if not args.serial_nms else stream
     dets = [torch.empty(B, A, 7, dtype=torch.float32, device=dev) for _ in range(2)]
     cnts = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(2)]
@@ -479,11 +485,11 @@ def main():
     def step(ev0=None, ev1=None):
         nonlocal det, counts
         k = state["k"]
-        if k > 0 and not args.serial_nms:
-            stream.wait_event(filt[(k - 1) % 2])  # the previous batch's filter has read the output
+        if not args.serial_nms and k >= slots:
+            stream.wait_event(filt[(k - slots) % 2])  # the filter of the last batch in this output slot
         if ev0 is not None:
             ev0.record(stream)
-        out = plan.replay()
+        out = plan.replay(k % slots)
         if ev1 is not None:
             ev1.record(stream)
         det, counts = dets[k % 2], cnts[k % 2]
@@ -550,6 +556,7 @@ def main():
             "chunk": plan.chunk,
             "parallel_chunks": plan.parallel_chunks,
             "graph": plan.graph_mode,
+            "output_slots": slots,
         },
         "roofline": {
             "kernel": "the forward conv stack (conv_ws / conv_ws1 / conv_r3h / conv_pwf / stem_rows / head_pred: every launch of one forward; HIP events on the plan stream around each graph replay)",

@@ -20,7 +20,7 @@ namespace yxh {
 
 // conv_ws tiles for 80 / 160 / 320 / 512 input channels (yolox_x, yolox_l) and the fp32-gradient
 // forms (tiles 281-288): tile ids 261..260+kNumWsWideTiles (conv_ws_dispatch ids 61..)
-constexpr int kNumWsWideTiles = 28;
+constexpr int kNumWsWideTiles = 29;
 
 // ---------------------------------------------------------------- implicit GEMM
 // Block: 256 threads = 4 waves on a WR x WC grid; tile TN output channels x TM

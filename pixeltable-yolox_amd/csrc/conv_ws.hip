@@ -882,6 +882,9 @@ static int ws_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 86: return launch_ws<T, 64, 1, 16, 4, 64, 2, 1, 2, 2, false, 0, 0, 0, 64, true>(p, st);
         case 87: return launch_ws<T, 128, 1, 16, 4, 128, 4, 1, 1, 1, false, 0, 0, 0, 128, true>(p, st);
         case 88: return launch_ws<T, 256, 1, 8, 4, 64, 2, 4, 1, 1, false, 0, 0, 0, 256, true>(p, st);
+        // the training step's stem conv (Focus 12 channels stored as 16 -> yolox_x's 80, 3x3 s1): K = 32 with
+        // the upper 16-channel half zero (round 5; it ran on the register-staged conv_igemm at ~110 TFLOP/s)
+        case 89: return launch_ws<T, 32, 1, 16, 4, 80, 5, 1, 1, 1, false, 0, 0, 0, 16>(p, st);
         default: set_error("conv_ws tile id %d", id); return YXH_EINVAL;
     }
 }

@@ -720,6 +720,11 @@ class Plan:
         self._ops = (N.Op * (len(ctx.ops) * self.nchunks))()  # chunk c = ops [c*nops, (c+1)*nops)
         self._input_index = None
         self._graph = None
+        # a second graph of the same forward writing its rows to ``output_alt`` (capture(slots=2)):
+        # a serving loop alternates the two, so batch k+1's forward never waits for batch k's NMS
+        # to finish reading the rows
+        self._graph_alt = None
+        self.output_alt: Optional[torch.Tensor] = None
         self._graph_ptrs = None
         self._param_sig = None
         self._packed_epoch = -1
@@ -1122,6 +1127,9 @@ class Plan:
         if self._graph is not None:
             N.check(self.lib.yxh_graph_destroy(self._graph))
             self._graph = None
+        if self._graph_alt is not None:
+            N.check(self.lib.yxh_graph_destroy(self._graph_alt))
+            self._graph_alt = None
         if self._segments is not None:
             for chunk in self._segments:
                 for g, forks in chunk:
@@ -1130,15 +1138,31 @@ class Plan:
                         self.lib.yxh_graph_destroy(gk)
             self._segments = None
 
-    def capture(self) -> None:
-        """Capture the whole forward into a hipGraph reading ``static_input()``."""
+    def capture(self, slots: int = 1) -> None:
+        """Capture the whole forward into a hipGraph reading ``static_input()``; ``slots`` = 2
+        also captures it writing ``output_alt`` (replay(1))."""
+        if slots not in (1, 2):
+            raise ValueError("slots must be 1 or 2")
         self.pack_weights()
         self._bind_input(self.static_input())
         self._destroy_graphs()
-        g = C.c_void_p()
         torch.cuda.synchronize(self.device)
         if self.graph_mode == "streams" and not self.parallel_chunks and self._capture_streams():
+            if slots == 2:
+                raise NotImplementedError("two output slots need a single-graph capture form")
             return
+        self._graph = self._capture_graph()
+        if slots == 2:
+            if self.output_alt is None:
+                self.output_alt = torch.empty_like(self.output)
+            self._bind_output(self.output_alt)
+            try:
+                self._graph_alt = self._capture_graph()
+            finally:
+                self._bind_output(None)
+
+    def _capture_graph(self):
+        g = C.c_void_p()
         if self.graph_mode == "dag":
             off, deps = self._dag_arrays()
             N.check(self.lib.yxh_graph_create_dag(self._ops, len(self._ops), off, deps, N.stream_ptr(self.device),
@@ -1157,7 +1181,7 @@ class Plan:
         else:
             N.check(self.lib.yxh_graph_create(self._ops, len(self._ops), N.stream_ptr(self.device), C.byref(g)),
                     "graph capture")
-        self._graph = g
+        return g
 
     def _dag_arrays(self):
         """(dep_off, deps) of the dataflow DAG over all chunks: buffers are keyed by arena
@@ -1198,8 +1222,9 @@ class Plan:
         arr = lambda v: (C.c_int32 * max(1, len(v)))(*v)  # noqa: E731
         return arr(lanes), arr(off), arr(deps)
 
-    def replay(self) -> torch.Tensor:
-        """Launch the captured forward.  Parameters changed since the last packing are
+    def replay(self, slot: int = 0) -> torch.Tensor:
+        """Launch the captured forward (``slot`` 1: the graph writing ``output_alt``, see
+        capture(slots=2)).  Parameters changed since the last packing are
         re-folded into the same weight arena first (the graph reads it in place); on this
         serving path the check is the module's weights epoch (one integer compare), which
         load_state_dict, FusedStep.step and YoloxModule.weights_changed() advance --
@@ -1208,7 +1233,12 @@ class Plan:
         if self._packed_epoch != self._epoch():
             self.pack_weights()
         if self._graph is None and self._segments is None:
-            self.capture()
+            self.capture(2 if slot else 1)
+        if slot:
+            if self._graph_alt is None:
+                raise RuntimeError("replay(1) needs capture(slots=2)")
+            N.check(self.lib.yxh_graph_launch(self._graph_alt, N.stream_ptr(self.device)), "graph replay")
+            return self.output_alt
         if self._segments is not None:
             self._launch_streams()
         else:
@@ -1286,7 +1316,7 @@ class Plan:
                 self._ops[c * self._nops + i].u.conv.tile = t
         torch.cuda.synchronize(self.device)
         if self._graph is not None or self._segments is not None:  # captured graphs hold the old tiles
-            self.capture()
+            self.capture(2 if self._graph_alt is not None else 1)
         return chosen
 
     # -------------------------------------------------------------- reporting

@@ -286,9 +286,17 @@ def _f(v) -> float:
     return float(v.detach()) if torch.is_tensor(v) else float(v)
 
 
-def _oracle_train_step(oracle, monkeypatch, m, name, x, labels, spp_in):
+def _oracle_train_step(oracle, monkeypatch, m, name, x, labels, spp_in, assign=None, flips=None):
     """The oracle's fp32 autograd train step on the module's own weights, with SPP's pooling
-    ROUTING taken from the device forward (see configs[2]); returns (losses, sd)."""
+    ROUTING taken from the device forward (see configs[2]); returns (losses, sd).
+
+    ``assign`` (the device's SimOTA result, TrainGraph.assign): the oracle's losses use the
+    device's fg anchors and matched ground truths (their IoU targets from the oracle's own boxes)
+    -- SimOTA's top-k / min-cost matching is discrete, so where the 16-bit forward moves a cost
+    across a tie the two runs train different anchors and the losses differ by whole terms; the
+    assignment itself is pinned exactly elsewhere (tests/test_gpu_train.py SimOTA vs the
+    reference fixture, A = 33 600).  ``flips`` collects, per image, how many fg anchors the
+    oracle's own assignment would change."""
     import torch.nn.functional as F
     sd = {k: v.detach().cpu().float().clone() for k, v in m.state_dict().items()}
     max_pool2d = F.max_pool2d
@@ -298,11 +306,31 @@ def _oracle_train_step(oracle, monkeypatch, m, name, x, labels, spp_in):
         return t.flatten(2).gather(2, idx.flatten(2)).view_as(idx)
 
     monkeypatch.setattr(F, "max_pool2d", pool_routed_like_device)
+    simota = oracle.simota_assign
+    if assign is not None:
+        fg_all = assign["fg_mask"].bool().cpu()
+        matched_all = assign["matched_gt_inds"].long().cpu()
+        imgs = [b for b in range(labels.shape[0]) if int((labels[b].sum(1) > 0).sum()) > 0]
+        order = iter(imgs)
+
+        def simota_routed_like_device(gt_boxes, gt_classes, pred_boxes, *rest):
+            b = next(order)
+            fg = fg_all[b]
+            matched = matched_all[b][fg]
+            ious = oracle.bboxes_iou(gt_boxes, pred_boxes[fg], False)
+            piou = ious[matched, torch.arange(matched.numel())]
+            if flips is not None:
+                own_fg = simota(gt_boxes, gt_classes, pred_boxes, *rest)[0]
+                flips.append(int((own_fg != fg).sum()))
+            return fg, matched, piou, gt_classes[matched], int(fg.sum())
+
+        monkeypatch.setattr(oracle, "simota_assign", simota_routed_like_device)
     sdo = {k: v.requires_grad_("running" not in k and "num_batches" not in k) for k, v in sd.items()}
     torch.set_num_threads(16)
     ref = oracle.forward_train(sdo, oracle.ARCHS[name], x, labels)
     ref["total_loss"].backward()
     monkeypatch.setattr(F, "max_pool2d", max_pool2d)
+    monkeypatch.setattr(oracle, "simota_assign", simota)
     return ref, sdo
 
 
@@ -377,7 +405,8 @@ def test_configs4_yolox_x_1280_train_step_fp16_derived_bound(oracle, monkeypatch
     (oracle.stored_as(float16) in train mode: fp16 image, conv weights, conv outputs and block
     outputs, fp32 sums and BN statistics): each loss and each named gradient may be off the fp32
     oracle by at most FACTOR x the emulation's own distance from it (+ 1e-3 of the tensor's max,
-    the fp32 noise floor).  The factor covers what the emulation does not model -- 16-bit
+    the fp32 noise floor), both oracle runs on the device's SimOTA assignment (it is discrete:
+    _oracle_train_step).  The factor covers what the emulation does not model -- 16-bit
     backward maps and the device's summation order; measured on MI355X at batch 2 (round 4,
     printed with -s): 1.9x at worst (the stem weight's gradient, 0.147 vs 0.077 of its max;
     obj_preds.2.bias 2.8x of a 4e-5 distance, under the floor), losses within 0.1x.  Host memory:
@@ -390,13 +419,19 @@ def test_configs4_yolox_x_1280_train_step_fp16_derived_bound(oracle, monkeypatch
     x = torch.from_numpy(synthetic_images(B, 1280, 1280, seed=5)).permute(0, 3, 1, 2).float()
     labels = torch.from_numpy(synthetic_labels(B, 1280, 1280, max_gt=120, seed=6))
     out16, spp_in = _device_train_step(monkeypatch, m, x, labels, torch.float16)
+    assign = {k: v.clone() for k, v in m._train_graph.assign.items()}
     grads = {n: p.grad.cpu().float().clone() for n, p in m.named_parameters() if n in GRAD_NAMES}
     for n, p in m.named_parameters():
         assert torch.isfinite(p.grad).all(), n
-    ref, sdo = _oracle_train_step(oracle, monkeypatch, m, "yolox_x", x, labels, spp_in)
+    flips = []
+    ref, sdo = _oracle_train_step(oracle, monkeypatch, m, "yolox_x", x, labels, spp_in, assign, flips)
     ref_grads = {n: sdo[n].grad.clone() for n in GRAD_NAMES}
+    nfg = int(assign["fg_mask"].bool().sum())
+    # the device's assignment agrees with the fp32 oracle's own on all but a few anchors (a swapped anchor
+    # counts twice; measured on MI355X: 15 of 577 fg anchors over the 8 images)
+    assert sum(flips) <= 0.05 * nfg, (flips, nfg)
     with oracle.stored_as(torch.float16):
-        emu, sde = _oracle_train_step(oracle, monkeypatch, m, "yolox_x", x, labels, spp_in)
+        emu, sde = _oracle_train_step(oracle, monkeypatch, m, "yolox_x", x, labels, spp_in, assign)
     stats = {}
     for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss"):
         r = _f(ref[k])
@@ -410,7 +445,8 @@ def test_configs4_yolox_x_1280_train_step_fp16_derived_bound(oracle, monkeypatch
         d_emu = float((sde[name].grad - gr).abs().max()) / scale
         stats[name] = (d_dev, d_emu)
         assert d_dev <= FACTOR * d_emu + 1e-3, (name, stats[name], stats)
-    print("configs4 fp16 (dev, emulation) distances from the fp32 oracle:", stats)
+    print("configs4 fp16 (dev, emulation) distances from the fp32 oracle:", stats,
+          f"(SimOTA routed from the device; the oracle's own assignment differs on {flips} of {nfg} fg anchors)")
 
 
 def test_configs0_yolox_tiny_416_single_image(golden, oracle, tmp_path):

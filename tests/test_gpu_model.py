@@ -69,6 +69,14 @@ def test_uint8_nhwc_input_and_graph_replay(golden):
     g2 = plan.replay().clone()
     torch.cuda.synchronize()
     assert torch.equal(g1, ref) and torch.equal(g2, ref)
+    # two output slots (the bench's serving loop): the second graph writes output_alt only
+    plan.capture(slots=2)
+    plan.output.zero_()
+    a1 = plan.replay(1)
+    torch.cuda.synchronize()
+    assert a1.data_ptr() == plan.output_alt.data_ptr() != plan.output.data_ptr()
+    assert torch.equal(a1, ref) and not plan.output.any()
+    assert torch.equal(plan.replay(0), ref) and torch.equal(plan.replay(1), ref)
 
 
 def test_weights_repacked_after_load_state_dict(golden):

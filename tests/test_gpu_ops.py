@@ -764,7 +764,7 @@ WS_WIDE_WITHDRAWN = {270, 273, 275, 277, 278}  # spilled (10- / 16-wave blocks):
 WS_WIDE_GEOMS = [  # cin, cout, s, H, W (input), batch: yolox_x (80 / 160 / 320) and yolox_l (512) 3x3s
     (80, 80, 1, 35, 41, 2), (80, 160, 2, 66, 70, 2), (160, 160, 1, 40, 38, 2), (160, 320, 2, 42, 38, 2),
     (320, 320, 1, 20, 22, 2), (320, 320, 2, 20, 20, 2), (320, 640, 2, 21, 19, 2), (512, 512, 1, 12, 14, 2),
-    (320, 96, 1, 9, 7, 3)]
+    (320, 96, 1, 9, 7, 3), (16, 80, 1, 40, 36, 2)]
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
@@ -780,7 +780,7 @@ def test_conv_ws_3x3_wide_channels(dtype, geom):
     wide = torch.zeros(B, H, W, cin + 32, dtype=dtype, device=DEV)
     wide[..., 16:16 + cin] = nhwc(x, dtype)
     ran = 0
-    for tid in range(261, 281):
+    for tid in list(range(261, 281)) + [289]:  # 289: the training stem's 16 -> 80 (K 32, upper half zero)
         if tid in WS_WIDE_WITHDRAWN:
             continue
         try:
