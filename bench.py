@@ -6,9 +6,8 @@ One step = one batch through the hot path: the captured hipGraph of the whole
 forward (Focus -> CSPDarknet -> PAFPN -> decoupled head with fused decode, 53
 kernels) followed by device post-processing (filter, sort, bitmask NMS) at the
 processor defaults (conf 0.5, nms 0.65); a batch's NMS runs on a side stream beside the
-next batch's forward, which writes the other of two output slots (two captured graphs), so
-it waits only for the filter pass of the batch two back (the one reader of its slot) --
---serial-nms runs them back to back on one stream.  Inputs are resident in HBM (uint8 NHWC, as the
+next batch's forward, which waits only for the NMS filter pass (the one reader of the
+forward's output) -- --serial-nms runs them back to back on one stream.  Inputs are resident in HBM (uint8 NHWC, as the
 processor's letterbox hands them to the forward) before the timed region.  With --gpus N (torchrun, one process per GPU) each rank
 runs an independent replica -- inference has no exchange step, so there is no
 collective in the data path -- and value = all images / max
@@ -87,8 +86,11 @@ def parse():
     ap.add_argument("--nms", type=float, default=0.65)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--one-slot", action="store_true",
-                    help="one output slot: each forward waits for the previous batch's NMS filter (round-4 pipeline)")
+    ap.add_argument("--fwd-priority", action="store_true",
+                    help="run the forward on a high-priority stream (the NMS side stream stays normal)")
+    ap.add_argument("--two-slot", action="store_true",
+                    help="two output slots (two captured graphs): a forward never waits for the previous batch's "
+                         "NMS filter; measured slower (the NMS then overlaps the next forward's first layers)")
     ap.add_argument("--serial-nms", action="store_true",
                     help="NMS behind each forward on one stream (default: beside the next batch's forward)")
     ap.add_argument("--dry-run", action="store_true",
@@ -465,15 +467,18 @@ def main():
     if args.tune_file and rank == 0 and not os.path.exists(args.tune_file):
         engine.save_tune_cache(args.tune_file)
     # Serving pipeline: the NMS of batch k runs on a side stream beside the forward of batch
-    # k+1, and the forward's output rows are double-buffered too (two captured graphs of the same
-    # forward, Plan.capture(slots=2)): forward k+1 writes the other slot, so it never waits for
-    # batch k's NMS; forward k+2 waits for the filter pass of batch k -- the one reader of that
-    # slot (event recorded by yxh_postprocess_ev), long done by then.  Detections are
-    # double-buffered.  --serial-nms puts the NMS back behind each forward on one stream.
-    slots = 1 if args.serial_nms or args.one_slot else 2
+    # k+1, which waits only for batch k's filter pass (the one reader of the forward's output rows,
+    # event recorded by yxh_postprocess_ev); detections are double-buffered.  --two-slot also
+    # double-buffers the output rows (Plan.capture(slots=2)) so no forward waits at all: on MI355X
+    # that measured slower (18 147-18 302 vs 18 508-18 577 img/s, profiles/r05/output_slots_ab.txt) --
+    # the NMS kernels then run beside the next forward's stem and stretch it more than the wait
+    # costs.  --serial-nms puts the NMS back behind each forward on one stream.
+    slots = 2 if args.two_slot and not args.serial_nms else 1
     plan.capture(slots)
     A = plan.anchors
-    stream = torch.cuda.current_stream(dev)
+    # --fwd-priority: the forward on a high-priority stream, so the NMS kernels of the previous batch
+    # (side stream, normal priority) fill gaps instead of taking CUs from the forward
+    stream = torch.cuda.Stream(dev, priority=-1) if args.fwd_priority else torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(dev) if not args.serial_nms else stream
     dets = [torch.empty(B, A, 7, dtype=torch.float32, device=dev) for _ in range(2)]
     cnts = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(2)]
@@ -489,12 +494,14 @@ def main():
             stream.wait_event(filt[(k - slots) % 2])  # the filter of the last batch in this output slot
         if ev0 is not None:
             ev0.record(stream)
-        out = plan.replay(k % slots)
+        with torch.cuda.stream(stream):
+            out = plan.replay(k % slots)
         if ev1 is not None:
             ev1.record(stream)
         det, counts = dets[k % 2], cnts[k % 2]
         if args.serial_nms:
-            postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts)
+            with torch.cuda.stream(stream):
+                postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts)
         else:
             fwd_done.record(stream)
             side.wait_event(fwd_done)

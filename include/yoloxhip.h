@@ -327,11 +327,11 @@ size_t yxh_sizeof_aug_image(void);
  *   workspace >= yxh_postprocess_workspace_bytes(B, A)
  * Any candidate count (anchors <= 2^19 per image).  The u64 suppression matrix is built
  * and consumed in passes of R sorted rows x ceil(A/64) words per image, R chosen so one
- * pass holds at most the mask budget (256 MiB over the batch), so the workspace grows
+ * pass holds at most the mask budget (320 MiB over the batch), so the workspace grows
  * linearly in A for large inputs instead of quadratically.
  */
 size_t yxh_postprocess_workspace_bytes(int32_t batch, int32_t anchors);
-/* Process-wide mask budget in bytes (0 = the 256 MiB default).  Changes the workspace size
+/* Process-wide mask budget in bytes (0 = the 320 MiB default).  Changes the workspace size
  * and the pass count of later calls; tests use a tiny budget to force many passes. */
 void yxh_set_nms_mask_budget(size_t bytes);
 int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_classes,

@@ -41,7 +41,10 @@ namespace yxh {
 constexpr int kSortCap = 16384;      // keys sorted per block in LDS (128 KiB)
 constexpr int kMaxAnchors = 1 << 19;  // pp_reduce keeps one removed-bit per candidate in LDS
 constexpr int kRow = 8;  // x1 y1 x2 y2 obj conf cls score
-constexpr size_t kMaskBudget = 256ull << 20;  // bytes of suppression words per pass (all images)
+// bytes of suppression words per pass (all images): 320 MiB holds every row of the bench's batch (32 x 8 400
+// anchors: 285 MiB) in one pass -- at 256 MiB a second mask + reduce pass launched ~8 000 blocks that
+// had nothing to do (the candidates of conf 0.5 fit the first 64-row blocks)
+constexpr size_t kMaskBudget = 320ull << 20;
 size_t g_mask_budget = kMaskBudget;  // yxh_set_nms_mask_budget (tests: force many passes)
 
 struct PPWork {
@@ -65,12 +68,19 @@ __device__ __forceinline__ unsigned int ordered(float f) {
 // each take the argmax over a quarter of the classes (first maximum wins, as a serial
 // strict '>' scan does), combined with two lane shuffles.
 __global__ __launch_bounds__(256) void pp_filter(float* pred, int A, int C, float conf, PPWork w) {
-    extern __shared__ float tile[];  // [64][5+C]
+    extern __shared__ __attribute__((aligned(16))) float tile[];  // [64][5+C]
     const int D = 5 + C;
     const int b = blockIdx.y, a0 = blockIdx.x * 64, tid = threadIdx.x;
     const int rows = min(64, A - a0);
     float* src = pred + ((long long)b * A + a0) * D;
-    for (int q = tid; q < rows * D; q += 256) tile[q] = src[q];
+    // the block's rows are one contiguous run: 16-byte loads when it is aligned (the bench's
+    // [32, 8400, 85] rows: every block), 4-byte ones otherwise
+    const int n = rows * D;
+    if ((n & 3) == 0 && ((uintptr_t)src & 15) == 0) {
+        for (int q = tid; q < (n >> 2); q += 256) ((float4*)tile)[q] = ((const float4*)src)[q];
+    } else {
+        for (int q = tid; q < n; q += 256) tile[q] = src[q];
+    }
     __syncthreads();
     const int r = tid >> 2, part = tid & 3;
     const float* p = tile + min(r, rows - 1) * D;
@@ -450,7 +460,9 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     for (int rb0 = 0; rb0 < w.capw; rb0 += rbp) {
         // worst-case pairs of this pass (n = A): rbp row blocks x up to capw - rb0 column blocks
         const long long worst = (long long)rbp * (w.capw - rb0);
-        const int gx = (int)std::min<long long>(worst, std::max(128, 8192 / B));
+        // blocks per image: pairs are dealt round-robin, so few blocks serve few candidates (the
+        // common case) without an empty grid of thousands, and many candidates still spread out
+        const int gx = (int)std::min<long long>(worst, std::max(32, 2048 / B));
         hipLaunchKernelGGL(pp_mask, dim3(gx, B), dim3(256), 0, st, A, nms, agnostic, vanilla_numel, w, rb0,
                            rb0 + rbp);
         YXH_CHECK_LAUNCH("pp_mask");
