@@ -460,9 +460,10 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     for (int rb0 = 0; rb0 < w.capw; rb0 += rbp) {
         // worst-case pairs of this pass (n = A): rbp row blocks x up to capw - rb0 column blocks
         const long long worst = (long long)rbp * (w.capw - rb0);
-        // blocks per image: pairs are dealt round-robin, so few blocks serve few candidates (the
-        // common case) without an empty grid of thousands, and many candidates still spread out
-        const int gx = (int)std::min<long long>(worst, std::max(32, 2048 / B));
+        // blocks per image (pairs dealt round-robin): at conf 0.5 an image of the bench keeps ~1 000
+        // candidates = ~150 64 x 64 pairs, so fewer blocks serialise them (64 per image measured
+        // 49.7 vs 29.4 us per pass, profiles/r05/nms_r5n.txt)
+        const int gx = (int)std::min<long long>(worst, std::max(128, 8192 / B));
         hipLaunchKernelGGL(pp_mask, dim3(gx, B), dim3(256), 0, st, A, nms, agnostic, vanilla_numel, w, rb0,
                            rb0 + rbp);
         YXH_CHECK_LAUNCH("pp_mask");

@@ -108,7 +108,9 @@ struct RedArgs {
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void chan_reduce(RedArgs a) {
     constexpr int EPC = Chunk<T>::N;
-    __shared__ float red[2][256 * EPC];
+    // one staging buffer for both sums in turn (8 KiB at 16 bits): beside the side stream's weight
+    // gradients (up to ~140 KiB of LDS per CU) a 16 KiB block often found no room on a CU
+    __shared__ float red[256 * EPC];
     // blockIdx.y = channel group of up to 256 16-byte chunks (yolox_x fp32: 1280 channels)
     const int C = a.x.C, cg = blockIdx.y * 256 * EPC, CL = min(C - cg, 256 * EPC), nch = CL / EPC;
     const int tid = threadIdx.x;
@@ -180,22 +182,19 @@ __global__ __launch_bounds__(256) void chan_reduce(RedArgs a) {
             accum(v, gv);
         }
     }
+    // thread t < C sums channel t over the row lanes (fixed order: deterministic), Σ1 then Σ2
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) {
-        red[0][tid * EPC + e] = s1[e];
-        red[1][tid * EPC + e] = s2[e];
-    }
-    __syncthreads();
-    // thread t < C sums channel t over the row lanes (fixed order: deterministic)
-    for (int c = tid; c < CL; c += 256) {
-        const int qq = c / EPC, e = c - qq * EPC;
-        float t1 = 0.0f, t2 = 0.0f;
-        for (int l = 0; l < rpi; ++l) {
-            t1 += red[0][(l * nch + qq) * EPC + e];
-            t2 += red[1][(l * nch + qq) * EPC + e];
+    for (int k = 0; k < 2; ++k) {
+        if (k) __syncthreads();  // every thread is done reading the Σ1 stage
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) red[tid * EPC + e] = k ? s2[e] : s1[e];
+        __syncthreads();
+        for (int c = tid; c < CL; c += 256) {
+            const int qq = c / EPC, e = c - qq * EPC;
+            float t = 0.0f;
+            for (int l = 0; l < rpi; ++l) t += red[(l * nch + qq) * EPC + e];
+            a.partial[((long long)blockIdx.x * 2 + k) * C + cg + c] = t;
         }
-        a.partial[((long long)blockIdx.x * 2) * C + cg + c] = t1;
-        a.partial[((long long)blockIdx.x * 2 + 1) * C + cg + c] = t2;
     }
 }
 
@@ -212,42 +211,39 @@ struct FinArgs {
 };
 
 // 4 channels per block, a wave per channel: each lane sums its strided share of the
-// per-block partials in double (four independent chains, so the loads of four rows are in
-// flight at once: the kernel is latency-bound, ~1024 partials per channel), then a
+// per-block partials in double (eight independent chains, so the loads of eight rows are in
+// flight at once: the kernel is latency-bound, <= 512 partials per channel), then a
 // fixed-order tree over the lanes: deterministic.
 __global__ __launch_bounds__(256) void chan_finalize(FinArgs f) {
     __shared__ double red[2][256];
     const int j = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + j;
-    double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
+    // eight independent chains: the <= 512 partials of a channel (red_blocks) arrive in ONE round of
+    // loads per lane instead of two dependent rounds
+    constexpr int U = 8;
+    double a1[U], a2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a1[u] = a2[u] = 0.0;
     if (c < f.C) {
         const long long rs = 2LL * f.C;  // partial row stride (one block's [2][C])
         const float* p0 = f.partial + c;
-        int b = lane;
-        for (; b + 192 < f.nblk; b += 256) {
-            float v1[4], v2[4];
+        for (int b = lane; b < f.nblk; b += 64 * U) {
+            float v1[U], v2[U];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                v1[u] = p0[(long long)(b + 64 * u) * rs];
-                v2[u] = p0[(long long)(b + 64 * u) * rs + f.C];
+            for (int u = 0; u < U; ++u) {
+                const int bb = b + 64 * u;
+                v1[u] = bb < f.nblk ? p0[(long long)bb * rs] : 0.0f;
+                v2[u] = bb < f.nblk ? p0[(long long)bb * rs + f.C] : 0.0f;
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U; ++u) {
                 a1[u] += v1[u];
                 a2[u] += v2[u];
             }
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int bb = b + 64 * u;
-            if (bb < f.nblk) {
-                a1[u] += p0[(long long)bb * rs];
-                a2[u] += p0[(long long)bb * rs + f.C];
-            }
-        }
     }
-    red[0][threadIdx.x] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
-    red[1][threadIdx.x] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+    red[0][threadIdx.x] = ((a1[0] + a1[1]) + (a1[2] + a1[3])) + ((a1[4] + a1[5]) + (a1[6] + a1[7]));
+    red[1][threadIdx.x] = ((a2[0] + a2[1]) + (a2[2] + a2[3])) + ((a2[4] + a2[5]) + (a2[6] + a2[7]));
     __syncthreads();
     for (int s = 32; s > 0; s >>= 1) {
         if (lane < s) {
@@ -1617,7 +1613,7 @@ int check_view(const yxh_src* s, int dt, const char* what) {
 
 constexpr int kRedMaxBlocks = 1024;
 
-// Reduction blocks: ~8 rows per thread, at most YXH_RED_BLOCKS (default 512: two 4-wave blocks
+// Reduction blocks: ~32 rows per thread, at most YXH_RED_BLOCKS (default 512: two 4-wave blocks
 // per CU, one round; chan_finalize then reads 512 partials per channel instead of 1024 -- it is
 // latency-bound on the strided partial rows and runs once per BatchNorm per pass)
 int red_cap() {
@@ -1632,7 +1628,9 @@ int red_cap() {
 int red_blocks(int M, int C, int dt, int* rpb) {
     const int nch = C / (16 / esz(dt));
     const int rpi = nch >= 256 ? 1 : 256 / nch;
-    int nblk = (int)(((long long)M + rpi * 8 - 1) / (rpi * 8));  // ~8 rows per thread (4 in flight)
+    // ~32 rows per thread (2-4 in flight): the mid-size maps of yolox_s (fp32: 64-256 channels at 160-40 px)
+    // then leave 4x fewer partials for chan_finalize, which is latency-bound on them
+    int nblk = (int)(((long long)M + rpi * 32 - 1) / (rpi * 32));
     const int cap = red_cap();
     nblk = nblk < 1 ? 1 : (nblk > cap ? cap : nblk);
     *rpb = (M + nblk - 1) / nblk;

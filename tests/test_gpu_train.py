@@ -804,8 +804,8 @@ def test_train_step_bf16_autocast_close_to_fp32(monkeypatch):
     The assignment is discrete (dynamic-k top-k over costs): a bf16 rounding can move
     one anchor across a level, which zeroes a whole per-level cls branch gradient in
     one run and not the other.  Tile tuning is off here (by-shape tiles, deterministic
-    accumulation order), and when the foreground counts differ the check falls back to
-    the tensors both runs update (mean cosine > 0.9)."""
+    accumulation order), and when the foreground anchors differ (count or placement) the check
+    falls back to the tensors both runs update (mean cosine > 0.9)."""
     import yolox_amd.train as T
     monkeypatch.setenv("YOLOX_AMD_TRAIN_TUNE", "0")
     monkeypatch.setattr(T, "_TRAIN_TILES", {})
@@ -814,16 +814,19 @@ def test_train_step_bf16_autocast_close_to_fp32(monkeypatch):
     out32 = m(x.cuda(), labels.cuda())
     out32["total_loss"].backward()
     g32 = {n: p.grad.clone() for n, p in m.named_parameters()}
+    fg32 = m._train_graph.assign["fg_mask"].bool().clone()
     m.load_state_dict(sd)
     m.zero_grad(set_to_none=True)
     with torch.autocast("cuda", dtype=torch.bfloat16):
         out16 = m(x.cuda(), labels.cuda())
     out16["total_loss"].backward()
     torch.cuda.synchronize()
+    fg16 = m._train_graph.assign["fg_mask"].bool()
     assert abs(float(out16["total_loss"]) - float(out32["total_loss"])) < 0.05 * float(out32["total_loss"])
     cos = {n: float(F.cosine_similarity(p.grad.flatten(), g32[n].flatten(), dim=0))
            for n, p in m.named_parameters() if p.numel() > 1000}
-    if float(out16["num_fg"]) != float(out32["num_fg"]):  # different assignment
+    # different assignment: the same foreground COUNT can still put an anchor on another level
+    if float(out16["num_fg"]) != float(out32["num_fg"]) or not torch.equal(fg16, fg32):
         both = [c for n, c in cos.items()
                 if float(dict(m.named_parameters())[n].grad.abs().max()) > 0 and float(g32[n].abs().max()) > 0]
         assert np.mean(both) > 0.9, np.mean(both)
