@@ -71,8 +71,10 @@ def metric_name(args) -> str:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 100 timed steps (~0.17 s of the default workload): the 20-step window read 0.8-1.6 % low on one
+    # box (clock ramp; profiles/r05/bench_r5p_*.json)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="yolox_s")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--chunk", type=int, default=0, help="images per pass of the op list (0 = whole batch)")

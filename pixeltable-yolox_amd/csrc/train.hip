@@ -160,9 +160,10 @@ __global__ __launch_bounds__(256) void chan_reduce(RedArgs a) {
     };
     // U rows in flight per thread: all loads first, then the rows in order (the same
     // fixed summation order as one row at a time).  BWD holds y, the fp32 gradient and four
-    // coefficient rows per channel: at U = 4 it took 159 VGPRs (3 waves per SIMD, so the
-    // 1024-block grid ran in two rounds: the slowest kernel of the configs[4] step's main stream)
-    constexpr int U = MODE == RED_BWD ? 2 : 4;
+    // coefficient rows per channel: at U = 4 the 16-bit form took 159 VGPRs (3 waves per SIMD, so
+    // the 1024-block grid ran in two rounds: the slowest kernel of the configs[4] step's main
+    // stream); fp32 (4 channels per 16-byte chunk) fits 91 at U = 4
+    constexpr int U = MODE == RED_BWD && sizeof(T) == 2 ? 2 : 4;
     if (rl < rpi) {
         int r = r0 + rl;
         for (; r + (U - 1) * rpi < r1; r += U * rpi) {
@@ -1613,7 +1614,7 @@ int check_view(const yxh_src* s, int dt, const char* what) {
 
 constexpr int kRedMaxBlocks = 1024;
 
-// Reduction blocks: ~32 rows per thread, at most YXH_RED_BLOCKS (default 512: two 4-wave blocks
+// Reduction blocks: ~8 rows per thread, at most YXH_RED_BLOCKS (default 512: two 4-wave blocks
 // per CU, one round; chan_finalize then reads 512 partials per channel instead of 1024 -- it is
 // latency-bound on the strided partial rows and runs once per BatchNorm per pass)
 int red_cap() {
@@ -1628,9 +1629,9 @@ int red_cap() {
 int red_blocks(int M, int C, int dt, int* rpb) {
     const int nch = C / (16 / esz(dt));
     const int rpi = nch >= 256 ? 1 : 256 / nch;
-    // ~32 rows per thread (2-4 in flight): the mid-size maps of yolox_s (fp32: 64-256 channels at 160-40 px)
-    // then leave 4x fewer partials for chan_finalize, which is latency-bound on them
-    int nblk = (int)(((long long)M + rpi * 32 - 1) / (rpi * 32));
+    // ~8 rows per thread (2-4 in flight).  (~32 rows per thread left 4x fewer partials for chan_finalize
+    // but too few blocks in flight for the mid-size fp32 maps: configs[2] 570 -> 527 img/s, round 5)
+    int nblk = (int)(((long long)M + rpi * 8 - 1) / (rpi * 8));
     const int cap = red_cap();
     nblk = nblk < 1 ? 1 : (nblk > cap ? cap : nblk);
     *rpb = (M + nblk - 1) / nblk;
