@@ -1768,6 +1768,18 @@ int channel_sum_launch(int dt, int B, const yxh_src* x, float* out, void* ws, si
 
 namespace {
 
+// Blocks a weight-gradient grid aims for (splits x tiles): YXH_WGRAD_BLOCKS, default 512 = two per CU.
+// The weight gradients run on a side stream beside the data-gradient chain; a grid that fills every
+// CU's registers leaves the main stream's BatchNorm reductions no room until its blocks retire.
+int wgrad_target_blocks() {
+    static const int v = [] {
+        const char* e = getenv("YXH_WGRAD_BLOCKS");
+        const int x = e ? atoi(e) : 512;
+        return x < 64 ? 64 : x > 4096 ? 4096 : x;
+    }();
+    return v;
+}
+
 template <typename T, int TN, int TM, int WR, int WC, int KS>
 int launch_wgrad_t(WgradParams p, hipStream_t st) {
     constexpr int EPC = Chunk<T>::N;
@@ -1779,7 +1791,7 @@ int launch_wgrad_t(WgradParams p, hipStream_t st) {
     (void)KP;
     // ~2 blocks per CU over the whole grid; at least 8 stages per split
     const long long tiles = (long long)ntn * ntap * p.ntc;
-    long long splits = (512 + tiles - 1) / tiles;
+    long long splits = (wgrad_target_blocks() + tiles - 1) / tiles;
     const long long max_splits = (p.nst + 7) / 8;
     if (splits > max_splits) splits = max_splits;
     splits = ws_cap_splits(p, splits);
@@ -1832,7 +1844,7 @@ int launch_wgrad_f32(WgradParams p, hipStream_t st) {
     const int ntn = (p.cout + TN - 1) / TN, ntc = (p.cin + TC - 1) / TC;
     p.nst = (int)(((long long)p.M + KP - 1) / KP);
     const long long tiles = (long long)ntn * ntc * taps;
-    long long splits = (512 + tiles - 1) / tiles;  // about two blocks per CU
+    long long splits = (wgrad_target_blocks() + tiles - 1) / tiles;  // about two blocks per CU
     const long long max_splits = (p.nst + 3) / 4;  // >= 4 stages per split
     if (splits > max_splits) splits = max_splits;
     splits = ws_cap_splits(p, splits);
@@ -1859,7 +1871,7 @@ int launch_wgrad9t_f32(WgradParams p, hipStream_t st) {
     const int ntn = (p.cout + TN - 1) / TN, ntc = (p.cin + TC - 1) / TC;
     p.nst = p.B * p.out_h * nseg;
     const long long tiles = (long long)ntn * ntc;
-    long long splits = (512 + tiles - 1) / tiles;
+    long long splits = (wgrad_target_blocks() + tiles - 1) / tiles;
     const long long max_splits = (p.nst + 3) / 4;
     if (splits > max_splits) splits = max_splits;
     splits = ws_cap_splits(p, splits);
@@ -1891,7 +1903,7 @@ int launch_wgrad9t_h(WgradParams p, hipStream_t st) {
         const int ntn = (p.cout + TN - 1) / TN, ntc = (p.cin + TC - 1) / TC;
         p.nst = p.B * p.out_h * nseg;
         const long long tiles = (long long)ntn * ntc;
-        long long splits = (512 + tiles - 1) / tiles;
+        long long splits = (wgrad_target_blocks() + tiles - 1) / tiles;
         const long long max_splits = (p.nst + 3) / 4;
         if (splits > max_splits) splits = max_splits;
         splits = ws_cap_splits(p, splits, 16LL << 20);
