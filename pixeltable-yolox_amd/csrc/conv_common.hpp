@@ -310,7 +310,7 @@ constexpr int kNumWsPostTiles = 16;
 int conv_ws1_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumWs1Tiles = 10;
 // ... and its deep row pipelines (conv_ws1 ids 11..10+kNumWs1DeepTiles): tile ids 241..240+kNumWs1DeepTiles
-constexpr int kNumWs1DeepTiles = 12;  // 249-252: upsampled source 0
+constexpr int kNumWs1DeepTiles = 18;  // 249-252, 256: upsampled source 0; 253-258: full-width (round 5)
 // fp32 1x1 GEMM for the training path, k-minor MFMA operands (conv_pw1f.hip): tile ids 211..210+kNumPw1fTiles
 int conv_pw1f_dispatch(int dtype, int id, const ConvParams& p, hipStream_t st);
 constexpr int kNumPw1fTiles = 4;

@@ -320,6 +320,17 @@ static int ws1_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 20: return launch_ws1<T, 512, 64, 64, 2, 2, 2, 1, 2, true>(p, st);
         case 21: return launch_ws1<T, 256, 64, 128, 4, 1, 1, 2, 2, true>(p, st);
         case 22: return launch_ws1<T, 256, 32, 128, 4, 1, 1, 1, 4, true>(p, st);
+        // every output channel in one block (round 5): the 40x40 / 20x20 1x1s with 256 outputs read
+        // their input ONCE instead of once per 128- / 64-channel slice (the re-read through LDS-DMA
+        // was most of their time: 2.5-5.5x a copy of their bytes, profiles/r04/pw_probe_r4.txt);
+        // 128 weight registers per wave (K split two ways past 256 input channels)
+        // (two 4-wave blocks per CU / eight-wave blocks hold 256 registers per lane: 32-pixel tiles spilled)
+        case 23: return launch_ws1<T, 256, 32, 256, 4, 1, 1, 1, 3>(p, st);
+        case 24: return launch_ws1<T, 256, 64, 256, 4, 1, 1, 1, 3>(p, st);
+        case 25: return launch_ws1<T, 512, 16, 256, 4, 2, 1, 1, 4>(p, st);
+        case 26: return launch_ws1<T, 512, 16, 256, 4, 2, 1, 1, 4, true>(p, st);
+        case 27: return launch_ws1<T, 128, 64, 256, 4, 1, 1, 1, 3>(p, st);
+        case 28: return launch_ws1<T, 1024, 32, 128, 4, 2, 1, 1, 2>(p, st);
         default: set_error("conv_ws1 tile id %d", id); return YXH_EINVAL;
     }
 }

@@ -1052,7 +1052,7 @@ def test_conv_ws1_upsampled_source(c0, c1, cout, H, W, B):
     want = ref_conv(torch.cat([F.interpolate(x0, scale_factor=2, mode="nearest"), x1], 1), conv, bn, "silu")
     srcs = [(buf0, 32, c0, 1), (X1, 0, c1, 0)]
     ran = 0
-    for tid in range(249, 253):
+    for tid in list(range(249, 253)) + [256]:
         try:
             y = run_conv(srcs, conv, bn, dtype, tile=2 * tid)
         except NotImplementedError as e:
@@ -1067,13 +1067,15 @@ WS1_GEOMS = [  # sources (channels, buffer channels, channel offset), cout, H, W
     ([(64, 64, 0)], 64, 37, 45, 3), ([(32, 64, 0), (32, 32, 0)], 64, 40, 24, 2), ([(128, 160, 16)], 128, 20, 21, 4),
     ([(128, 256, 0), (128, 128, 0)], 256, 20, 20, 2), ([(256, 256, 0)], 128, 23, 17, 3),
     ([(256, 512, 256), (256, 256, 0)], 512, 11, 13, 4), ([(1024, 1024, 0)], 512, 10, 10, 4),
-    ([(256, 256, 0)], 256, 40, 40, 32)]
+    ([(256, 256, 0)], 256, 40, 40, 32), ([(128, 128, 0)], 256, 19, 23, 2), ([(512, 512, 0)], 256, 12, 14, 3),
+    ([(256, 256, 0)], 240, 9, 11, 2)]
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("geom", WS1_GEOMS)
 def test_conv_ws1_1x1(dtype, geom):
-    """conv_ws1 (ids 201-210, and 241-248: 3-4 row buffers in flight): weight-stationary
+    """conv_ws1 (ids 201-210, 241-248: 3-4 row buffers in flight, 253-258: every output channel in
+    one block, round 5): weight-stationary
     persistent 1x1 conv over one or two dense sources (channel slices of wider buffers), output
     into a channel slice, every variant built for this cin vs torch fp32; partial last pixel
     tile, cout tails of the block."""
@@ -1091,7 +1093,7 @@ def test_conv_ws1_1x1(dtype, geom):
     want = ref_conv(torch.cat(parts, 1), conv, bn, "silu")
     out = torch.zeros(B, H, W, cout + 16, dtype=dtype, device=DEV)
     ran = 0
-    for tid in list(range(201, 211)) + list(range(241, 249)):
+    for tid in list(range(201, 211)) + list(range(241, 249)) + [253, 254, 255, 257, 258]:
         try:
             y = run_conv(bufs, conv, bn, dtype, out=out, out_coff=8, tile=2 * tid)
         except NotImplementedError as e:
