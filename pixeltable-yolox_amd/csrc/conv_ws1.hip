@@ -200,7 +200,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
             for (int q = WCB; q < NP; ++q) epi_piece(tprev, accp, q / FR, q % FR);
 
         if constexpr (WK > 1) {
-            char* red = smem + 2 * HBYTES;
+            char* red = smem + NBUF * HBYTES;  // past every row buffer (NBUF - 1 tiles are in flight)
             const int grp = wm * WN + wn;
 #pragma unroll
             for (int i = 0; i < FR; ++i)
