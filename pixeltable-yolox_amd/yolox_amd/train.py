@@ -146,6 +146,11 @@ CONV_TUNE_TILES = _BASE_TILES + ([] if os.environ.get("YOLOX_AMD_TRAIN_TILES16")
 CONV_TUNE_TILES_F32 = _BASE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)] + [2 * i for i in range(211, 217)]
 WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 25)) + list(range(25, 31))
 _TRAIN_TILES: dict = {}
+# YOLOX_AMD_TUNE_CHECK_DET=1 (tests): every applicable candidate also runs twice into a zeroed sink and
+# must write the same bytes both times; (shape key, tile) pairs that do not are collected here
+_CHECK_DET = os.environ.get("YOLOX_AMD_TUNE_CHECK_DET", "0") == "1"
+TUNE_DET_FAILURES: list = []
+TUNE_DET_CHECKED = [0]
 # diagnostic (tools/train_shapes.py): every conv / wgrad launch of the training step, in order
 _LAUNCH_LOG: Optional[list] = [] if os.environ.get("YOLOX_AMD_TRAIN_LOG") else None
 
@@ -401,6 +406,16 @@ class TrainGraph:
                 ms = ev0.elapsed_time(ev1) / reps
                 if ms < best[0]:
                     best = (ms, tile)
+                if _CHECK_DET:
+                    sink = scratch[:out_bytes]
+                    sink.zero_()
+                    fn(ref, st)
+                    first = sink.clone()
+                    sink.zero_()
+                    fn(ref, st)
+                    if not torch.equal(first, sink):
+                        TUNE_DET_FAILURES.append((key, tile))
+                    TUNE_DET_CHECKED[0] += 1
         finally:
             setattr(d, out_field, real)
         _TRAIN_TILES[key] = best[1]

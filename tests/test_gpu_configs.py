@@ -399,6 +399,37 @@ def _device_train_step(monkeypatch, m, x, labels, amp_dtype=None):
     return out, spp_in
 
 
+@pytest.mark.parametrize("name,size,dtype", [("yolox_s", 640, None), ("yolox_x", 1280, torch.float16)])
+def test_every_training_candidate_tile_is_deterministic(monkeypatch, name, size, dtype):
+    """Race detector for the training tuner's candidates at the benched shapes (configs[2]: yolox_s fp32
+    batch 8; configs[4]: yolox_x 1280 --fp16 batch 8): the first step tunes every forward conv, data
+    gradient and weight gradient shape, and with the check on every applicable candidate tile runs twice
+    more into a zeroed sink and must write the same bytes both times (split-K partial sums are reduced in
+    a fixed order, so even the accumulating forms are bit-stable)."""
+    import yolox_amd.train as T
+    from yolox_amd.models import YoloxModule
+    from yolox_amd.weights import synthetic_images, synthetic_labels
+    monkeypatch.setattr(T, "_TRAIN_TILES", {})
+    monkeypatch.setattr(T, "_CHECK_DET", True)
+    monkeypatch.setattr(T, "TUNE_DET_FAILURES", [])
+    monkeypatch.setattr(T, "TUNE_DET_CHECKED", [0])
+    B = 8
+    m = YoloxModule.synthetic(name, seed=0, device="cuda").train()
+    x = torch.from_numpy(synthetic_images(B, size, size, seed=5)).permute(0, 3, 1, 2).float().cuda()
+    labels = torch.from_numpy(synthetic_labels(B, size, size, max_gt=120, seed=6)).cuda()
+    m.zero_grad(set_to_none=True)
+    if dtype is None:
+        out = m(x, labels)
+    else:
+        with torch.autocast("cuda", dtype=dtype):
+            out = m(x.to(dtype), labels)
+    out["total_loss"].backward()
+    torch.cuda.synchronize()
+    print(f"{name}: {T.TUNE_DET_CHECKED[0]} (shape, tile) pairs checked, failures {T.TUNE_DET_FAILURES}")
+    assert not T.TUNE_DET_FAILURES
+    assert T.TUNE_DET_CHECKED[0] > 100
+
+
 GRAD_NAMES = ("backbone.backbone.stem.conv.conv.weight", "backbone.backbone.dark2.0.conv.weight",
               "backbone.backbone.dark5.1.conv2.conv.weight", "backbone.C3_n4.conv3.conv.weight",
               "head.stems.0.conv.weight", "head.cls_convs.0.1.conv.weight", "head.cls_preds.0.weight",
