@@ -14,6 +14,8 @@ L = N.lib()
 dev = torch.device("cuda:0")
 st = N.stream_ptr(dev)
 SHAPES = [(204800, 64, 64), (51200, 128, 128), (819200, 64, 64), (12800, 512, 512), (51200, 256, 256)]
+if os.environ.get("PW_SHAPES"):  # "M,K,N;M,K,N": e.g. a sweep over M for the fixed vs per-pixel cost
+    SHAPES = [tuple(int(v) for v in t.split(",")) for t in os.environ["PW_SHAPES"].split(";")]
 TILES = [int(t) for t in sys.argv[1:]] or [97 * 2, 99 * 2, 203 * 2, 205 * 2, 206 * 2, 207 * 2]
 
 
