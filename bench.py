@@ -5,9 +5,11 @@ configs[1]: batch 32 per GPU, synthetic uniform [0,255] images, seeded weights).
 One step = one batch through the hot path: the captured hipGraph of the whole
 forward (Focus -> CSPDarknet -> PAFPN -> decoupled head with fused decode, 53
 kernels) followed by device post-processing (filter, sort, bitmask NMS) at the
-processor defaults (conf 0.5, nms 0.65); a batch's NMS runs on a side stream beside the
-next batch's forward, which waits only for the NMS filter pass (the one reader of the
-forward's output) -- --serial-nms runs them back to back on one stream.  Inputs are resident in HBM (uint8 NHWC, as the
+processor defaults (conf 0.5, nms 0.65); the NMS filter pass (the one reader of the forward's
+output) runs in stream order behind its forward and the rest of that batch's NMS on a side stream
+beside the next batch's forward (yxh_postprocess_split; --nms-event: the whole NMS on the side
+stream, the next forward waiting on the filter's event) -- --serial-nms runs them back to back on
+one stream.  Inputs are resident in HBM (uint8 NHWC, as the
 processor's letterbox hands them to the forward) before the timed region.  With --gpus N (torchrun, one process per GPU) each rank
 runs an independent replica -- inference has no exchange step, so there is no
 collective in the data path -- and value = all images / max
@@ -95,6 +97,10 @@ def parse():
                          "NMS filter; measured slower (the NMS then overlaps the next forward's first layers)")
     ap.add_argument("--serial-nms", action="store_true",
                     help="NMS behind each forward on one stream (default: beside the next batch's forward)")
+    ap.add_argument("--nms-event", action="store_true",
+                    help="the whole NMS on the side stream, the next forward waiting on its filter event across "
+                         "streams (round 4-5 form; default: the filter in order behind the forward on its stream, "
+                         "the rest of the NMS on the side stream, yxh_postprocess_split)")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise only the process topology (spawn, rendezvous, barrier, max over ranks) "
                          "with gloo on the CPU; prints one JSON line from rank 0")
@@ -504,12 +510,16 @@ def main():
         if args.serial_nms:
             with torch.cuda.stream(stream):
                 postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts)
-        else:
+        elif args.nms_event:
             fwd_done.record(stream)
             side.wait_event(fwd_done)
             with torch.cuda.stream(side):
                 postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts,
                                    filter_done=filt[k % 2])
+        else:  # filter in stream order behind the forward, sort / mask / reduce beside the next forward
+            with torch.cuda.stream(stream):
+                postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts,
+                                   filter_done=filt[k % 2], rest_stream=side)
         state["k"] = k + 1
 
     for _ in range(args.warmup):
@@ -566,6 +576,7 @@ def main():
             "parallel_chunks": plan.parallel_chunks,
             "graph": plan.graph_mode,
             "output_slots": slots,
+            "nms_streams": "serial" if args.serial_nms else ("event" if args.nms_event else "split"),
         },
         "roofline": {
             "kernel": "the forward conv stack (conv_ws / conv_ws1 / conv_r3h / conv_pwf / stem_rows / head_pred: every launch of one forward; HIP events on the plan stream around each graph replay)",

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 16
+#define YXH_ABI_VERSION 17
 
 enum yxh_status {
     YXH_OK = 0,
@@ -346,6 +346,16 @@ int yxh_postprocess_ev(float* pred, int32_t batch, int32_t anchors, int32_t num_
                        float conf_thre, double nms_thre, int32_t class_agnostic,
                        int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,
                        size_t workspace_bytes, void* filter_done, void* stream);
+/* The same, split over two streams (ABI 17): the count reset and the filter pass on `filter_stream`,
+ * `filter_done` (required) recorded there, then `rest_stream` waits on it and runs the sort, gather,
+ * mask and reduce passes.  A serving loop passes its forward's stream as `filter_stream`: the next
+ * batch's forward follows the filter in stream order (no cross-stream wait on its path) while the NMS
+ * proper runs beside it.  det / counts / workspace are complete once `rest_stream` reaches them. */
+int yxh_postprocess_split(float* pred, int32_t batch, int32_t anchors, int32_t num_classes,
+                          float conf_thre, double nms_thre, int32_t class_agnostic,
+                          int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,
+                          size_t workspace_bytes, void* filter_done, void* filter_stream,
+                          void* rest_stream);
 
 /*
  * yxh_yolox_loss: YoloxHead.get_losses (yolo_head.py:253-411) with SimOTA assignment

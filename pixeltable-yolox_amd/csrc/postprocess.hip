@@ -405,8 +405,13 @@ size_t pp_workspace(int B, int A) {
     return s;
 }
 
+// rest: the stream of the passes after the filter (sort, gather, mask, reduce); nullptr = st.  With a
+// separate rest stream, filter_done (required) is recorded on st after the filter and rest waits on it:
+// a serving loop keeps the filter in order behind its forward and runs the NMS proper beside the next one.
 int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
-                float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t filter_done) {
+                float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t filter_done,
+                hipStream_t rest) {
+    YXH_CHECK_ARG(!rest || rest == st || filter_done, "a separate rest stream needs the filter_done event");
     YXH_CHECK_ARG(pred && det && counts, "null pointer");
     YXH_CHECK_ARG(B > 0 && A >= 0 && C > 0, "postprocess shape B=%d A=%d C=%d", B, A, C);
     YXH_CHECK_ARG(ws && ws_bytes >= pp_workspace(B, A), "workspace too small (%zu < %zu)", ws_bytes,
@@ -435,13 +440,20 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     hipLaunchKernelGGL(pp_init, dim3(1), dim3(256), 0, st, B, w.cnt, counts);
     YXH_CHECK_LAUNCH("pp_init");
     int rc = YXH_OK;
-    if (A == 0) return filter_done ? check_hip(hipEventRecord(filter_done, st), "record filter_done") : YXH_OK;
-    hipLaunchKernelGGL(pp_filter, dim3((A + 63) / 64, B), dim3(256), lds, st, pred, A, C, conf, w);
-    YXH_CHECK_LAUNCH("pp_filter");
+    if (A > 0) {
+        hipLaunchKernelGGL(pp_filter, dim3((A + 63) / 64, B), dim3(256), lds, st, pred, A, C, conf, w);
+        YXH_CHECK_LAUNCH("pp_filter");
+    }
     if (filter_done) {  // pred is read and rewritten only by the filter
         rc = check_hip(hipEventRecord(filter_done, st), "record filter_done");
         if (rc) return rc;
     }
+    if (rest && rest != st) {  // counts (pp_init) and the filter's workspace rows are rest's inputs
+        rc = check_hip(hipStreamWaitEvent(rest, filter_done, 0), "rest stream wait");
+        if (rc) return rc;
+        st = rest;
+    }
+    if (A == 0) return YXH_OK;
     const int nch = (A + kSortCap - 1) / kSortCap;
     hipLaunchKernelGGL(pp_sort_chunk, dim3(nch, B), dim3(1024), 0, st, A, w);
     YXH_CHECK_LAUNCH("pp_sort_chunk");

@@ -73,7 +73,8 @@ int yolox_loss_bwd(const float* preds, const float* raw, const float* labels, in
                    const float* piou, const int* num_fg, const float* gtot, int use_l1, int dt, void* g_ro,
                    void* g_cls, hipStream_t st);
 int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
-                float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t filter_done);
+                float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t filter_done,
+                hipStream_t rest);
 int head_pred_launch(const yxh_head_desc* d, hipStream_t st);
 int stem_s2_launch(const yxh_stem2_desc* d, hipStream_t st);
 int augment_batch_launch(const uint8_t* pool, const yxh_aug_image* images, int B, int H, int W, uint8_t* mosaic_ws,
@@ -170,14 +171,24 @@ int yxh_postprocess(float* pred, int32_t batch, int32_t anchors, int32_t num_cla
                     double nms_thre, int32_t class_agnostic, int64_t vanilla_numel, float* det, int32_t* counts,
                     void* workspace, size_t workspace_bytes, void* stream) {
     return postprocess(pred, batch, anchors, num_classes, conf_thre, nms_thre, class_agnostic, vanilla_numel, det,
-                       counts, workspace, workspace_bytes, (hipStream_t)stream, nullptr);
+                       counts, workspace, workspace_bytes, (hipStream_t)stream, nullptr, nullptr);
 }
 
 int yxh_postprocess_ev(float* pred, int32_t batch, int32_t anchors, int32_t num_classes, float conf_thre,
                        double nms_thre, int32_t class_agnostic, int64_t vanilla_numel, float* det, int32_t* counts,
                        void* workspace, size_t workspace_bytes, void* filter_done, void* stream) {
     return postprocess(pred, batch, anchors, num_classes, conf_thre, nms_thre, class_agnostic, vanilla_numel, det,
-                       counts, workspace, workspace_bytes, (hipStream_t)stream, (hipEvent_t)filter_done);
+                       counts, workspace, workspace_bytes, (hipStream_t)stream, (hipEvent_t)filter_done, nullptr);
+}
+
+int yxh_postprocess_split(float* pred, int32_t batch, int32_t anchors, int32_t num_classes, float conf_thre,
+                          double nms_thre, int32_t class_agnostic, int64_t vanilla_numel, float* det, int32_t* counts,
+                          void* workspace, size_t workspace_bytes, void* filter_done, void* filter_stream,
+                          void* rest_stream) {
+    YXH_CHECK_ARG(filter_done, "yxh_postprocess_split: null filter_done event");
+    return postprocess(pred, batch, anchors, num_classes, conf_thre, nms_thre, class_agnostic, vanilla_numel, det,
+                       counts, workspace, workspace_bytes, (hipStream_t)filter_stream, (hipEvent_t)filter_done,
+                       (hipStream_t)rest_stream);
 }
 
 size_t yxh_yolox_loss_workspace_bytes(int32_t batch, int32_t anchors, int32_t max_labels) {

@@ -42,10 +42,10 @@ class _Workspace:
         self.buf.record_stream(stream)  # the allocator may recycle it only after this stream's use
         return self.buf
 
-    def release(self, device) -> None:
+    def release(self, device, stream: Optional[torch.cuda.Stream] = None) -> None:
         if self.done is None:
             self.done = torch.cuda.Event()
-        self.done.record(torch.cuda.current_stream(device))
+        self.done.record(stream if stream is not None else torch.cuda.current_stream(device))
 
 
 def _workspace(device, B: int, A: int) -> "_Workspace":
@@ -58,12 +58,15 @@ def _workspace(device, B: int, A: int) -> "_Workspace":
 def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: float = 0.7,
                        nms_thre: float = 0.45, class_agnostic: bool = False,
                        vanilla_numel: int = VANILLA_NUMEL_CPU, det: Optional[torch.Tensor] = None,
-                       counts: Optional[torch.Tensor] = None, filter_done: Optional[torch.cuda.Event] = None):
+                       counts: Optional[torch.Tensor] = None, filter_done: Optional[torch.cuda.Event] = None,
+                       rest_stream: Optional[torch.cuda.Stream] = None):
     """Asynchronous form: returns (det [B, A, 7], counts [B] int32) on the device,
     nothing synchronised, on the current stream.  ``prediction`` (fp32, on device) becomes xyxy
     in place.  ``filter_done`` is recorded once ``prediction`` is no longer read (after the
     filter pass): a producer that waits on it may overwrite ``prediction`` while the rest of
-    the NMS runs."""
+    the NMS runs.  ``rest_stream`` (needs ``filter_done``): only the filter runs on the current
+    stream; the sort / mask / reduce passes run on ``rest_stream`` after it (yxh_postprocess_split),
+    and det / counts are complete in that stream's order."""
     N.require_device(prediction, "prediction")
     if prediction.dtype != torch.float32 or not prediction.is_contiguous():
         raise ValueError("prediction must be a contiguous float32 [B, A, 5+C] tensor")
@@ -75,6 +78,8 @@ def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: fl
         det = torch.empty(B, max(A, 1), 7, dtype=torch.float32, device=dev)
     if counts is None:
         counts = torch.empty(B, dtype=torch.int32, device=dev)
+    if rest_stream is not None and filter_done is None:
+        raise ValueError("rest_stream needs a filter_done event")
     if filter_done is not None and not filter_done.cuda_event:
         filter_done.record()  # torch creates the event lazily, on its first record
     ws = _workspace(dev, B, A)
@@ -85,13 +90,20 @@ def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: fl
                 prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre),
                 int(bool(class_agnostic)), int(vanilla_numel), det.data_ptr(), counts.data_ptr(), buf.data_ptr(),
                 buf.numel(), N.stream_ptr(dev)), "postprocess")
-        else:
+        elif rest_stream is None:
             N.check(N.lib().yxh_postprocess_ev(
                 prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre),
                 int(bool(class_agnostic)), int(vanilla_numel), det.data_ptr(), counts.data_ptr(), buf.data_ptr(),
                 buf.numel(), filter_done.cuda_event, N.stream_ptr(dev)), "postprocess")
+        else:
+            for t in (buf, det, counts):  # written on rest_stream: the allocator must wait for it
+                t.record_stream(rest_stream)
+            N.check(N.lib().yxh_postprocess_split(
+                prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre),
+                int(bool(class_agnostic)), int(vanilla_numel), det.data_ptr(), counts.data_ptr(), buf.data_ptr(),
+                buf.numel(), filter_done.cuda_event, N.stream_ptr(dev), rest_stream.cuda_stream), "postprocess")
     finally:
-        ws.release(dev)
+        ws.release(dev, rest_stream)
     return det, counts
 
 

@@ -123,6 +123,35 @@ def test_filter_done_event_lets_the_producer_overwrite_pred(oracle):
             np.testing.assert_array_equal(det[b, :n[b]].cpu().numpy(), w)
 
 
+@pytest.mark.parametrize("empty", [False, True])
+def test_split_streams_filter_in_order_rest_beside(oracle, empty):
+    """yxh_postprocess_split (bench.py's default serving step): the count reset and the filter on
+    the producer's own stream, the sort / mask / reduce on a side stream after `filter_done`.  The
+    producer overwrites `pred` right behind the filter in stream order (no event wait) and the
+    results stay bit-exact vs the oracle; an all-filtered batch (A > 0, no candidates) too."""
+    from yolox_amd.utils.boxes import postprocess_device
+    pred = synthetic_pred(3, 2000, 80, 22, dense=True)
+    if empty:
+        pred[..., 4] = 0.0
+    p = torch.from_numpy(pred.copy()).cuda()
+    ev, side = torch.cuda.Event(), torch.cuda.Stream()
+    det, counts = postprocess_device(p, 80, 0.3, 0.65, filter_done=ev, rest_stream=side)
+    want_xyxy = p[..., :4].clone()  # stream order: after the filter's in-place write
+    p.fill_(-7.0)  # the next batch's forward, in order on the same stream
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    ref = pred.copy()
+    want = oracle.postprocess(ref, 80, 0.3, 0.65)
+    np.testing.assert_array_equal(want_xyxy.cpu().numpy(), ref[..., :4])
+    n = counts.cpu().tolist()
+    for b, w in enumerate(want):
+        assert n[b] == (0 if w is None else len(w))
+        if w is not None:
+            np.testing.assert_array_equal(det[b, :n[b]].cpu().numpy(), w)
+    with pytest.raises(ValueError):
+        postprocess_device(p, 80, 0.3, 0.65, rest_stream=side)  # the split form needs the event
+
+
 def test_single_class_many_overlaps(oracle):
     pred = synthetic_pred(2, 1024, 1, 5, dense=True)
     run_both(oracle, pred, 1, 0.0, 0.5)
