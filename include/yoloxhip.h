@@ -349,8 +349,10 @@ int yxh_postprocess_ev(float* pred, int32_t batch, int32_t anchors, int32_t num_
 /* The same, split over two streams (ABI 17): the count reset and the filter pass on `filter_stream`,
  * `filter_done` (required) recorded there, then `rest_stream` waits on it and runs the sort, gather,
  * mask and reduce passes.  A serving loop passes its forward's stream as `filter_stream`: the next
- * batch's forward follows the filter in stream order (no cross-stream wait on its path) while the NMS
- * proper runs beside it.  det / counts / workspace are complete once `rest_stream` reaches them. */
+ * batch's forward follows the filter in stream order while the NMS proper runs beside it.  det /
+ * counts / workspace are complete once `rest_stream` reaches them, so the caller must not hand the
+ * same workspace to the next batch's filter before then: the Python layer alternates two workspaces
+ * (yolox_amd/utils/boxes.py), so a filter waits only on the NMS of the batch two before it. */
 int yxh_postprocess_split(float* pred, int32_t batch, int32_t anchors, int32_t num_classes,
                           float conf_thre, double nms_thre, int32_t class_agnostic,
                           int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,

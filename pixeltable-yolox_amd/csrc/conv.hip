@@ -551,7 +551,8 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
                   "weight_frag: 16-bit, cout %% 16 == 0, cin %% 32 == 0, groups 1");
     p.wf = d->weight_frag;
     YXH_CHECK_ARG(d->grid_cap >= 0, "grid_cap %d", d->grid_cap);
-    p.cus = d->grid_cap > 0 && d->grid_cap < 256 ? d->grid_cap : 256;
+    const int cus = device_cus();
+    p.cus = d->grid_cap > 0 && d->grid_cap < cus ? d->grid_cap : cus;
     p.grp2 = grp2 ? 1 : 0;
     if (d->post_weight) {
         // a 1x1 post conv (or the head form: two groups, each with its own preds) runs on the

@@ -197,6 +197,8 @@ __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
     constexpr int WROWS = NF * 16;
     constexpr int WRB = CIN * 2 + 16;            // LDS weight row: +16 B (odd 16-B slots: conflict-free)
     constexpr int STGF = 16 * (5 + NCF * 16);    // per-wave staging floats (>= 16 rows of 5 + C)
+    // ~70 KB of LDS for CIN 128: one block per CU on gfx950 (160 KiB), built for that target only
+    static_assert(WROWS * WRB + WROWS * 4 + NW * STGF * 4 <= 160 * 1024, "head_pred2 LDS exceeds gfx950's 160 KiB");
     __shared__ __attribute__((aligned(16))) char wl[WROWS * WRB];
     __shared__ float bl[WROWS];
     __shared__ __attribute__((aligned(16))) float stg_all[NW][STGF];
@@ -335,7 +337,7 @@ int head_pred_launch(const yxh_head_desc* d, hipStream_t st) {
                         d->cls.bstride % 8 == 0;
     if (!v1 && rows16 && (d->cin == 64 || d->cin == 128)) {
         const long long groups = (M + 15) / 16;
-        const unsigned grid2 = (unsigned)std::min<long long>((groups + 7) / 8, 256);  // one 8-wave block per CU
+        const unsigned grid2 = (unsigned)std::min<long long>((groups + 7) / 8, device_cus());  // one 8-wave block per CU
 #define YXH_HEAD2(T, CIN) hipLaunchKernelGGL((head_pred2<T, CIN, 5>), dim3(grid2), dim3(512), 0, st, *d)
         if (d->dtype == YXH_BF16 && d->cin == 128) YXH_HEAD2(bf16, 128);
         else if (d->dtype == YXH_BF16) YXH_HEAD2(bf16, 64);

@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <vector>
 
 #include "yxh_common.hpp"
@@ -24,6 +25,18 @@ int check_hip(hipError_t e, const char* what) {
     if (e == hipSuccess) return YXH_OK;
     set_error("%s: %s", what, hipGetErrorString(e));
     return YXH_EHIP;
+}
+
+int device_cus() {
+    static std::atomic<int> cache[64];  // 0 = not queried yet
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    int n = cache[dev].load(std::memory_order_relaxed);
+    if (n == 0) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cache[dev].store(n, std::memory_order_relaxed);
+    }
+    return n;
 }
 
 int conv2d(const yxh_conv_desc* d, hipStream_t st);

@@ -227,7 +227,8 @@ class YoloxConfig:
     def preprocess(self, inputs, targets, tsize):
         """config.py:296-305: bilinear resize of the batch to ``tsize`` (align_corners False:
         yxh_resize_bilinear, one HIP launch, ATen's arithmetic) with the box columns scaled to
-        match (``scale_targets``)."""
+        match (``scale_targets``).  The batch must be on the ROCm device (the training loader
+        produces it there); a CPU batch raises ValueError rather than taking another resize."""
         from .utils.resize import resize_bilinear
         if self._multiscale(tsize) != (1, 1):
             inputs = resize_bilinear(inputs, tsize)

@@ -327,8 +327,11 @@ class TrainGraph:
 
     def _dw_wgrad(self, x: N.Src, dy: N.Src, C_: int, stride: int, out_h: int, out_w: int, batch: int,
                   dw: torch.Tensor) -> None:
-        """Depthwise weight gradient (yxh_dw_wgrad): written into the gradient buffer; its per-block
-        partials go to a workspace of the issuing stream."""
+        """Depthwise weight gradient (yxh_dw_wgrad): WRITTEN (not added) into the gradient buffer --
+        safe because one reverse pass replays one tape, in which each depthwise weight is used by
+        exactly one conv (GradBuffer.begin zeroes and publish adds what param.grad held, so torch's
+        accumulation over backward calls still holds); its per-block partials go to a workspace of
+        the issuing stream."""
         need = int(self.lib.yxh_dw_wgrad_workspace_bytes(batch, out_h, out_w, C_, 3))
         side = self._wside is not None and torch.cuda.current_stream(self.device) == self._wside
         name = "_dw_ws_side" if side else "_dw_ws"
@@ -479,6 +482,11 @@ class TrainGraph:
         dw = conv.groups != 1  # depthwise: groups == cin == cout, one un-upsampled source
         if dw and not (conv.groups == cin == cout and len(inputs) == 1 and inputs[0][1] == 0 and k == 3 and p == 1):
             raise NotImplementedError("grouped convs other than a 3x3 depthwise conv over one source")
+        if dw and (cout * self.esize) % 16:
+            # yxh_dw_dgrad reads dy as 16-byte pixel rows (train_dw.hip dw_dgrad_launch); the yolox_nano /
+            # yolox_tiny widths all meet this
+            raise NotImplementedError(f"depthwise conv training needs channels % {16 // self.esize} == 0 "
+                                      f"(16-byte gradient rows), got {cout}")
         w, _ = self._fwd_weight(conv, 1 if dw else cin)
         srcs = [a.src(up) for a, up in inputs]
         y = torch.empty(B, oh, ow, cout, dtype=self.dtype, device=self.device)
@@ -964,13 +972,21 @@ class _BlockFn(torch.autograd.Function):
     def forward(ctx, anchor, x, graph, run):
         outs, acts, in_act = run()
         ctx.graph, ctx.acts, ctx.in_act, ctx.x_dtype = graph, acts, in_act, x.dtype
+        # this call's tape and the tensors it reads belong to this autograd node: a block called
+        # again before backward (a shared module on two inputs) records a tape of its own
+        ctx.tape, ctx.keep = graph.tape, graph._keep
+        graph.tape, graph._keep = [], None
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *gouts):
+        if ctx.tape is None:
+            raise RuntimeError("block backward called twice on one forward (retain_graph is not supported)")
         for a, go in zip(ctx.acts, gouts):
             if go is not None:
                 a.grad = go.permute(0, 2, 3, 1).to(torch.float32).contiguous()
+        ctx.graph.tape, ctx.graph._keep = ctx.tape, ctx.keep
+        ctx.tape = ctx.keep = None
         ctx.graph.backward(None)
         a = ctx.in_act
         gx = None

@@ -21,13 +21,18 @@ VANILLA_NUMEL_CPU = 4000   # the reference CPU path (parity target)
 VANILLA_NUMEL_CUDA = 20000
 
 _workspaces: dict = {}
+_split_next: dict = {}  # device -> the split path's next workspace slot (1 or 2)
 
 
 class _Workspace:
-    """One yxh_postprocess scratch buffer per device, shared by every stream: each call
-    waits for the previous call's completion event (on whatever stream that ran) and
-    records its own, so calls on different streams never overlap on it, and a caller that
-    makes a new stream per request reuses the same buffer instead of leaking one each."""
+    """One yxh_postprocess scratch buffer per (device, slot), shared by every stream: each
+    call waits for the previous call's completion event on that slot (on whatever stream that
+    ran) and records its own, so calls on different streams never overlap on it, and a caller
+    that makes a new stream per request reuses the same buffer instead of leaking one each.
+
+    The split path (filter on the forward stream, the rest on ``rest_stream``) alternates two
+    slots: batch k+1's filter reuses the buffer of batch k-1, whose sort / mask / reduce finished
+    long before, so the forward stream never waits on the NMS of the batch just before it."""
 
     def __init__(self):
         self.buf: Optional[torch.Tensor] = None
@@ -48,9 +53,14 @@ class _Workspace:
         self.done.record(stream if stream is not None else torch.cuda.current_stream(device))
 
 
-def _workspace(device, B: int, A: int) -> "_Workspace":
+def _workspace(device, B: int, A: int, split: bool = False) -> "_Workspace":
     need = int(N.lib().yxh_postprocess_workspace_bytes(B, A))
-    ws = _workspaces.setdefault(torch.device(device), _Workspace())
+    dev = torch.device(device)
+    slot = 0
+    if split:
+        slot = _split_next.get(dev, 1)
+        _split_next[dev] = 3 - slot
+    ws = _workspaces.setdefault((dev, slot), _Workspace())
     ws.acquire(device, need)
     return ws
 
@@ -82,7 +92,7 @@ def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: fl
         raise ValueError("rest_stream needs a filter_done event")
     if filter_done is not None and not filter_done.cuda_event:
         filter_done.record()  # torch creates the event lazily, on its first record
-    ws = _workspace(dev, B, A)
+    ws = _workspace(dev, B, A, split=rest_stream is not None)
     buf = ws.buf
     try:
         if filter_done is None:

@@ -3,7 +3,12 @@
 YoloxConfig.preprocess (reference config.py:296-305) resizes every non-``input_size`` training
 iteration with ``F.interpolate(inputs, size=tsize, mode="bilinear", align_corners=False)``; here the
 same arithmetic runs as one HIP launch over the [B, C, H, W] batch (bit-identical to ATen's bilinear
-kernel on the same device: tests/test_gpu_augment.py).  ROCm tensors only -- there is no CPU path.
+kernel on the same device: tests/test_gpu_augment.py).  ROCm tensors only -- there is no CPU path:
+a CPU batch raises (``N.require_device``) instead of silently taking another kernel.
+
+Layout: the kernel reads contiguous NCHW.  A channels_last batch is made NCHW-contiguous first and
+the result is NCHW-contiguous; bit-identity is pinned against ATen's NCHW bilinear kernel only (ATen
+runs a separate NHWC kernel for channels_last input, which this module does not claim to match).
 """
 from __future__ import annotations
 

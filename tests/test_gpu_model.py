@@ -397,6 +397,53 @@ def test_building_blocks_train_mode(golden, oracle, key):
             assert (buf.cpu() - want).abs().max().item() <= 1e-5 * (want.abs().max().item() + 1.0), name
 
 
+@pytest.mark.parametrize("key", ["conv3s1", "bottleneck", "csp_short"])
+def test_building_block_called_twice_before_backward(golden, oracle, key):
+    """A shared train-mode block applied to two inputs whose losses are summed (y1 = m(x1);
+    y2 = m(x2); (y1 r1 + y2 r2).sum().backward(), as the reference's eager modules allow): each
+    call keeps its own tape, so both inputs get their gradients and the parameter gradients are
+    the sum over the two calls -- vs the oracle's autograd of the same two calls (1e-3)."""
+    from yolox_amd.models import network
+    d = golden("blocks.npz")
+    cls, args, kw = BLOCK_CASES[key]
+    m = getattr(network, cls)(*args, **kw)
+    pre = f"{key}.p."
+    sd0 = {k[len(pre):]: torch.from_numpy(v) for k, v in d.items() if k.startswith(pre)}
+    m.load_state_dict(sd0)
+    for b in m.modules():
+        if isinstance(b, torch.nn.BatchNorm2d):
+            b.eps, b.momentum = 1e-3, 0.03
+    m = m.cuda().train()
+    x0 = torch.from_numpy(d[f"{key}.x"])
+    g = torch.Generator().manual_seed(12)
+    x1 = x0.cuda().requires_grad_(True)
+    x2 = (x0.flip(0) * 0.5 + 0.25 * torch.randn(tuple(x0.shape), generator=g)).cuda().requires_grad_(True)
+    y1 = m(x1)
+    y2 = m(x2)
+    r1 = torch.randn(tuple(y1.shape), generator=g)
+    r2 = torch.randn(tuple(y2.shape), generator=g)
+    ((y1 * r1.cuda()).sum() + (y2 * r2.cuda()).sum()).backward()
+    torch.cuda.synchronize()
+    sdo = {f"b.{k}": v.clone().float().requires_grad_(v.is_floating_point() and "running" not in k
+                                                      and "num_batches" not in k) for k, v in sd0.items()}
+    xo1 = x1.detach().cpu().clone().requires_grad_(True)
+    xo2 = x2.detach().cpu().clone().requires_grad_(True)
+    yo1 = _oracle_block(oracle, cls, args, kw, sdo, xo1)
+    yo2 = _oracle_block(oracle, cls, args, kw, sdo, xo2)
+    ((yo1 * r1).sum() + (yo2 * r2).sum()).backward()
+    for y, yo in ((y1, yo1), (y2, yo2)):
+        assert (y.detach().cpu() - yo.detach()).abs().max().item() <= 1e-4 * yo.abs().max().item()
+    for x, xo in ((x1, xo1), (x2, xo2)):
+        assert x.grad is not None
+        assert (x.grad.cpu() - xo.grad).abs().max().item() <= 1e-3 * xo.grad.abs().max().item()
+    for name, prm in m.named_parameters():
+        gr = sdo[f"b.{name}"].grad
+        assert (prm.grad.cpu() - gr).abs().max().item() <= 1e-3 * (gr.abs().max().item() + 1e-12), name
+    for name, buf in m.named_buffers():
+        if name.endswith("num_batches_tracked"):
+            assert int(buf) == int(sd0[name]) + 2, name
+
+
 def test_cspdarknet_out_features_and_train_mode(golden):
     """CspDarknet with the reference's other out_features (darknet.py:165-177: "stem", "dark2"):
     eval -- a block plan that keeps the stem map (the fused stem launch is planned out), the shared

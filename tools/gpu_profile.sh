@@ -2,7 +2,8 @@
 # GPU box: evidence for one bench configuration -- bench (+ per-layer table, tune file), rocprofv3
 # kernel trace + stats of the same bench, PMC HBM traffic (FETCH_SIZE / WRITE_SIZE in separate
 # passes, MI355X_MICROARCH.md HBM section) and an SQ / GRBM pass for MFMA utilisation per kernel.
-# Usage: bash tools/gpu_profile.sh TAG [bench args...]   (e.g. --model yolox_l --batch 16 --dtype fp16)
+# Usage: [TRAFFIC_ARGS='yolox_l 16 640 fp16'] bash tools/gpu_profile.sh TAG [bench args...]
+#        (e.g. --model yolox_l --batch 16 --dtype fp16; TRAFFIC_ARGS names the workload in the traffic JSON)
 set -o pipefail
 TAG=${1:-run}
 shift
@@ -30,6 +31,10 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
     -d gpurun_out/pmc_${TAG}_SQ2 -o run --output-format csv \
     -- python bench.py $ARGS --steps 4 --warmup 1 --no-cpu-baseline --tune-file $TUNE \
     > gpurun_out/pmc_${TAG}_SQ2.log 2>&1 || exit 1
+python tools/forward_timeline.py gpurun_out/prof_$TAG/run_kernel_trace.csv > gpurun_out/timeline_$TAG.txt || exit 1
+# HBM bytes of exactly the 4 timed forwards of the PMC passes, launch list reconciled with the trace
+python tools/traffic.py gpurun_out/pmc_$TAG gpurun_out/traffic_$TAG.json --replays 4 \
+    --timeline gpurun_out/timeline_$TAG.txt $TRAFFIC_ARGS || exit 1
 python tools/mfma_util.py gpurun_out/pmc_${TAG}_SQ/run_counter_collection.csv --last 3 \
     --stalls gpurun_out/pmc_${TAG}_SQ2/run_counter_collection.csv --json gpurun_out/mfma_util_$TAG.json \
     > gpurun_out/mfma_util_$TAG.txt || exit 1
