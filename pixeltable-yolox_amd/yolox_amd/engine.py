@@ -913,17 +913,27 @@ class Plan:
         stream = N.stream_ptr(self.device)
         dt = self.ctx.dcode
         keep = []
+        # a 16-bit YoloxModule folds from the float32 values it had before its cast (models/yolox.py
+        # fp32_master): the packed weights are then rounded once, like the oracle's bf16 emulation; a
+        # submodule of a YoloxModule planned on its own (module.backbone(x), a block) holds the
+        # module's masters as _fold_masters
+        from .models.yolox import fold_master
+        masters = self._model.__dict__.get("_masters") or self._model.__dict__.get("_fold_masters") or {}
+
+        def f32(t):
+            m = fold_master(masters, t)
+            return (m if m is not None else t.detach()).to(self.device, torch.float32).contiguous()
+
         for s in self.ctx.weights:
             row = 0
             for conv, bn in s.convs:
-                w = conv.weight.detach().to(self.device, torch.float32).contiguous()
+                w = f32(conv.weight)
                 keep.append(w)
                 args = [None, None, None, None, None]
                 if conv.bias is not None:
-                    args[0] = conv.bias.detach().to(self.device, torch.float32).contiguous()
+                    args[0] = f32(conv.bias)
                 if bn is not None:
-                    args[1:] = [t.detach().to(self.device, torch.float32).contiguous()
-                                for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)]
+                    args[1:] = [f32(t) for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)]
                 keep.extend(a for a in args if a is not None)
                 eps = float(bn.eps) if bn is not None else 0.0
                 ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731

@@ -29,6 +29,15 @@ from .processor import Detections, YoloxProcessor
 HOME = Path(os.environ.get("YOLOX_HOME", str(Path.home() / ".cache" / "yolox")))
 
 
+def fold_master(masters: dict, t: torch.Tensor) -> Optional[torch.Tensor]:
+    """The float32 fold master of parameter / buffer ``t`` in a YoloxModule's ``masters`` (see
+    YoloxModule._record_masters), or None when it has none or ``t`` changed since its cast."""
+    m = masters.get(id(t))
+    if m is None or m[2] != t.data_ptr() or m[3] != t._version:
+        return None
+    return m[1]
+
+
 def default_device() -> str:
     return "cuda" if torch.cuda.is_available() else "cpu"
 
@@ -40,6 +49,13 @@ class YoloxModule(nn.Module):
         self.head = head if head is not None else YoloxHead(80)
         self._plans: dict = {}
         self._weights_epoch = 0  # advanced on every weight change the captured plans must see
+        # fp32 fold masters (below): one dict for the module's life, mutated in place, which every
+        # submodule also holds -- a submodule planned on its own (module.backbone(x), a block) folds
+        # from it too
+        self.__dict__["_masters"] = {}
+        for m in self.modules():
+            if m is not self:
+                m.__dict__["_fold_masters"] = self._masters
 
     def weights_changed(self) -> None:
         """Tell captured plans (engine.Plan.replay) that parameters or BN statistics were
@@ -48,8 +64,47 @@ class YoloxModule(nn.Module):
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         r = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        # a float32 state dict loaded into a 16-bit module: keep its values as the fold masters
+        self._record_masters({k: v for k, v in state_dict.items()
+                              if torch.is_tensor(v) and v.dtype == torch.float32})
         self.weights_changed()
         return r
+
+    # ---------------------------------------------------------------- fp32 fold masters
+    # Perf mode (``.to(torch.bfloat16)`` / ``.half()``) rounds every parameter AND the BatchNorm
+    # statistics to 16 bits.  Folding BN into the conv weights from those rounded values
+    # (w16 * g16 / sqrt(var16 + eps), beta16 - mean16 * ...) rounds each weight twice and shifts
+    # every channel's bias by up to half a 16-bit ulp of beta and mean -- an offset shared by all
+    # pixels of the channel, which the next layers do not average out.  Measured on the 32
+    # configs[1] images (tools/map_noise.py, profiles/r06/map_noise.txt): the oracle with
+    # bf16-rounded parameters + bf16 storage is 1.56x further from the fp32 oracle at p99 than
+    # with fp32 parameters -- the device's whole round-5 excess.  So the module keeps the float32
+    # values it had before the cast (on the module's device), and the plans fold from them: the
+    # packed weights are rounded once.  A master is used only while its 16-bit parameter is the
+    # tensor (storage and version) the cast produced; any later edit of that parameter makes the
+    # plan fold from the edited 16-bit value.
+    def _float_tensors(self):
+        for n, t in self.named_parameters():
+            if t.is_floating_point():
+                yield n, t
+        for n, t in self.named_buffers():
+            if t.is_floating_point():
+                yield n, t
+
+    def _record_masters(self, sources: dict) -> None:
+        """sources: name -> float32 value of that parameter / buffer before its 16-bit cast."""
+        masters = self._masters
+        for n, t in self._float_tensors():
+            src = sources.get(n)
+            if t.dtype in (torch.bfloat16, torch.float16) and src is not None and tuple(src.shape) == tuple(t.shape):
+                masters[id(t)] = (n, src.detach().to(t.device, torch.float32).contiguous(), t.data_ptr(), t._version)
+            elif id(t) in masters and t.dtype == torch.float32:
+                del masters[id(t)]
+
+    def fp32_master(self, t: torch.Tensor) -> Optional[torch.Tensor]:
+        """The float32 value ``t`` (a parameter or BN buffer of this module) had before its
+        16-bit cast, if ``t`` is unchanged since; else None."""
+        return fold_master(self._masters, t)
 
     # ---------------------------------------------------------------- execution
     @property
@@ -113,7 +168,18 @@ class YoloxModule(nn.Module):
 
     def _apply(self, fn, *args, **kwargs):
         self._plans = {}  # device / dtype changes invalidate every plan
-        return super()._apply(fn, *args, **kwargs)
+        # float32 values before the cast (or the masters of a 16-bit module being moved): the
+        # fold masters of the 16-bit result (see _record_masters)
+        before = {}
+        for n, t in self._float_tensors():
+            if t.dtype == torch.float32:
+                before[n] = t.data
+            elif self.fp32_master(t) is not None:
+                before[n] = self.fp32_master(t)
+        r = super()._apply(fn, *args, **kwargs)
+        self._masters.clear()
+        self._record_masters(before)
+        return r
 
     # ---------------------------------------------------------------- loading
     @classmethod

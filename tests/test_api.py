@@ -190,3 +190,33 @@ def test_synthetic_weights_are_deterministic():
     for k in shapes:
         assert torch.equal(a[k], b[k])
     assert not torch.equal(a["a.conv.weight"], synthetic_state_dict(shapes, seed=2)["a.conv.weight"])
+
+
+def test_fp32_fold_masters_survive_the_16bit_cast():
+    """Perf mode (.to(bfloat16)) keeps each parameter's / BN statistic's float32 value as the fold
+    master (models/yolox.py: the plan folds BN from it, so packed weights are rounded once); a moved
+    module keeps them, an edited parameter or a float32 module has none, and a float32 state dict
+    loaded into a 16-bit module becomes the masters."""
+    from yolox_amd.config import named_config
+    from yolox_amd.weights import synthetic_state_dict
+    m = named_config("yolox_nano").get_model()
+    sd = synthetic_state_dict(m.state_dict(), seed=0, bn_stats="yolox_nano")
+    m.load_state_dict(sd)
+    conv, bn = m.backbone.backbone.stem.conv.conv, m.backbone.backbone.stem.conv.bn
+    assert m.fp32_master(conv.weight) is None  # float32 module: folds from the parameters themselves
+    m = m.to(torch.bfloat16)
+    assert conv.weight.dtype == torch.bfloat16
+    for t, k in ((conv.weight, "backbone.backbone.stem.conv.conv.weight"),
+                 (bn.running_var, "backbone.backbone.stem.conv.bn.running_var"),
+                 (bn.bias, "backbone.backbone.stem.conv.bn.bias")):
+        assert torch.equal(m.fp32_master(t), sd[k].float()), k
+    m = m.to(torch.float16)  # 16 -> 16 bit: the float32 masters carry over
+    assert torch.equal(m.fp32_master(conv.weight), sd["backbone.backbone.stem.conv.conv.weight"])
+    with torch.no_grad():
+        conv.weight.mul_(2)  # an edit: the plan must fold from the edited value
+    assert m.fp32_master(conv.weight) is None
+    assert m.fp32_master(bn.weight) is not None
+    m.load_state_dict(sd)  # float32 values into the 16-bit module: masters again
+    assert torch.equal(m.fp32_master(conv.weight), sd["backbone.backbone.stem.conv.conv.weight"])
+    m = m.float()
+    assert m.fp32_master(conv.weight) is None

@@ -150,8 +150,12 @@ def map_parity(host, ref, emu, dev_dets, size, tag):
     synthetic nets: a box the device keeps is the oracle's box to IoU > 0.95; what costs AP is
     detections whose confidence sits at the 0.5 threshold or whose NMS partner flips (the ~150
     detections per image of a random-weight net crowd the threshold far more than a trained
-    net's).  Measured on MI355X (round 5, printed with -s): configs[1] bf16 device 0.867 vs the
-    bf16-storage emulation 0.951 (2.7x its loss); see MAP_FLOOR.  Returns the numbers."""
+    net's).  The AP of a faithful 16-bit implementation depends on its summation order: oracle
+    emulations that differ only in that score 0.909-0.951 on configs[1] (tools/map_noise.py,
+    profiles/r06/map_noise.txt).  Measured on MI355X (round 6, printed with -s): configs[1] bf16
+    device 0.917 vs the emulation's 0.951, configs[3] fp16 0.964 vs 0.974.  (Round 5's 0.867 came
+    from folding BatchNorm from bf16-rounded parameters, fixed by the fp32 fold masters,
+    models/yolox.py.)  Returns the numbers."""
     from oracle import reference_cpu as O
     ref_dets = O.postprocess(ref.copy(), 80, 0.5, 0.65)
     emu_dets = O.postprocess(emu.copy(), 80, 0.5, 0.65)
@@ -168,9 +172,13 @@ def map_parity(host, ref, emu, dev_dets, size, tag):
 
 
 # absolute floors (AP50:95, AP50) of the device detections vs the fp32 oracle's, and the factor on
-# the 16-bit-storage emulation's AP loss (measured round 5: configs[1] 0.867 / 2.7x)
-MAP_FLOOR = {"configs1": (0.85, 0.85), "configs3": (0.85, 0.85)}
-MAP_FACTOR = 3.0
+# the 16-bit-storage emulation's AP loss (measured round 6: configs[1] 0.917 = 1.7x, configs[3] 0.964 = 1.4x;
+# emulations differing only in summation order: 0.909-0.951 = up to 1.9x, tools/map_noise.py)
+MAP_FLOOR = {"configs1": (0.90, 0.90), "configs3": (0.93, 0.93)}
+MAP_FACTOR = 2.0
+# the device's probability / box-centre distance from the fp32 oracle over the emulation's (measured
+# round 6 with the fp32 fold masters: max 1.06x, p99 1.00x on configs[1]; 0.95x / 0.99x on configs[3])
+DERIVED_FACTOR = 1.25
 
 
 def test_configs1_yolox_s_640_bf16_batch32(oracle):
@@ -183,12 +191,13 @@ def test_configs1_yolox_s_640_bf16_batch32(oracle):
     host = out.cpu().numpy()
     # all 32 images.  The factor covers the summation order: the device's fp32 accumulations
     # run in another order than the oracle's, which flips the bf16 rounding of values near a
-    # rounding boundary in every stored map, and the flips compound over ~60 layers.  Measured
-    # on MI355X (round 4, stats printed with -s): max 1.68x, p99 1.56x the storage-only distance
+    # rounding boundary in every stored map.  Measured on MI355X (round 6, stats printed with -s):
+    # max 1.06x, p99 1.00x the storage-only distance (round 5: 1.68x / 1.56x -- BN folded from
+    # bf16-rounded parameters, see YoloxModule.fp32_master)
     ref = oracle_forward(oracle, "yolox_s", imgs)
     emu = oracle_forward(oracle, "yolox_s", imgs, torch.bfloat16)
     print("configs1 bf16 vs fp32 oracle (dev max, emu max, dev p99, emu p99):",
-          derived_bounds_hold(host, ref, emu, 2.0))
+          derived_bounds_hold(host, ref, emu, DERIVED_FACTOR))
     # device NMS (bench step: conf 0.5, nms 0.65) on the replayed output == oracle NMS
     pred = out.clone()
     det, counts = postprocess_device(pred, 80, 0.5, 0.65)
@@ -274,7 +283,7 @@ def test_configs3_yolox_l_640_fp16_batch16(oracle):
     ref = oracle_forward(oracle, "yolox_l", imgs)
     emu = oracle_forward(oracle, "yolox_l", imgs, torch.float16)
     print("configs3 fp16 vs fp32 oracle (dev max, emu max, dev p99, emu p99):",
-          derived_bounds_hold(host, ref, emu, 2.0))
+          derived_bounds_hold(host, ref, emu, DERIVED_FACTOR))
     # device NMS (processor defaults conf 0.5, nms 0.65) on the replayed fp16-plan output
     pred = out.clone()
     det, counts = postprocess_device(pred, 80, 0.5, 0.65)

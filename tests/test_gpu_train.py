@@ -796,44 +796,47 @@ def test_train_step_other_widths_match_oracle(oracle, name):
     assert all(torch.isfinite(prm.grad).all() for prm in m.parameters())
 
 
-def test_train_step_bf16_autocast_close_to_fp32(monkeypatch):
-    """bf16 compute (autocast, as --fp16 training does with fp16) gives gradients
-    aligned with the fp32 ones (cosine per tensor with > 1k elements: min > 0.95,
-    mean > 0.99) when both precisions make the same SimOTA assignment.
-
-    The assignment is discrete (dynamic-k top-k over costs): a bf16 rounding can move
-    one anchor across a level, which zeroes a whole per-level cls branch gradient in
-    one run and not the other.  Tile tuning is off here (by-shape tiles, deterministic
-    accumulation order), and when the foreground anchors differ (count or placement) the check
-    falls back to the tensors both runs update (mean cosine > 0.9)."""
+def test_train_step_bf16_autocast_close_to_fp32(oracle, monkeypatch):
+    """bf16 compute (autocast, as --fp16 training does with fp16) against the oracle's fp32 autograd
+    within bounds DERIVED from the oracle run with bf16 storage (oracle.stored_as(bfloat16) in train
+    mode), as configs[4]'s fp16 test does: each loss and every parameter gradient with > 1k elements
+    may be off the fp32 oracle by at most FACTOR x the emulation's own distance (+ 1e-3 of the
+    tensor's max).  Both oracle runs take the device's SimOTA assignment (routed: the matching is
+    discrete, so a bf16 rounding that moves one anchor across a level would otherwise swap whole
+    loss terms); the oracle's own assignment may differ on at most 5 % of the fg anchors.  Tile
+    tuning is off (by-shape tiles)."""
     import yolox_amd.train as T
+    from test_gpu_configs import _device_train_step, _f, _oracle_train_step
     monkeypatch.setenv("YOLOX_AMD_TRAIN_TUNE", "0")
     monkeypatch.setattr(T, "_TRAIN_TILES", {})
+    FACTOR = 3.0
     m, sd, x, labels, _ = _model_and_batch()
     m = m.cuda().train()
-    out32 = m(x.cuda(), labels.cuda())
-    out32["total_loss"].backward()
-    g32 = {n: p.grad.clone() for n, p in m.named_parameters()}
-    fg32 = m._train_graph.assign["fg_mask"].bool().clone()
-    m.load_state_dict(sd)
-    m.zero_grad(set_to_none=True)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
-        out16 = m(x.cuda(), labels.cuda())
-    out16["total_loss"].backward()
-    torch.cuda.synchronize()
-    fg16 = m._train_graph.assign["fg_mask"].bool()
-    assert abs(float(out16["total_loss"]) - float(out32["total_loss"])) < 0.05 * float(out32["total_loss"])
-    cos = {n: float(F.cosine_similarity(p.grad.flatten(), g32[n].flatten(), dim=0))
-           for n, p in m.named_parameters() if p.numel() > 1000}
-    # different assignment: the same foreground COUNT can still put an anchor on another level
-    if float(out16["num_fg"]) != float(out32["num_fg"]) or not torch.equal(fg16, fg32):
-        both = [c for n, c in cos.items()
-                if float(dict(m.named_parameters())[n].grad.abs().max()) > 0 and float(g32[n].abs().max()) > 0]
-        assert np.mean(both) > 0.9, np.mean(both)
-        return
-    # bf16 activations / conv-output gradients (8 mantissa bits) through ~80 layers
-    assert min(cos.values()) > 0.95, min(cos.items(), key=lambda kv: kv[1])
-    assert np.mean(list(cos.values())) > 0.99, np.mean(list(cos.values()))
+    out16, spp_in = _device_train_step(monkeypatch, m, x, labels, torch.bfloat16)
+    assign = {k: v.clone() for k, v in m._train_graph.assign.items()}
+    grads = {n: p.grad.cpu().float().clone() for n, p in m.named_parameters() if p.numel() > 1000}
+    flips = []
+    ref, sdo = _oracle_train_step(oracle, monkeypatch, m, "yolox_s", x, labels, spp_in, assign, flips)
+    nfg = int(assign["fg_mask"].bool().sum())
+    assert nfg > 0 and sum(flips) <= max(2, 0.05 * nfg), (flips, nfg)
+    with oracle.stored_as(torch.bfloat16):
+        emu, sde = _oracle_train_step(oracle, monkeypatch, m, "yolox_s", x, labels, spp_in, assign)
+    stats = {}
+    for k in ("total_loss", "iou_loss", "conf_loss", "cls_loss"):
+        r = _f(ref[k])
+        d_dev, d_emu = abs(float(out16[k]) - r), abs(_f(emu[k]) - r)
+        stats[k] = (d_dev / abs(r), d_emu / abs(r))
+        assert d_dev <= FACTOR * d_emu + 1e-3 * abs(r), (k, stats[k])
+    for name, g in grads.items():
+        gr = sdo[name].grad
+        scale = float(gr.abs().max()) + 1e-12
+        d_dev = float((g - gr).abs().max()) / scale
+        d_emu = float((sde[name].grad - gr).abs().max()) / scale
+        stats[name] = (d_dev, d_emu)
+        assert d_dev <= FACTOR * d_emu + 1e-3, (name, stats[name])
+    worst = max((v[0] / (v[1] + 1e-3), k) for k, v in stats.items())
+    print(f"bf16 step (dev, emulation) distances from the fp32 oracle, worst ratio {worst}; "
+          f"SimOTA routed from the device, the oracle's own assignment differs on {flips} of {nfg}")
 
 
 def test_sgd_step_changes_eval_plan():
