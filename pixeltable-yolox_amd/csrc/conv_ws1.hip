@@ -183,9 +183,9 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
         for (int s = 0; s < WCB; ++s) {
             if (s + PD < WCB) load_b(s + PD, bf[(s + PD) % (PD + 1)]);
 #pragma unroll
-            for (int i = 0; i < FR; ++i)
+            for (int j = 0; j < FC; ++j)  // pixel-fragment-major (conv_ws.hip): more cover for the next reads
 #pragma unroll
-                for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], a[i][s], bf[s % (PD + 1)][j]);
+                for (int i = 0; i < FR; ++i) Mma<T>::run(acc[i][j], a[i][s], bf[s % (PD + 1)][j]);
             if constexpr (EPI)
                 if (s < NP) epi_piece(tprev, accp, s / FR, s % FR);
             if (s + PD < WCB) __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);
