@@ -9,7 +9,9 @@ processor defaults (conf 0.5, nms 0.65); the NMS filter pass (the one reader of 
 output) runs in stream order behind its forward and the rest of that batch's NMS on a side stream
 beside the next batch's forward (yxh_postprocess_split; --nms-event: the whole NMS on the side
 stream, the next forward waiting on the filter's event) -- --serial-nms runs them back to back on
-one stream.  Inputs are resident in HBM (uint8 NHWC, as the
+one stream.  The filter reads the per-anchor score records the head launches write beside the rows
+(16 bytes per anchor instead of 340; yxh_postprocess_scored, identical detections; --no-scores: the
+rows' class columns).  Inputs are resident in HBM (uint8 NHWC, as the
 processor's letterbox hands them to the forward) before the timed region.  With --gpus N (torchrun, one process per GPU) each rank
 runs an independent replica -- inference has no exchange step, so there is no
 collective in the data path -- and value = all images / max
@@ -101,6 +103,9 @@ def parse():
                     help="the whole NMS on the side stream, the next forward waiting on its filter event across "
                          "streams (round 4-5 form; default: the filter in order behind the forward on its stream, "
                          "the rest of the NMS on the side stream, yxh_postprocess_split)")
+    ap.add_argument("--no-scores", action="store_true",
+                    help="the NMS filter reads the rows' class columns (default: the per-anchor score records the head "
+                         "launches write beside the rows, Plan.enable_scores / yxh_postprocess_scored)")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise only the process topology (spawn, rendezvous, barrier, max over ranks) "
                          "with gloo on the CPU; prints one JSON line from rank 0")
@@ -333,8 +338,9 @@ def main_train(args, world, rank):
 
     for _ in range(args.warmup):
         out = step()
-    # one process, YOLOX_AMD_TRAIN_GRAPH=1: the forward + reverse pass replays as hipGraph segments
-    if world == 1 and args.warmup >= 1 and os.environ.get("YOLOX_AMD_TRAIN_GRAPH", "0") == "1":
+    # YOLOX_AMD_TRAIN_GRAPH=1: the forward + reverse pass replays as hipGraph segments (under DDP the
+    # reducer's bucket all-reduces are issued between the replayed segments, CapturedTrainStep)
+    if args.warmup >= 1 and os.environ.get("YOLOX_AMD_TRAIN_GRAPH", "0") == "1":
         from yolox_amd.train import CapturedTrainStep
         opt.zero_grad(set_to_none=True)
         cap = CapturedTrainStep(model, imgs, labels, dtype=amp or torch.float32,
@@ -482,6 +488,9 @@ def main():
     # the NMS kernels then run beside the next forward's stem and stretch it more than the wait
     # costs.  --serial-nms puts the NMS back behind each forward on one stream.
     slots = 2 if args.two_slot and not args.serial_nms else 1
+    # the head launches also write 16-byte score records per anchor, which the NMS filter reads
+    # instead of the 85 fp32 columns of every row (identical detections; tests/test_gpu_postprocess.py)
+    scores = None if args.no_scores or slots == 2 else plan.enable_scores()
     plan.capture(slots)
     A = plan.anchors
     # --fwd-priority: the forward on a high-priority stream, so the NMS kernels of the previous batch
@@ -509,17 +518,18 @@ def main():
         det, counts = dets[k % 2], cnts[k % 2]
         if args.serial_nms:
             with torch.cuda.stream(stream):
-                postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts)
+                postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts,
+                                   scores=scores)
         elif args.nms_event:
             fwd_done.record(stream)
             side.wait_event(fwd_done)
             with torch.cuda.stream(side):
                 postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts,
-                                   filter_done=filt[k % 2])
+                                   filter_done=filt[k % 2], scores=scores)
         else:  # filter in stream order behind the forward, sort / mask / reduce beside the next forward
             with torch.cuda.stream(stream):
                 postprocess_device(out, model.head.num_classes, args.conf, args.nms, det=det, counts=counts,
-                                   filter_done=filt[k % 2], rest_stream=side)
+                                   filter_done=filt[k % 2], rest_stream=side, scores=scores)
         state["k"] = k + 1
 
     for _ in range(args.warmup):
@@ -577,6 +587,7 @@ def main():
             "graph": plan.graph_mode,
             "output_slots": slots,
             "nms_streams": "serial" if args.serial_nms else ("event" if args.nms_event else "split"),
+            "nms_filter": "score records" if scores is not None else "rows",
         },
         "roofline": {
             "kernel": "the forward conv stack (conv_ws / conv_ws1 / conv_r3h / conv_pwf / stem_rows / head_pred: every launch of one forward; HIP events on the plan stream around each graph replay)",

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YXH_ABI_VERSION 17
+#define YXH_ABI_VERSION 18
 
 enum yxh_status {
     YXH_OK = 0,
@@ -358,6 +358,16 @@ int yxh_postprocess_split(float* pred, int32_t batch, int32_t anchors, int32_t n
                           int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,
                           size_t workspace_bytes, void* filter_done, void* filter_stream,
                           void* rest_stream);
+/* The same passes with the filter fed by the forward's per-anchor score records (ABI 18;
+ * yxh_head_desc.scores of the forward that wrote `pred`): one thread per anchor reads its 16-byte
+ * record and the row's 16-byte box (rewritten as xyxy in place, boxes.py:32-37) instead of all
+ * 5 + C columns -- 32 B of reads per anchor instead of 340 at 80 classes.  Identical results to
+ * yxh_postprocess (the records hold the filter's own fp32 values).  filter_done / rest_stream as
+ * yxh_postprocess_ev / _split (either may be NULL; rest_stream needs filter_done). */
+int yxh_postprocess_scored(float* pred, const float* scores, int32_t batch, int32_t anchors,
+                           int32_t num_classes, float conf_thre, double nms_thre, int32_t class_agnostic,
+                           int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,
+                           size_t workspace_bytes, void* filter_done, void* filter_stream, void* rest_stream);
 
 /*
  * yxh_yolox_loss: YoloxHead.get_losses (yolo_head.py:253-411) with SimOTA assignment
@@ -572,7 +582,12 @@ typedef struct {
  * A*(5+C)).  w_reg [5][cin] (reg 4 + obj 1) / w_cls [C][cin] in `dtype`, fp32 biases.
  * train = 1: obj/cls stay logits (get_output_and_grid, :213-231); train = 2 (ABI 16): the
  * eval rows without the box decode (decode_in_inference = False, :208-211): reg raw, obj/cls
- * sigmoid. */
+ * sigmoid.
+ * scores (ABI 18, NULL = none; eval decode rows (train = 0) of the 64 / 128-channel 16-bit levels
+ * only): per anchor one float4 {obj * max class, max class, its index, obj} -- the fp32 values
+ * utils.postprocess's filter computes from the row (boxes.py:46-48: first maximum, obj * conf), from
+ * the same registers -- at [image][a_off + pixel], image stride out_bstride / (5 + C) anchors.
+ * yxh_postprocess_scored reads these 16 bytes instead of the row's C class columns. */
 typedef struct {
     int32_t dtype, batch, h, w, cin, num_classes;
     yxh_src reg, cls;
@@ -586,6 +601,7 @@ typedef struct {
     float stride;
     int32_t train;
     int32_t reserved;
+    float* scores;
 } yxh_head_desc;
 int yxh_head_pred(const yxh_head_desc* d, void* stream);
 

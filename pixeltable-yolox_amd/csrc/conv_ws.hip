@@ -607,11 +607,19 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             // pixel-fragment-major: fragment j's FR uses come together, so its register is free (and
             // the next step's read into it can issue) FR * (FC - 1) MFMAs before that read's first use
             // (channel-major freed every fragment only in the step's last FC MFMAs: ~3 MFMAs of cover
-            // for an LDS read at one wave per SIMD); each accumulator's K order is unchanged
+            // for an LDS read at one wave per SIMD); each accumulator's K order is unchanged.  The
+            // head-form tiles keep channel-major (fragment-major spilled their 288-register set)
+            if constexpr (HP) {
 #pragma unroll
-            for (int j = 0; j < FC; ++j)
+                for (int i = 0; i < FR; ++i)
 #pragma unroll
-                for (int i = 0; i < FR; ++i) Mma<T>::run(acc[i][j], a[i][tap][c], bf[s % (PD + 1)][j]);
+                    for (int j = 0; j < FC; ++j) Mma<T>::run(acc[i][j], a[i][tap][c], bf[s % (PD + 1)][j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < FC; ++j)
+#pragma unroll
+                    for (int i = 0; i < FR; ++i) Mma<T>::run(acc[i][j], a[i][tap][c], bf[s % (PD + 1)][j]);
+            }
             // piece s of the previous tile's epilogue rides on this step's MFMAs
             if constexpr (EPI)
                 if (s < NP) epi_piece(e, accp, s / FR, s % FR);

@@ -262,6 +262,12 @@ __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
         const int pix = (int)(m - (m / hw) * hw);
         const int gy = pix / d.w, gx = pix - gy * d.w;
         float* row = stg + frow * rowf;
+        // serving score records (ABI 18): this lane's classes (f - 1) * 16 + fq * 4 + r, in increasing
+        // order, scanned as postprocess.hip's filter scans a row (class 0 -- lane fq 0 -- starts the
+        // scan even when NaN, every later class replaces only on a strict '>'), from the very values
+        // the row gets
+        float cbest = -INFINITY, objv = 0.0f;
+        int cbi = C;
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
 #pragma unroll
@@ -275,19 +281,47 @@ __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
                             if (d.train != 2) v = ch < 2 ? (v + (float)(ch == 0 ? gx : gy)) * st : hd_exp(v) * st;
                         } else {
                             v = d.train == 1 ? v : hd_sigmoid(v);
+                            objv = v;
                         }
                         row[ch] = v;
                     }
                 } else if (ch - 16 < C) {
                     v += bl[ch];
-                    row[5 + ch - 16] = d.train == 1 ? v : hd_sigmoid(v);
+                    const float sv = d.train == 1 ? v : hd_sigmoid(v);
+                    row[5 + ch - 16] = sv;
+                    if (ch == 16 || sv > cbest) {
+                        cbest = sv;
+                        cbi = ch - 16;
+                    }
                 }
+            }
+        }
+        if (d.scores != nullptr) {
+            // the four lanes of a pixel (fq = 0..3: lanes frow + 16 fq) merged with the filter's rules
+#pragma unroll
+            for (int off = 16; off < 64; off <<= 1) {
+                const float ob = __shfl_xor(cbest, off);
+                const int oi = __shfl_xor(cbi, off);
+                bool take;
+                if (oi >= C) take = false;
+                else if (cbi >= C) take = true;
+                else if (cbest != cbest) take = false;  // class 0 is NaN: the serial answer
+                else if (ob != ob) take = true;
+                else take = ob > cbest || (ob == cbest && oi < cbi);
+                if (take) { cbest = ob; cbi = oi; }
+            }
+            const float obj = __shfl(objv, frow + 16);  // ch 4 (obj) lives in lane fq = 1
+            const long long mr = g * 16 + frow;
+            if (fq == 0 && mr < M) {
+                const long long img = mr / hw;
+                *(float4*)(d.scores + 4 * (img * (d.out_bstride / rowf) + d.a_off + (mr - img * hw))) =
+                    make_float4(obj * cbest, cbest, (float)cbi, obj);
             }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): every lane's rows are in LDS
         __builtin_amdgcn_wave_barrier();
-        // ---- the group's rows are contiguous in the output (split once at an image boundary)
         const int n = (int)(M - m0 < 16 ? M - m0 : 16);
+        // ---- the group's rows are contiguous in the output (split once at an image boundary)
         int t0 = 0, bi = (int)(m0 / hw), p0 = (int)(m0 - (long long)bi * hw);
         while (t0 < n) {
             const int cnt = min(n - t0, hw - p0);
@@ -335,6 +369,10 @@ int head_pred_launch(const yxh_head_desc* d, hipStream_t st) {
     const bool rows16 = ((uintptr_t)d->reg.ptr % 16) == 0 && ((uintptr_t)d->cls.ptr % 16) == 0 &&
                         d->reg.cstride % 8 == 0 && d->cls.cstride % 8 == 0 && d->reg.bstride % 8 == 0 &&
                         d->cls.bstride % 8 == 0;
+    YXH_CHECK_ARG(!d->scores || (!v1 && rows16 && (d->cin == 64 || d->cin == 128) && d->train == 0 &&
+                                 ((uintptr_t)d->scores % 16) == 0 && d->out_bstride % (5 + d->num_classes) == 0),
+                  "head_pred: score records need the head_pred2 path (eval decode rows, 64 / 128 16-bit channels, "
+                  "16-byte rows) and a 16-byte aligned buffer");
     if (!v1 && rows16 && (d->cin == 64 || d->cin == 128)) {
         const long long groups = (M + 15) / 16;
         const unsigned grid2 = (unsigned)std::min<long long>((groups + 7) / 8, device_cus());  // one 8-wave block per CU

@@ -127,6 +127,34 @@ __global__ __launch_bounds__(256) void pp_filter(float* pred, int A, int C, floa
     }
 }
 
+// The filter fed by the forward's per-anchor score records (yxh_head_desc.scores, ABI 18): one
+// thread per anchor reads its 16-byte record {obj * max class, max class, class index, obj} --
+// computed by head_pred2 from the very fp32 values it wrote into the row, with this file's
+// first-maximum / NaN rules -- and the row's 16-byte box, which it rewrites as xyxy in place.
+// Candidates are those of pp_filter (sc >= conf, the same key and candidate row).
+__global__ __launch_bounds__(256) void pp_filter_scored(float* pred, const float4* scores, int A, int C, float conf,
+                                                        PPWork w) {
+    const int b = blockIdx.y, a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= A) return;
+    const int D = 5 + C;
+    const long long ra = (long long)b * A + a;
+    const float4 rec = scores[ra];
+    float* g = pred + ra * D;
+    const float cx = g[0], cy = g[1], bw = g[2], bh = g[3];
+    const float hw = bw / 2.0f, hh = bh / 2.0f;
+    const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
+    g[0] = x1; g[1] = y1; g[2] = x2; g[3] = y2;
+    const float sc = rec.x;
+    if (sc >= conf) {
+        const int slot = atomicAdd(&w.cnt[b], 1);
+        w.slot_of[ra] = slot;
+        w.key[(long long)b * A + slot] = ((unsigned long long)(~ordered(sc)) << 32) | (unsigned int)a;
+        float* o = w.cand + ((long long)b * A + slot) * kRow;
+        *(float4*)o = make_float4(x1, y1, x2, y2);
+        *(float4*)(o + 4) = make_float4(rec.w, rec.y, rec.z, sc);
+    }
+}
+
 // counters of the filter (per image) and the caller's detection counts, zeroed in one launch
 __global__ __launch_bounds__(256) void pp_init(int B, int* cnt, int* counts) {
     for (int q = threadIdx.x; q < B; q += 256) {
@@ -410,7 +438,7 @@ size_t pp_workspace(int B, int A) {
 // a serving loop keeps the filter in order behind its forward and runs the NMS proper beside the next one.
 int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
                 float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t filter_done,
-                hipStream_t rest) {
+                hipStream_t rest, const float* scores) {
     YXH_CHECK_ARG(!rest || rest == st || filter_done, "a separate rest stream needs the filter_done event");
     YXH_CHECK_ARG(pred && det && counts, "null pointer");
     YXH_CHECK_ARG(B > 0 && A >= 0 && C > 0, "postprocess shape B=%d A=%d C=%d", B, A, C);
@@ -440,7 +468,11 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     hipLaunchKernelGGL(pp_init, dim3(1), dim3(256), 0, st, B, w.cnt, counts);
     YXH_CHECK_LAUNCH("pp_init");
     int rc = YXH_OK;
-    if (A > 0) {
+    if (A > 0 && scores) {
+        hipLaunchKernelGGL(pp_filter_scored, dim3((A + 255) / 256, B), dim3(256), 0, st, pred, (const float4*)scores, A, C,
+                           conf, w);
+        YXH_CHECK_LAUNCH("pp_filter_scored");
+    } else if (A > 0) {
         hipLaunchKernelGGL(pp_filter, dim3((A + 63) / 64, B), dim3(256), lds, st, pred, A, C, conf, w);
         YXH_CHECK_LAUNCH("pp_filter");
     }

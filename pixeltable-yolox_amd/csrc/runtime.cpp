@@ -87,7 +87,7 @@ int yolox_loss_bwd(const float* preds, const float* raw, const float* labels, in
                    void* g_cls, hipStream_t st);
 int postprocess(float* pred, int B, int A, int C, float conf, double nms, int agnostic, long long vanilla_numel,
                 float* det, int* counts, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t filter_done,
-                hipStream_t rest);
+                hipStream_t rest, const float* scores = nullptr);
 int head_pred_launch(const yxh_head_desc* d, hipStream_t st);
 int stem_s2_launch(const yxh_stem2_desc* d, hipStream_t st);
 int augment_batch_launch(const uint8_t* pool, const yxh_aug_image* images, int B, int H, int W, uint8_t* mosaic_ws,
@@ -202,6 +202,16 @@ int yxh_postprocess_split(float* pred, int32_t batch, int32_t anchors, int32_t n
     return postprocess(pred, batch, anchors, num_classes, conf_thre, nms_thre, class_agnostic, vanilla_numel, det,
                        counts, workspace, workspace_bytes, (hipStream_t)filter_stream, (hipEvent_t)filter_done,
                        (hipStream_t)rest_stream);
+}
+
+int yxh_postprocess_scored(float* pred, const float* scores, int32_t batch, int32_t anchors, int32_t num_classes,
+                           float conf_thre, double nms_thre, int32_t class_agnostic, int64_t vanilla_numel, float* det,
+                           int32_t* counts, void* workspace, size_t workspace_bytes, void* filter_done,
+                           void* filter_stream, void* rest_stream) {
+    YXH_CHECK_ARG(scores && ((uintptr_t)scores % 16) == 0, "yxh_postprocess_scored: 16-byte aligned score records");
+    return postprocess(pred, batch, anchors, num_classes, conf_thre, nms_thre, class_agnostic, vanilla_numel, det,
+                       counts, workspace, workspace_bytes, (hipStream_t)filter_stream, (hipEvent_t)filter_done,
+                       (hipStream_t)rest_stream, scores);
 }
 
 size_t yxh_yolox_loss_workspace_bytes(int32_t batch, int32_t anchors, int32_t max_labels) {
@@ -410,10 +420,14 @@ int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, c
                            const int32_t* deps, int32_t nlanes, void* stream, void** graph_exec) {
     // Cap = the most capture streams a GPU test replays (tests/test_gpu_model.py: 8 chunk lanes,
     // bit-exact).  Round 2 saw a segfault in the join / hipStreamEndCapture with 7 streams (head
-    // levels plus three reg lanes, chunked plan); its cause is NOT identified: that op list held no
-    // memset node (those were in the loss / optimizer ops only), every op had been captured and
-    // recorded its event, and the same function has since captured 4-12 streams of plain kernels
-    // (profiles/r04/lanes_probe.txt) and the 8-lane plan.  Past 8 lanes use yxh_graph_create_dag.
+    // levels plus three reg lanes, chunked plan), never reproduced since (4-12 streams of plain
+    // kernels, profiles/r04/lanes_probe.txt; the 8-lane plan).  Reading this function for what that
+    // op list could have had that the probes did not (round 6): a lane with NO op.  Such a lane's
+    // stream joined the capture only through the fork, whose event is recorded right after
+    // BeginCapture, before any node exists (an empty dependency set); at the join its event record
+    // and the origin's wait then carry that empty set -- the one capture path no passing run
+    // exercised.  Lanes without ops now never join the capture (no stream, no fork wait, no join);
+    // tests/test_gpu_model.py captures a plan with two empty lanes.  The cap stays at 8.
     constexpr int kMaxLanes = 8;
     YXH_CHECK_ARG(graph_exec && (ops || n == 0) && lanes && dep_off, "null argument");
     YXH_CHECK_ARG(nlanes >= 1 && nlanes <= kMaxLanes, "nlanes %d", nlanes);
@@ -426,13 +440,16 @@ int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, c
     }
     (void)stream;
     hipStream_t st[kMaxLanes] = {};
+    bool used[kMaxLanes] = {};
+    used[0] = true;  // the origin stream carries the capture
+    for (int i = 0; i < n; ++i) used[lanes[i]] = true;
     hipEvent_t fork = nullptr;
     std::vector<hipEvent_t> ev(n, nullptr), join(nlanes, nullptr);
     int rc = YXH_OK, orc = YXH_OK;
     bool capturing = false;
     hipGraph_t g = nullptr;
     for (int l = 0; l < nlanes && !rc; ++l)
-        rc = check_hip(hipStreamCreateWithFlags(&st[l], hipStreamNonBlocking), "lane stream");
+        if (used[l]) rc = check_hip(hipStreamCreateWithFlags(&st[l], hipStreamNonBlocking), "lane stream");
     if (!rc) rc = check_hip(hipEventCreateWithFlags(&fork, hipEventDisableTiming), "event");
     for (int i = 0; i < n && !rc; ++i) rc = check_hip(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "event");
     for (int l = 0; l < nlanes && !rc; ++l)
@@ -446,7 +463,8 @@ int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, c
     }
     LDBG("lanes: capture begun rc=%d\n", rc);
     if (!rc) rc = check_hip(hipEventRecord(fork, st[0]), "fork");
-    for (int l = 1; l < nlanes && !rc; ++l) rc = check_hip(hipStreamWaitEvent(st[l], fork, 0), "fork wait");
+    for (int l = 1; l < nlanes && !rc; ++l)
+        if (used[l]) rc = check_hip(hipStreamWaitEvent(st[l], fork, 0), "fork wait");
     for (int i = 0; i < n && !rc && !orc; ++i) {
         hipStream_t s = st[lanes[i]];
         for (int k = dep_off[i]; k < dep_off[i + 1] && !rc; ++k)
@@ -465,6 +483,7 @@ int yxh_graph_create_lanes(const yxh_op* ops, int32_t n, const int32_t* lanes, c
     LDBG("lanes: ops done rc=%d orc=%d\n", rc, orc);
     if (capturing) {  // join every lane (also after an error, so the capture ends cleanly)
         for (int l = 1; l < nlanes; ++l) {
+            if (!used[l]) continue;
             (void)hipEventRecord(join[l], st[l]);
             (void)hipStreamWaitEvent(st[0], join[l], 0);
         }

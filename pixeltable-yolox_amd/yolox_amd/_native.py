@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 LIB_PATH = os.environ.get(
     "YOLOX_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libyoloxhip.so"))
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 # enums (yoloxhip.h)
 OK, EINVAL, EHIP, EUNSUPPORTED = 0, -1, -2, -3
@@ -136,7 +136,8 @@ class HeadDesc(C.Structure):
     _fields_ = [("dtype", C.c_int32), ("batch", C.c_int32), ("h", C.c_int32), ("w", C.c_int32), ("cin", C.c_int32),
                 ("num_classes", C.c_int32), ("reg", Src), ("cls", Src), ("w_reg", C.c_void_p), ("b_reg", C.c_void_p),
                 ("w_cls", C.c_void_p), ("b_cls", C.c_void_p), ("out", C.c_void_p), ("out_bstride", C.c_int64),
-                ("a_off", C.c_int32), ("stride", C.c_float), ("train", C.c_int32), ("reserved", C.c_int32)]
+                ("a_off", C.c_int32), ("stride", C.c_float), ("train", C.c_int32), ("reserved", C.c_int32),
+                ("scores", C.c_void_p)]
 
 
 class PackJob(C.Structure):
@@ -204,6 +205,7 @@ def lib():
             "yxh_postprocess": ([vp, i32, i32, i32, f32, f64, i32, i64, vp, vp, vp, sz, vp], C.c_int),
             "yxh_postprocess_ev": ([vp, i32, i32, i32, f32, f64, i32, i64, vp, vp, vp, sz, vp, vp], C.c_int),
             "yxh_postprocess_split": ([vp, i32, i32, i32, f32, f64, i32, i64, vp, vp, vp, sz, vp, vp, vp], C.c_int),
+            "yxh_postprocess_scored": ([vp, vp, i32, i32, i32, f32, f64, i32, i64, vp, vp, vp, sz, vp, vp, vp], C.c_int),
             "yxh_yolox_loss_workspace_bytes": ([i32, i32, i32], sz),
             "yxh_yolox_loss": ([vp, vp, vp, i32, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, sz, vp],
                                C.c_int),
@@ -258,7 +260,7 @@ def lib():
 
 EXPORTED = ["yxh_abi_version", "yxh_last_error", "yxh_sizeof_op", "yxh_sizeof_conv_desc", "yxh_conv2d", "yxh_head_pred",
             "yxh_focus_pack", "yxh_spp_maxpool", "yxh_stem_conv", "yxh_stem_s2", "yxh_stem_pack", "yxh_fold_bn_pack", "yxh_letterbox_batch", "yxh_augment_batch", "yxh_sizeof_aug_image", "yxh_postprocess_workspace_bytes", "yxh_set_nms_mask_budget",
-            "yxh_postprocess", "yxh_postprocess_ev", "yxh_postprocess_split", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes", "yxh_graph_create_dag",
+            "yxh_postprocess", "yxh_postprocess_ev", "yxh_postprocess_split", "yxh_postprocess_scored", "yxh_yolox_loss_workspace_bytes", "yxh_yolox_loss", "yxh_run_ops", "yxh_graph_create", "yxh_graph_create_lanes", "yxh_graph_create_dag",
             "yxh_graph_launch", "yxh_graph_destroy", "yxh_reduce_workspace_bytes", "yxh_bn_stats", "yxh_bn_act_fwd",
             "yxh_bn_act_bwd", "yxh_channel_sum", "yxh_conv_wgrad", "yxh_pack_dgrad_weight", "yxh_pack_weights_batch", "yxh_pack_frag", "yxh_spp_bwd",
             "yxh_upsample_bwd", "yxh_dw_wgrad_workspace_bytes", "yxh_dw_wgrad", "yxh_dw_dgrad", "yxh_resize_bilinear",

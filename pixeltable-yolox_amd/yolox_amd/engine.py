@@ -725,6 +725,8 @@ class Plan:
         # to finish reading the rows
         self._graph_alt = None
         self.output_alt: Optional[torch.Tensor] = None
+        # per-anchor serving score records written by the head launches (enable_scores, ABI 18)
+        self.scores: Optional[torch.Tensor] = None
         self._graph_ptrs = None
         self._param_sig = None
         self._packed_epoch = -1
@@ -816,6 +818,7 @@ class Plan:
                 hd.out = out_base
                 hd.out_bstride = out.anchors * out.row
                 hd.a_off, hd.stride, hd.train = a_off, a["stride"], a["train"]
+                hd.scores = (self.scores.data_ptr() + c * B * self.anchors * 16) if self.scores is not None else None
             elif rec.kind == N.OP_SPP:
                 s = op.u.spp
                 buf: Buffer = a["buf"]
@@ -1148,11 +1151,33 @@ class Plan:
                         self.lib.yxh_graph_destroy(gk)
             self._segments = None
 
+    def enable_scores(self) -> Optional[torch.Tensor]:
+        """Have the head launches also write per-anchor serving records [B, A, 4] fp32
+        {obj * max class, max class, class index, obj} (yxh_head_desc.scores), which
+        ``postprocess_device(..., scores=)`` filters instead of the rows' class columns (32 instead
+        of 340 bytes read per anchor).  The records belong to the forward that wrote the output
+        rows: the next forward overwrites them.  Eval decode plans whose every level is one
+        head_pred launch over 64 / 128 16-bit channels only; returns None (nothing enabled)
+        otherwise.  Call before capture()."""
+        if self._graph is not None or self._graph_alt is not None:
+            raise RuntimeError("enable_scores() before capture()")
+        heads = [r for r in self.ctx.ops if r.kind == N.OP_HEAD]
+        other = [r for r in self.ctx.ops if r.kind == N.OP_CONV and (r.args["dst_f32"] or r.args.get("head_post"))]
+        if (self.stage != "full" or not heads or other or self.ctx.dtype == torch.float32
+                or any(r.args["cin"] not in (64, 128) or r.args["train"] != PlanCtx.HEAD_EVAL for r in heads)):
+            return None
+        if self.scores is None:
+            self.scores = torch.zeros(self.batch, self.anchors, 4, dtype=torch.float32, device=self.device)
+            self._encode_ops()
+        return self.scores
+
     def capture(self, slots: int = 1) -> None:
         """Capture the whole forward into a hipGraph reading ``static_input()``; ``slots`` = 2
         also captures it writing ``output_alt`` (replay(1))."""
         if slots not in (1, 2):
             raise ValueError("slots must be 1 or 2")
+        if slots == 2 and self.scores is not None:
+            raise NotImplementedError("score records are single-buffered: one output slot")
         self.pack_weights()
         self._bind_input(self.static_input())
         self._destroy_graphs()

@@ -776,9 +776,18 @@ class CapturedTrainStep:
     their fixed storage, so in-place optimizer steps between replays are seen.  ``grad_scale``
     (a one-element fp32 device tensor, e.g. ``GradScaler._scale``) is read by every replay.
 
+    Data parallel (round 6): when the model runs under ``yolox_amd.dp.DistributedDataParallel``
+    (the reducer's hooks are installed on the TrainGraph by an eager DDP step), the capture records
+    in which segment -- and so on which stream, at which point of it -- every parameter's
+    gradient is reported ready, instead of issuing collectives inside the capture.  A replay then
+    resets the reducer, reports the same parameters right after replaying that segment on that
+    segment's stream (the eager step's exact event placement: the reducer's bucketed RCCL
+    all-reduces are issued between segments, overlapping the later segments), and finishes the
+    reducer behind the last segment (1/world mean on the compute stream), as the eager backward does.
+
     Requirements: the step ran eagerly once for this shape (tiles tuned, the repack table
-    recorded), one process (the data-parallel reducer's per-bucket hooks stay eager), and the
-    parameters keep their storage (``model.to`` / re-created tensors need a new capture)."""
+    recorded), and the parameters keep their storage (``model.to`` / re-created tensors need a new
+    capture)."""
 
     def __init__(self, model, images: torch.Tensor, targets: torch.Tensor, dtype: Optional[torch.dtype] = None,
                  grad_scale: Optional[torch.Tensor] = None):
@@ -786,8 +795,10 @@ class CapturedTrainStep:
         dtype = dtype or compute_dtype_from_autocast()
         if g is None or g.dtype != dtype or g.device != model.device:
             raise RuntimeError("CapturedTrainStep: run one eager training step of this shape first")
-        if g.on_param_ready is not None or g.on_backward_end is not None:
-            raise RuntimeError("CapturedTrainStep: data-parallel reducer hooks are not captured")
+        # data-parallel hooks (DistributedDataParallel.forward installs them): reported between the
+        # replayed segments, never captured
+        self.on_ready, self.on_end = g.on_param_ready, g.on_backward_end
+        self.reducer = getattr(self.on_ready, "__self__", None)
         if g.batch_pack and g._pack_table is None:
             raise RuntimeError("CapturedTrainStep: the repack table is not recorded yet (run an eager step)")
         self.model, self.g, self.dev = model, g, model.device
@@ -804,7 +815,8 @@ class CapturedTrainStep:
         # nodes to its own queues, which serialised the weight gradients with the data-gradient
         # chain on MI355X: profiles/r03/train_graph.txt.)
         self.pool = None  # the first segment's private pool, shared by the later segments (CUDAGraph.pool())
-        self.plan: list = []  # ("main" | "side", CUDAGraph)
+        self.plan: list = []  # ("main" | "side", CUDAGraph or None (an empty main segment), [ready params])
+        self._ready_cur: list = []  # parameters reported ready in the main segment being captured
         self._empty: list = []  # captured main segments with no launch (kept alive, not replayed)
         self._keep: list = []  # conv-output gradients read by side segments: alive for the whole step
         # YOLOX_AMD_MAIN_PRIORITY=1: the main segments replay on a high-priority stream, so the
@@ -829,11 +841,13 @@ class CapturedTrainStep:
         with torch.cuda.stream(self.main):
             self._begin()
             g._segcap = self if self.side_stream is not None else None
+            g.on_param_ready, g.on_backward_end = self._ready_cur.append, None
             try:
                 self.out = g.forward(self.images, self.targets)
                 g.backward(grad_scale)  # begin(): p.grad is None here, nothing to carry over
             finally:
                 g._segcap = None
+                g.on_param_ready, g.on_backward_end = self.on_ready, self.on_end
                 self._end()
         self.events = [torch.cuda.Event() for _ in self.plan]
 
@@ -854,10 +868,13 @@ class CapturedTrainStep:
                 warnings.warn_explicit(w.message, w.category, w.filename, w.lineno)
         if self.pool is None:
             self.pool = self._cur.pool()
-        if empty:
+        if empty:  # kept as the pool owner; its readiness reports stay at this point of the main stream
             self._empty.append(self._cur)
+            if self._ready_cur:
+                self.plan.append(("main", None, self._ready_cur))
         else:
-            self.plan.append(("main", self._cur))
+            self.plan.append(("main", self._cur, self._ready_cur))
+        self._ready_cur = []
         self._cur = None
 
     def side(self, pending: list) -> None:
@@ -871,7 +888,7 @@ class CapturedTrainStep:
                 launch()
                 self._keep.append(dy)
             gs.capture_end()
-        self.plan.append(("side", gs))
+        self.plan.append(("side", gs, [param for _, _, param in pending]))
         self._begin()
 
     def _replay(self) -> None:
@@ -879,18 +896,30 @@ class CapturedTrainStep:
         self.main.wait_stream(caller)
         fork = torch.cuda.Event()  # a side segment ahead of every (non-empty) main one forks here
         fork.record(self.main)
+        ready = self.on_ready
+        if ready is not None and self.reducer is not None and hasattr(self.reducer, "reset"):
+            self.reducer.reset()  # what DistributedDataParallel.forward does before an eager step
         with torch.cuda.stream(self.main):
-            for (kind, gr), ev in zip(self.plan, self.events):
+            for (kind, gr, params), ev in zip(self.plan, self.events):
                 if kind == "main":
-                    gr.replay()
+                    if gr is not None:
+                        gr.replay()
+                    if ready is not None:
+                        for p in params:  # events on the main stream, right behind this segment
+                            ready(p)
                     fork = ev
                     ev.record(self.main)
                 else:
                     self.side_stream.wait_event(fork)
                     with torch.cuda.stream(self.side_stream):
                         gr.replay()
+                        if ready is not None:
+                            for p in params:  # events on the side stream, behind its segment
+                                ready(p)
             if self.side_stream is not None:
                 self.main.wait_stream(self.side_stream)
+            if self.on_end is not None:
+                self.on_end()  # the reducer's remaining buckets, the wait for them and the 1/world mean
         caller.wait_stream(self.main)
 
     def __call__(self, images: torch.Tensor, targets: torch.Tensor) -> dict:

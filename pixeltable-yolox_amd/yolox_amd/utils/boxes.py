@@ -69,14 +69,16 @@ def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: fl
                        nms_thre: float = 0.45, class_agnostic: bool = False,
                        vanilla_numel: int = VANILLA_NUMEL_CPU, det: Optional[torch.Tensor] = None,
                        counts: Optional[torch.Tensor] = None, filter_done: Optional[torch.cuda.Event] = None,
-                       rest_stream: Optional[torch.cuda.Stream] = None):
+                       rest_stream: Optional[torch.cuda.Stream] = None, scores: Optional[torch.Tensor] = None):
     """Asynchronous form: returns (det [B, A, 7], counts [B] int32) on the device,
     nothing synchronised, on the current stream.  ``prediction`` (fp32, on device) becomes xyxy
     in place.  ``filter_done`` is recorded once ``prediction`` is no longer read (after the
     filter pass): a producer that waits on it may overwrite ``prediction`` while the rest of
     the NMS runs.  ``rest_stream`` (needs ``filter_done``): only the filter runs on the current
     stream; the sort / mask / reduce passes run on ``rest_stream`` after it (yxh_postprocess_split),
-    and det / counts are complete in that stream's order."""
+    and det / counts are complete in that stream's order.  ``scores``: the [B, A, 4] serving records
+    the forward that wrote ``prediction`` emitted (engine.Plan.enable_scores): the filter reads them
+    instead of the class columns (yxh_postprocess_scored, same results)."""
     N.require_device(prediction, "prediction")
     if prediction.dtype != torch.float32 or not prediction.is_contiguous():
         raise ValueError("prediction must be a contiguous float32 [B, A, 5+C] tensor")
@@ -92,10 +94,23 @@ def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: fl
         raise ValueError("rest_stream needs a filter_done event")
     if filter_done is not None and not filter_done.cuda_event:
         filter_done.record()  # torch creates the event lazily, on its first record
+    if scores is not None:
+        N.require_device(scores, "scores")
+        if tuple(scores.shape) != (B, A, 4) or scores.dtype != torch.float32 or not scores.is_contiguous():
+            raise ValueError(f"scores must be a contiguous float32 {(B, A, 4)} tensor")
     ws = _workspace(dev, B, A, split=rest_stream is not None)
     buf = ws.buf
     try:
-        if filter_done is None:
+        if scores is not None:
+            if rest_stream is not None:
+                for t in (buf, det, counts):
+                    t.record_stream(rest_stream)
+            N.check(N.lib().yxh_postprocess_scored(
+                prediction.data_ptr(), scores.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre),
+                int(bool(class_agnostic)), int(vanilla_numel), det.data_ptr(), counts.data_ptr(), buf.data_ptr(),
+                buf.numel(), filter_done.cuda_event if filter_done is not None else None, N.stream_ptr(dev),
+                rest_stream.cuda_stream if rest_stream is not None else None), "postprocess")
+        elif filter_done is None:
             N.check(N.lib().yxh_postprocess(
                 prediction.data_ptr(), B, A, num_classes, float(conf_thre), float(nms_thre),
                 int(bool(class_agnostic)), int(vanilla_numel), det.data_ptr(), counts.data_ptr(), buf.data_ptr(),

@@ -40,6 +40,32 @@ def test_ddp_gradients_are_the_mean_of_single_rank_gradients(tmp_path):
         assert r["single_differs"]  # the ranks really trained on different batches
 
 
+def test_captured_dp_step_matches_eager_dp_step(tmp_path):
+    """The captured training step under DistributedDataParallel (round 6): two gloo ranks on the one
+    GPU, each with an eager-DP copy and a captured-DP copy of the model on its own batch -- losses,
+    averaged gradients and BN buffers bit for bit over three fused-SGD steps; every parameter is
+    reported to the reducer from some replayed segment; after averaging both ranks hold the same
+    gradients."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_gpu_worker.py"), "--rank", str(r), "--port",
+                               str(port), "--out", str(tmp_path / f"c{r}.json"), "--captured"], env=env)
+             for r in range(2)]
+    try:
+        rcs = [p.wait(timeout=300) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0]
+    for r in range(2):
+        res = json.load(open(tmp_path / f"c{r}.json"))
+        assert res["steps"] == 3 and res["grads_equal_across_ranks"], res
+        assert res["reported"] == res["nparams"] and res["segments"] >= 2, res
+
+
 def test_cli_train_single_gpu_multiscale():
     """`python -m yolox_amd train -c yolox_s -d 1 ...` (cli/train.py) end to end on the HIP path:
     12 iterations of Trainer.train_one_iter (fp16 autocast + GradScaler through FusedStep,

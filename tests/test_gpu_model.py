@@ -226,6 +226,34 @@ def test_eight_chunk_lanes_capture_matches_whole_batch():
     assert torch.equal(p.replay().clone(), a)
 
 
+def test_lane_capture_with_empty_lanes():
+    """yxh_graph_create_lanes with more lanes than the op list uses (the bench plan's lanes + 2 lanes
+    that hold no op -- the capture path round 2's unexplained 7-stream crash may have taken, runtime.cpp):
+    empty lanes never join the capture, and the graph replays the linear graph's output bit for bit."""
+    import ctypes as C
+    from yolox_amd import _native as N
+    from yolox_amd.engine import Plan
+    from yolox_amd.weights import synthetic_images
+    m = model("yolox_s", torch.bfloat16)
+    x = torch.from_numpy(synthetic_images(4, 160, 160, seed=5)).cuda()
+    p = Plan(m, 4, 160, 160, torch.bfloat16, "cuda", N.NHWC, torch.uint8)
+    p.graph_mode = "linear"
+    p.static_input().copy_(x)
+    want = p.replay().clone()
+    assert 1 < p.nlanes <= 6
+    lanes, off, deps = p._lane_arrays()
+    g = C.c_void_p()
+    N.check(p.lib.yxh_graph_create_lanes(p._ops, len(p._ops), lanes, off, deps, p.nlanes + 2,
+                                         N.stream_ptr(p.device), C.byref(g)), "lanes + 2 empty")
+    try:
+        for _ in range(2):
+            N.check(p.lib.yxh_graph_launch(g, N.stream_ptr(p.device)), "launch")
+            torch.cuda.synchronize()
+            assert torch.equal(p.output, want)
+    finally:
+        N.check(p.lib.yxh_graph_destroy(g), "destroy")
+
+
 def test_fused_stem_s2_plan_matches_unfused_plan():
     """The planned forward with Focus stem + dark2[0] as one yxh_stem_s2 launch (uint8 NHWC
     input, the bench / processor form) vs the same plan with the two as separate launches:

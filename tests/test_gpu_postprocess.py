@@ -191,3 +191,57 @@ def test_mask_passes_match_one_pass(oracle, budget):
         run_both(oracle, pred, 2, 0.0, 0.5)
     finally:
         lib.yxh_set_nms_mask_budget(0)
+
+
+@pytest.mark.parametrize("size,batch", [(320, 4), (640, 2)])
+def test_scored_filter_from_head_records(oracle, size, batch):
+    """Plan.enable_scores (ABI 18): the head launches also write per-anchor records {obj * max class,
+    max class, class index, obj}; (1) the output rows are bit-identical to a plan without records,
+    (2) every record equals the filter's own arithmetic on its row (first maximum, obj * conf in fp32),
+    (3) yxh_postprocess_scored's detections, counts and in-place xyxy rows are bit-identical to the
+    row-reading filter's and to the C oracle's, at three thresholds, on one stream and split over two."""
+    from yolox_amd import _native as N
+    from yolox_amd.engine import Plan
+    from yolox_amd.models import YoloxModule
+    from yolox_amd.utils.boxes import postprocess_device
+    from yolox_amd.weights import synthetic_images
+    m = YoloxModule.synthetic("yolox_s", seed=0, device="cuda", dtype=torch.bfloat16)
+    x = torch.from_numpy(synthetic_images(batch, size, size, seed=21)).cuda()
+    plain = Plan(m, batch, size, size, torch.bfloat16, "cuda", N.NHWC, torch.uint8)
+    plain.static_input().copy_(x)
+    want_rows = plain.replay().clone()
+    p = Plan(m, batch, size, size, torch.bfloat16, "cuda", N.NHWC, torch.uint8)
+    scores = p.enable_scores()
+    assert scores is not None and tuple(scores.shape) == (batch, p.anchors, 4)
+    p.static_input().copy_(x)
+    rows = p.replay().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(rows, want_rows)
+    h = rows.cpu().numpy()
+    cls = h[..., 5:]
+    best = cls.max(-1)
+    rec = scores.cpu().numpy()
+    np.testing.assert_array_equal(rec[..., 1], best)
+    np.testing.assert_array_equal(rec[..., 2], cls.argmax(-1).astype(np.float32))
+    np.testing.assert_array_equal(rec[..., 3], h[..., 4])
+    np.testing.assert_array_equal(rec[..., 0], (h[..., 4] * best).astype(np.float32))
+    side = torch.cuda.Stream()
+    for conf in (0.01, 0.3, 0.5):
+        want = oracle.postprocess(h.copy(), 80, conf, 0.65)
+        pa, pb = rows.clone(), rows.clone()
+        da, ca = postprocess_device(pa, 80, conf, 0.65)
+        db, cb = postprocess_device(pb, 80, conf, 0.65, scores=scores)
+        ev = torch.cuda.Event()
+        pc = rows.clone()
+        dc, cc = postprocess_device(pc, 80, conf, 0.65, scores=scores, filter_done=ev, rest_stream=side)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        assert torch.equal(pa, pb) and torch.equal(pa, pc)  # the in-place xyxy rows
+        assert torch.equal(ca, cb) and torch.equal(ca, cc)
+        n = ca.cpu().numpy()
+        for b in range(batch):
+            assert torch.equal(da[b, :n[b]], db[b, :n[b]]) and torch.equal(da[b, :n[b]], dc[b, :n[b]])
+            if want[b] is None:
+                assert n[b] == 0
+            else:
+                np.testing.assert_array_equal(db[b, :n[b]].cpu().numpy(), want[b])
