@@ -10,7 +10,7 @@ output) runs in stream order behind its forward and the rest of that batch's NMS
 beside the next batch's forward (yxh_postprocess_split; --nms-event: the whole NMS on the side
 stream, the next forward waiting on the filter's event) -- --serial-nms runs them back to back on
 one stream.  The filter reads the per-anchor score records the head launches write beside the rows
-(16 bytes per anchor instead of 340; yxh_postprocess_scored, identical detections; --no-scores: the
+(32 bytes per anchor instead of 340; yxh_postprocess_scored, identical detections; --no-scores: the
 rows' class columns).  Inputs are resident in HBM (uint8 NHWC, as the
 processor's letterbox hands them to the forward) before the timed region.  With --gpus N (torchrun, one process per GPU) each rank
 runs an independent replica -- inference has no exchange step, so there is no

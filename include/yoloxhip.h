@@ -359,11 +359,14 @@ int yxh_postprocess_split(float* pred, int32_t batch, int32_t anchors, int32_t n
                           size_t workspace_bytes, void* filter_done, void* filter_stream,
                           void* rest_stream);
 /* The same passes with the filter fed by the forward's per-anchor score records (ABI 18;
- * yxh_head_desc.scores of the forward that wrote `pred`): one thread per anchor reads its 16-byte
- * record and the row's 16-byte box (rewritten as xyxy in place, boxes.py:32-37) instead of all
- * 5 + C columns -- 32 B of reads per anchor instead of 340 at 80 classes.  Identical results to
- * yxh_postprocess (the records hold the filter's own fp32 values).  filter_done / rest_stream as
- * yxh_postprocess_ev / _split (either may be NULL; rest_stream needs filter_done). */
+ * yxh_head_desc.scores of the forward that wrote `pred`): one thread per anchor reads its 32-byte
+ * record and only writes the row's box as xyxy in place (boxes.py:32-37) -- 32 B read per anchor
+ * instead of 340 at 80 classes.  Identical results to yxh_postprocess (the records hold the
+ * filter's own fp32 values).  filter_done / rest_stream as yxh_postprocess_ev / _split (either may be
+ * NULL; rest_stream needs filter_done).  Workspace contract: this entry point does not reset the
+ * per-image candidate counters (no pp_init launch in front of the filter): it expects them zero,
+ * which every yxh_postprocess* call leaves them (the final reduce pass zeroes them) and a
+ * zero-filled workspace is on its first use. */
 int yxh_postprocess_scored(float* pred, const float* scores, int32_t batch, int32_t anchors,
                            int32_t num_classes, float conf_thre, double nms_thre, int32_t class_agnostic,
                            int64_t vanilla_numel, float* det, int32_t* counts, void* workspace,
@@ -584,10 +587,10 @@ typedef struct {
  * eval rows without the box decode (decode_in_inference = False, :208-211): reg raw, obj/cls
  * sigmoid.
  * scores (ABI 18, NULL = none; eval decode rows (train = 0) of the 64 / 128-channel 16-bit levels
- * only): per anchor one float4 {obj * max class, max class, its index, obj} -- the fp32 values
- * utils.postprocess's filter computes from the row (boxes.py:46-48: first maximum, obj * conf), from
- * the same registers -- at [image][a_off + pixel], image stride out_bstride / (5 + C) anchors.
- * yxh_postprocess_scored reads these 16 bytes instead of the row's C class columns. */
+ * only): per anchor 8 floats {obj * max class, max class, its index, obj, cx, cy, w, h} -- the fp32
+ * values utils.postprocess's filter computes from the row (boxes.py:46-48: first maximum, obj *
+ * conf) and the row's box, from the same registers -- at [image][a_off + pixel], image stride
+ * out_bstride / (5 + C) anchors.  yxh_postprocess_scored reads these 32 bytes instead of the row. */
 typedef struct {
     int32_t dtype, batch, h, w, cin, num_classes;
     yxh_src reg, cls;

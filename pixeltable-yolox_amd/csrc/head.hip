@@ -267,6 +267,7 @@ __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
         // scan even when NaN, every later class replaces only on a strict '>'), from the very values
         // the row gets
         float cbest = -INFINITY, objv = 0.0f;
+        float boxv[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // ch 0-3 (lane fq 0): the decoded box, copied into the record
         int cbi = C;
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
@@ -279,6 +280,7 @@ __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
                         v += bl[ch];
                         if (ch < 4) {
                             if (d.train != 2) v = ch < 2 ? (v + (float)(ch == 0 ? gx : gy)) * st : hd_exp(v) * st;
+                            boxv[r] = v;
                         } else {
                             v = d.train == 1 ? v : hd_sigmoid(v);
                             objv = v;
@@ -314,8 +316,9 @@ __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
             const long long mr = g * 16 + frow;
             if (fq == 0 && mr < M) {
                 const long long img = mr / hw;
-                *(float4*)(d.scores + 4 * (img * (d.out_bstride / rowf) + d.a_off + (mr - img * hw))) =
-                    make_float4(obj * cbest, cbest, (float)cbi, obj);
+                float4* rec = (float4*)(d.scores + 8 * (img * (d.out_bstride / rowf) + d.a_off + (mr - img * hw)));
+                rec[0] = make_float4(obj * cbest, cbest, (float)cbi, obj);
+                rec[1] = make_float4(boxv[0], boxv[1], boxv[2], boxv[3]);
             }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): every lane's rows are in LDS

@@ -127,22 +127,22 @@ __global__ __launch_bounds__(256) void pp_filter(float* pred, int A, int C, floa
     }
 }
 
-// The filter fed by the forward's per-anchor score records (yxh_head_desc.scores, ABI 18): one
-// thread per anchor reads its 16-byte record {obj * max class, max class, class index, obj} --
-// computed by head_pred2 from the very fp32 values it wrote into the row, with this file's
-// first-maximum / NaN rules -- and the row's 16-byte box, which it rewrites as xyxy in place.
-// Candidates are those of pp_filter (sc >= conf, the same key and candidate row).
+// The filter fed by the forward's per-anchor records (yxh_head_desc.scores, ABI 18): one thread per
+// anchor reads its 32-byte record {obj * max class, max class, class index, obj | cx, cy, w, h} --
+// written by head_pred2 from the very fp32 values it put in the row, the class maximum with this
+// file's first-maximum / NaN rules -- and only WRITES the row's xyxy box in place (boxes.py:32-37).
+// Candidates are pp_filter's (sc >= conf, the same key and candidate row).
 __global__ __launch_bounds__(256) void pp_filter_scored(float* pred, const float4* scores, int A, int C, float conf,
                                                         PPWork w) {
     const int b = blockIdx.y, a = blockIdx.x * 256 + threadIdx.x;
     if (a >= A) return;
     const int D = 5 + C;
     const long long ra = (long long)b * A + a;
-    const float4 rec = scores[ra];
-    float* g = pred + ra * D;
-    const float cx = g[0], cy = g[1], bw = g[2], bh = g[3];
+    const float4 rec = scores[2 * ra], box = scores[2 * ra + 1];
+    const float cx = box.x, cy = box.y, bw = box.z, bh = box.w;
     const float hw = bw / 2.0f, hh = bh / 2.0f;
     const float x1 = cx - hw, y1 = cy - hh, x2 = cx + hw, y2 = cy + hh;
+    float* g = pred + ra * D;
     g[0] = x1; g[1] = y1; g[2] = x2; g[3] = y2;
     const float sc = rec.x;
     if (sc >= conf) {
@@ -352,13 +352,20 @@ __global__ __launch_bounds__(256) void pp_mask(int A, double thr, int agnostic, 
 // loads across lanes) -- no dependent global load per kept box.  One launch per pass
 // (row blocks [rb0, rb1)): the removed set and the keep count continue from the
 // previous pass through the workspace / ``counts``.
-__global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int* counts, int rb0, int rb1) {
+// last: the final pass, which also zeroes the image's filter counter for the workspace's next call
+// (one wave: its load of the counter above precedes the store in program order), and an image
+// without candidates gets its count here (yxh_postprocess_scored skips pp_init).
+__global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int* counts, int rb0, int rb1, int last) {
     extern __shared__ unsigned long long removed[];  // [capw]
     const int b = blockIdx.x, lane = threadIdx.x;
     const int n = w.cnt[b];
     const int nw = (n + 63) / 64;
+    if (rb0 == 0 && n == 0 && lane == 0) counts[b] = 0;
     rb1 = min(rb1, nw);
-    if (rb0 >= rb1) return;
+    if (rb0 >= rb1) {
+        if (last && lane == 0) w.cnt[b] = 0;
+        return;
+    }
     unsigned long long* gremoved = w.removed + (long long)b * w.capw;
     for (int q = lane; q < nw; q += 64) removed[q] = rb0 == 0 ? 0ull : gremoved[q];
     __syncthreads();
@@ -402,7 +409,10 @@ __global__ __launch_bounds__(64) void pp_reduce(int A, PPWork w, float* det, int
     }
     if (rb1 < nw)  // a later pass continues from here
         for (int q = lane; q < nw; q += 64) gremoved[q] = removed[q];
-    if (lane == 0) counts[b] = nk;
+    if (lane == 0) {
+        counts[b] = nk;
+        if (last) w.cnt[b] = 0;
+    }
 }
 
 // Sorted rows per mask pass: a multiple of 64, all rows at once when the budget allows.
@@ -465,8 +475,12 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
     w.mask = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * w.cap * w.capw);
     unsigned long long* key2 = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * A);
     w.removed = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)B * w.capw);
-    hipLaunchKernelGGL(pp_init, dim3(1), dim3(256), 0, st, B, w.cnt, counts);
-    YXH_CHECK_LAUNCH("pp_init");
+    // the counters are zero on entry to the scored path: the final reduce pass of every call leaves
+    // them so, and a fresh workspace is zero-filled (yxh_postprocess_scored's contract)
+    if (!scores || A == 0) {
+        hipLaunchKernelGGL(pp_init, dim3(1), dim3(256), 0, st, B, w.cnt, counts);
+        YXH_CHECK_LAUNCH("pp_init");
+    }
     int rc = YXH_OK;
     if (A > 0 && scores) {
         hipLaunchKernelGGL(pp_filter_scored, dim3((A + 255) / 256, B), dim3(256), 0, st, pred, (const float4*)scores, A, C,
@@ -511,7 +525,8 @@ int postprocess(float* pred, int B, int A, int C, float conf, double nms, int ag
         hipLaunchKernelGGL(pp_mask, dim3(gx, B), dim3(256), 0, st, A, nms, agnostic, vanilla_numel, w, rb0,
                            rb0 + rbp);
         YXH_CHECK_LAUNCH("pp_mask");
-        hipLaunchKernelGGL(pp_reduce, dim3(B), dim3(64), (size_t)w.capw * 8, st, A, w, det, counts, rb0, rb0 + rbp);
+        hipLaunchKernelGGL(pp_reduce, dim3(B), dim3(64), (size_t)w.capw * 8, st, A, w, det, counts, rb0, rb0 + rbp,
+                           rb0 + rbp >= w.capw ? 1 : 0);
         YXH_CHECK_LAUNCH("pp_reduce");
     }
     return YXH_OK;

@@ -818,7 +818,7 @@ class Plan:
                 hd.out = out_base
                 hd.out_bstride = out.anchors * out.row
                 hd.a_off, hd.stride, hd.train = a_off, a["stride"], a["train"]
-                hd.scores = (self.scores.data_ptr() + c * B * self.anchors * 16) if self.scores is not None else None
+                hd.scores = (self.scores.data_ptr() + c * B * self.anchors * 32) if self.scores is not None else None
             elif rec.kind == N.OP_SPP:
                 s = op.u.spp
                 buf: Buffer = a["buf"]
@@ -1152,10 +1152,10 @@ class Plan:
             self._segments = None
 
     def enable_scores(self) -> Optional[torch.Tensor]:
-        """Have the head launches also write per-anchor serving records [B, A, 4] fp32
-        {obj * max class, max class, class index, obj} (yxh_head_desc.scores), which
-        ``postprocess_device(..., scores=)`` filters instead of the rows' class columns (32 instead
-        of 340 bytes read per anchor).  The records belong to the forward that wrote the output
+        """Have the head launches also write per-anchor serving records [B, A, 8] fp32
+        {obj * max class, max class, class index, obj, cx, cy, w, h} (yxh_head_desc.scores), which
+        ``postprocess_device(..., scores=)`` filters instead of the rows (32 instead of 340 bytes read
+        per anchor).  The records belong to the forward that wrote the output
         rows: the next forward overwrites them.  Eval decode plans whose every level is one
         head_pred launch over 64 / 128 16-bit channels only; returns None (nothing enabled)
         otherwise.  Call before capture()."""
@@ -1167,7 +1167,7 @@ class Plan:
                 or any(r.args["cin"] not in (64, 128) or r.args["train"] != PlanCtx.HEAD_EVAL for r in heads)):
             return None
         if self.scores is None:
-            self.scores = torch.zeros(self.batch, self.anchors, 4, dtype=torch.float32, device=self.device)
+            self.scores = torch.zeros(self.batch, self.anchors, 8, dtype=torch.float32, device=self.device)
             self._encode_ops()
         return self.scores
 

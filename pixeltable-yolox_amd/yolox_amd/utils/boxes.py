@@ -43,7 +43,9 @@ class _Workspace:
         if self.done is not None:
             stream.wait_event(self.done)
         if self.buf is None or self.buf.numel() < need:
-            self.buf = torch.empty(need, dtype=torch.uint8, device=device)
+            # zero-filled: yxh_postprocess_scored expects the candidate counters zero on entry (every
+            # call leaves them so)
+            self.buf = torch.zeros(need, dtype=torch.uint8, device=device)
         self.buf.record_stream(stream)  # the allocator may recycle it only after this stream's use
         return self.buf
 
@@ -76,7 +78,7 @@ def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: fl
     filter pass): a producer that waits on it may overwrite ``prediction`` while the rest of
     the NMS runs.  ``rest_stream`` (needs ``filter_done``): only the filter runs on the current
     stream; the sort / mask / reduce passes run on ``rest_stream`` after it (yxh_postprocess_split),
-    and det / counts are complete in that stream's order.  ``scores``: the [B, A, 4] serving records
+    and det / counts are complete in that stream's order.  ``scores``: the [B, A, 8] serving records
     the forward that wrote ``prediction`` emitted (engine.Plan.enable_scores): the filter reads them
     instead of the class columns (yxh_postprocess_scored, same results)."""
     N.require_device(prediction, "prediction")
@@ -96,8 +98,8 @@ def postprocess_device(prediction: torch.Tensor, num_classes: int, conf_thre: fl
         filter_done.record()  # torch creates the event lazily, on its first record
     if scores is not None:
         N.require_device(scores, "scores")
-        if tuple(scores.shape) != (B, A, 4) or scores.dtype != torch.float32 or not scores.is_contiguous():
-            raise ValueError(f"scores must be a contiguous float32 {(B, A, 4)} tensor")
+        if tuple(scores.shape) != (B, A, 8) or scores.dtype != torch.float32 or not scores.is_contiguous():
+            raise ValueError(f"scores must be a contiguous float32 {(B, A, 8)} tensor")
     ws = _workspace(dev, B, A, split=rest_stream is not None)
     buf = ws.buf
     try:

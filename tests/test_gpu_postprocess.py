@@ -196,7 +196,7 @@ def test_mask_passes_match_one_pass(oracle, budget):
 @pytest.mark.parametrize("size,batch", [(320, 4), (640, 2)])
 def test_scored_filter_from_head_records(oracle, size, batch):
     """Plan.enable_scores (ABI 18): the head launches also write per-anchor records {obj * max class,
-    max class, class index, obj}; (1) the output rows are bit-identical to a plan without records,
+    max class, class index, obj, cx, cy, w, h}; (1) the output rows are bit-identical to a plan without records,
     (2) every record equals the filter's own arithmetic on its row (first maximum, obj * conf in fp32),
     (3) yxh_postprocess_scored's detections, counts and in-place xyxy rows are bit-identical to the
     row-reading filter's and to the C oracle's, at three thresholds, on one stream and split over two."""
@@ -212,7 +212,7 @@ def test_scored_filter_from_head_records(oracle, size, batch):
     want_rows = plain.replay().clone()
     p = Plan(m, batch, size, size, torch.bfloat16, "cuda", N.NHWC, torch.uint8)
     scores = p.enable_scores()
-    assert scores is not None and tuple(scores.shape) == (batch, p.anchors, 4)
+    assert scores is not None and tuple(scores.shape) == (batch, p.anchors, 8)
     p.static_input().copy_(x)
     rows = p.replay().clone()
     torch.cuda.synchronize()
@@ -225,6 +225,7 @@ def test_scored_filter_from_head_records(oracle, size, batch):
     np.testing.assert_array_equal(rec[..., 2], cls.argmax(-1).astype(np.float32))
     np.testing.assert_array_equal(rec[..., 3], h[..., 4])
     np.testing.assert_array_equal(rec[..., 0], (h[..., 4] * best).astype(np.float32))
+    np.testing.assert_array_equal(rec[..., 4:8], h[..., :4])  # the row's cxcywh box
     side = torch.cuda.Stream()
     for conf in (0.01, 0.3, 0.5):
         want = oracle.postprocess(h.copy(), 80, conf, 0.65)
