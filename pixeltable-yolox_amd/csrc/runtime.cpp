@@ -28,13 +28,17 @@ int check_hip(hipError_t e, const char* what) {
 }
 
 int device_cus() {
-    static std::atomic<int> cache[64];  // 0 = not queried yet
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    int n = cache[dev].load(std::memory_order_relaxed);
+    // queried once per process, on the first launch's device: every conv launch asks, and a
+    // hipGetDevice per launch cost the eager training step (~1 600 launches, host-bound) 1.5-3 ms
+    // of host issue (profiles/r06).  One process drives one GPU model (one process per GPU).
+    static std::atomic<int> cache{0};
+    int n = cache.load(std::memory_order_relaxed);
     if (n == 0) {
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cache[dev].store(n, std::memory_order_relaxed);
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        cache.store(n, std::memory_order_relaxed);
     }
     return n;
 }

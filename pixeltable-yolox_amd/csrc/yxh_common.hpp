@@ -60,7 +60,7 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // Host-side error channel (thread-local message, see runtime.cpp).
 void set_error(const char* fmt, ...);
 int check_hip(hipError_t e, const char* what);
-// compute units of the current device (cached per device; 256 on MI355X): persistent grids
+// compute units of the GPU (queried once per process; 256 on MI355X): persistent grids
 // are sized from it, one block (or BPC blocks) per CU
 int device_cus();
 
