@@ -27,6 +27,11 @@
 #define YXH_WS_PROBE 0
 #endif
 
+// probe builds: the fragment-read distance of the 8-MFMA-step tiles (0 = the default, 1)
+#ifndef YXH_WS_PD8
+#define YXH_WS_PD8 0
+#endif
+
 #ifndef YXH_WS_NPIN
 #define YXH_WS_NPIN 48
 #endif
@@ -125,7 +130,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     static_assert(!F1 || (S == 1 && NW % NG == 0), "fused Bottleneck tile");
     constexpr int FCO = (FC + WK - 1) / WK;  // pixel fragments this wave finishes
     constexpr int NS = WCB * 9;              // K steps per tile (channel block x tap)
-    constexpr int PD = FR * FC >= 8 ? 1 : FR * FC >= 4 ? 2 : 3;  // fragment-read distance in K steps
+    constexpr int PD = YXH_WS_PD8 && FR * FC >= 8 ? YXH_WS_PD8 : FR * FC >= 8 ? 1 : FR * FC >= 4 ? 2 : 3;  // fragment-read distance in K steps
     static_assert(NCB % WK == 0 && WTN % 16 == 0 && WTM % 16 == 0 && TM % (16 * WM) == 0, "tile");
     // weights must stay in VGPRs: 160 of 256 (2 waves per SIMD), 288 of 512 (one 4-wave block per CU)
     static_assert(FR * 9 * WCB * 4 <= (NW == 4 && BPC == 1 ? 288 : 160), "weights must stay in VGPRs");
