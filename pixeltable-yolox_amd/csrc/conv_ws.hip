@@ -36,6 +36,15 @@
 #define YXH_WS_NPIN 48
 #endif
 
+// 1 (default): in the one-wave-per-SIMD tiles the activation is a compile-time property of the tile
+// loop (one copy of the loop for SiLU, one for none, picked once per block), so no epilogue piece
+// branches around its SiLU: the branch split every epilogue step into a basic block of its own, and
+// the SiLU's exp / rcp ran with no MFMA beside them (head level-0 tile 109 -> 102 us).  The 256-register
+// tiles keep the runtime test: a second loop copy spills them
+#ifndef YXH_WS_ACT_CT
+#define YXH_WS_ACT_CT 1
+#endif
+
 namespace yxh {
 
 namespace {
@@ -91,7 +100,6 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     constexpr int HX = (TX - 1) * S + 3, HY = (TY - 1) * S + 3, HXP = ws_hxp(TX, S);
     constexpr int C16 = CIN / 8, PS = ws_ps(C16, S), PSB = PS * 16;
     constexpr int SLOTS = HY * HXP * PS, LOADS = (SLOTS + 63) / 64, GB = (LOADS + NW - 1) / NW;
-    constexpr int HBYTES = LOADS * 1024;
     // partial sums: fragment j of wave group (wn, wm) is finished by wave wk = j % WK; the
     // WK - 1 others each leave their part in a slot of their own
     constexpr int RBYTES = WK > 1 ? WN * WM * FR * FC * (WK - 1) * 1024 : 0;
@@ -123,6 +131,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     // halo-shaped LDS image that the 3x3 then reads; wave w computes t channels
     // 32 (w % NG) .. +32 of every R-th 16-pixel halo fragment
     constexpr int NG = CIN / 32, R1 = NW / NG, NPA = (HY * HXP + 15) / 16;
+    constexpr int HBYTES = LOADS * 1024;
     constexpr int XOFF = 2 * HBYTES + RBYTES + NRING * RTB;
     constexpr int TOFF = XOFF + 3 * XTB;
     constexpr int HWOFF = TOFF + (F1 ? HBYTES : 0);
@@ -353,8 +362,10 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         return EpiCtx{__builtin_amdgcn_make_buffer_rsrc((void*)db, (short)0, (int)dbytes, 0x00020000),
                       smem + 2 * HBYTES + RBYTES + (k % NRING) * RTB, c};
     };
-    // one (pixel fragment o, channel fragment i) piece of the epilogue
-    auto epi_piece = [&](const EpiCtx& e, const f32x4 (&ap)[FR][FCO], const int o, const int i) {
+    // one (pixel fragment o, channel fragment i) piece of the epilogue; act_c: 0 = the runtime
+    // activation, 1 = SiLU, 2 = none (YXH_WS_ACT_CT: fixed for the whole tile loop)
+    auto epi_piece = [&](const EpiCtx& e, const f32x4 (&ap)[FR][FCO], const int o, const int i, auto act_c) {
+        constexpr int AC = decltype(act_c)::value;
         const int j = wk + WK * o;
         const int pl = (wm * FC + j) * 16 + frow;
         const int ty = pl / TX, tx = pl - ty * TX;
@@ -375,7 +386,10 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         T rt[4];
         __builtin_memcpy(rt, &rv, 8);
         const f32x4 x = ap[i][o] + f32x4{bias[i][0], bias[i][1], bias[i][2], bias[i][3]};
-        f32x4 v = silu ? yxh::silu4(x) : x;
+        f32x4 v;
+        if constexpr (AC == 1) v = yxh::silu4(x);
+        else if constexpr (AC == 2) v = x;
+        else v = silu ? yxh::silu4(x) : x;
         if (has_res) v = v + f32x4{to_f32(rt[0]), to_f32(rt[1]), to_f32(rt[2]), to_f32(rt[3])};
         T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
         u32x2 u;
@@ -389,12 +403,12 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             __builtin_amdgcn_raw_buffer_store_b64(u, e.dsrd, od, 0, 0);
         }
     };
-    auto epilogue = [&](const TileC c, const int k, const f32x4 (&ap)[FR][FCO]) {
+    auto epilogue = [&](const TileC c, const int k, const f32x4 (&ap)[FR][FCO], auto act_c) {
         const EpiCtx e = epi_ctx(c, k);
 #pragma unroll
         for (int o = 0; o < FCO; ++o)
 #pragma unroll
-            for (int i = 0; i < FR; ++i) epi_piece(e, ap, o, i);
+            for (int i = 0; i < FR; ++i) epi_piece(e, ap, o, i, act_c);
     };
 
     // Post work of a finished tile whose Y is complete in ring slot k % 3 (and X2 landed), as
@@ -515,7 +529,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
     // one tile: wait for its halo, start tile k+1's halo (+ residual), MMA of tile k with the
     // epilogue of tile k-1 spread over it, then the K-split reduce of tile k into accp
     auto tile_step = [&](const TileC cur, const int tile, const int k, TileC& cnext, const TileC prev,
-                         const TileC prev2, auto epi, auto post, auto first) -> int {
+                         const TileC prev2, auto epi, auto post, auto first, auto act_c) -> int {
         constexpr bool EPI = decltype(epi)::value;
         constexpr bool POST = decltype(post)::value && PGY;
         constexpr bool FIRST = decltype(first)::value;
@@ -627,7 +641,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
             }
             // piece s of the previous tile's epilogue rides on this step's MFMAs
             if constexpr (EPI)
-                if (s < NP) epi_piece(e, accp, s / FR, s % FR);
+                if (s < NP) epi_piece(e, accp, s / FR, s % FR, act_c);
             // ... and piece s of the post work of the tile before that
             // ... and the post work of the tile before that: piece u's operands are read in step
             // u * SP, its MFMAs and stores run in the next step
@@ -648,7 +662,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         }
         if constexpr (EPI)
 #pragma unroll
-            for (int q = NS; q < NP; ++q) epi_piece(e, accp, q / FR, q % FR);
+            for (int q = NS; q < NP; ++q) epi_piece(e, accp, q / FR, q % FR, act_c);
         if constexpr (POST) {
             if (SPLIT && (NS - 1) % SP == 0 && (NS - 1) / SP < NPU) post_math(pc, (NS - 1) / SP, pob);
 #pragma unroll
@@ -692,7 +706,8 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
 
     // the first tile is peeled off the loop: it consumes the weight loads, so the loop body
     // carries no compiler-visible pending load whose wait would also drain the halo DMA
-    int next = tile_step(cur, tile, 0, cnext, cur, cur, std::false_type{}, std::false_type{}, std::true_type{});
+    using act_rt = std::integral_constant<int, 0>;
+    int next = tile_step(cur, tile, 0, cnext, cur, cur, std::false_type{}, std::false_type{}, std::true_type{}, act_rt{});
     // head form: this block's group's pred weights [rows][TN] (rows of RS 16-byte slots) and
     // biases -> LDS once, after the first tile (read from tile 2 on, behind tile 1's barriers);
     // rows past the group's count are zero
@@ -708,25 +723,47 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws(ConvParams p, 
         for (int q = tid; q < HROWS; q += 64 * NW) ((float*)(wl + HROWS * RS * 16))[q] = q < hrows ? hb[q] : 0.0f;
     }
 
-    int k = 1;
-    for (; next < ntiles; ++k) {
-        prev2 = prev;
-        prev = cur;
-        cur = cnext;
-        if (PGY && k >= 2)  // the post pieces of tile k - 2 ride this tile's MFMAs
-            next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::integral_constant<bool, PGY>{}, std::false_type{});
-        else
-            next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::false_type{}, std::false_type{});
-    }
-    if constexpr (PGY) {  // the last tile's residual / X2 landed, the tile before it has its Y
-        dma::wait_vm<0>();
-        dma::barrier();
-        if (k >= 2) post_all(post_ctx(prev, k - 2));
-    }
-    epilogue(cur, k - 1, accp);
-    if constexpr (PGY) {
-        dma::barrier();
-        post_all(post_ctx(cur, k - 1));
+    // YXH_WS_ACT_CT: the tile loop once per activation in the one-wave-per-SIMD plain tiles (the
+    // post / head forms and the 256-register tiles keep the runtime test below: a second copy of
+    // their loop spills)
+    constexpr bool ACT_CT = YXH_WS_ACT_CT && !A32 && !PGY && !F1 && NW == 4 && BPC == 1;
+    if constexpr (ACT_CT) {
+        auto tile_loop = [&](auto act_c) {
+            int k = 1;
+            for (; next < ntiles; ++k) {
+                prev2 = prev;
+                prev = cur;
+                cur = cnext;
+                next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::false_type{}, std::false_type{},
+                                 act_c);
+            }
+            epilogue(cur, k - 1, accp, act_c);
+        };
+        if (silu) tile_loop(std::integral_constant<int, 1>{});
+        else tile_loop(std::integral_constant<int, 2>{});
+    } else {
+        int k = 1;
+        for (; next < ntiles; ++k) {
+            prev2 = prev;
+            prev = cur;
+            cur = cnext;
+            if (PGY && k >= 2)  // the post pieces of tile k - 2 ride this tile's MFMAs
+                next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::integral_constant<bool, PGY>{},
+                                 std::false_type{}, act_rt{});
+            else
+                next = tile_step(cur, next, k, cnext, prev, prev2, std::true_type{}, std::false_type{}, std::false_type{},
+                                 act_rt{});
+        }
+        if constexpr (PGY) {  // the last tile's residual / X2 landed, the tile before it has its Y
+            dma::wait_vm<0>();
+            dma::barrier();
+            if (k >= 2) post_all(post_ctx(prev, k - 2));
+        }
+        epilogue(cur, k - 1, accp, act_rt{});
+        if constexpr (PGY) {
+            dma::barrier();
+            post_all(post_ctx(cur, k - 1));
+        }
     }
     (void)ohw;
 }

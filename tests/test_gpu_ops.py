@@ -760,6 +760,36 @@ def test_conv_ws_3x3(dtype, geom):
     assert ran >= 1
 
 
+@pytest.mark.parametrize("geom", [(128, 128, 1, 40, 40, 4), (64, 64, 1, 37, 45, 3), (160, 160, 1, 40, 38, 2),
+                                  (256, 256, 1, 20, 20, 8)])
+def test_conv_ws_no_activation(geom):
+    """Round 6 (YXH_WS_ACT_CT / YXH_WS1_ACT_CT): the one-wave-per-SIMD conv_ws / conv_ws1 tiles run one
+    copy of their tile loop per activation -- the no-activation copy (the 16-bit training forward's
+    convs, BatchNorm applied after) vs torch fp32, every tile built for this cin, and the SiLU copy
+    of the same tiles on the same input."""
+    cin, cout, s, H, W, B = geom
+    dtype = torch.bfloat16
+    for k in ((3, 1) if cin != 160 else (3,)):
+        conv, bn = make_conv(cin, cout, k, s, seed=cin + cout + k)
+        x = torch.randn(B, cin, H, W, generator=torch.Generator().manual_seed(H + k))
+        tids = (list(range(161, 191)) + list(range(261, 281))) if k == 3 else \
+            (list(range(201, 211)) + list(range(241, 249)) + [253, 254, 255, 257, 258])
+        ran = 0
+        for act in ("none", "silu"):
+            want = ref_conv(x, conv, bn, act)
+            for tid in tids:
+                if tid in WS_WITHDRAWN or tid in {270, 273, 275, 277, 278}:
+                    continue
+                try:
+                    y = run_conv([(nhwc(x, dtype), 0, cin, 0)], conv, bn, dtype, act=act, tile=2 * tid)
+                except NotImplementedError as e:
+                    assert "input channels" in str(e), e
+                    continue
+                close(y.permute(0, 3, 1, 2), want, dtype)
+                ran += 1
+        assert ran >= 2, (geom, k)
+
+
 WS_WIDE_WITHDRAWN = {270, 273, 275, 277, 278}  # spilled (10- / 16-wave blocks): EINVAL
 WS_WIDE_GEOMS = [  # cin, cout, s, H, W (input), batch: yolox_x (80 / 160 / 320) and yolox_l (512) 3x3s
     (80, 80, 1, 35, 41, 2), (80, 160, 2, 66, 70, 2), (160, 160, 1, 40, 38, 2), (160, 320, 2, 42, 38, 2),
