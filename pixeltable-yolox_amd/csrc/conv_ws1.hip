@@ -14,7 +14,10 @@
 
 namespace yxh {
 
-template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC, int NBUF, bool UP0>
+// V16: 16-byte epilogue stores -- channel fragments i and i + 1 of a pixel fragment are exchanged
+// between lane rows by v_permlane16_swap so that every lane holds 8 consecutive channels of its
+// pixel (half the store instructions and offset computations of the 8-byte form)
+template <typename T, int CIN, int TM, int TN, int WN, int WK, int WM, int BPC, int NBUF, bool UP0, bool V16>
 __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p, int ntiles, int ntn, int nwork,
                                                                     int ps, int l0, int l1) {
     static_assert(sizeof(T) == 2, "16-bit operands");
@@ -142,8 +145,48 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
         __builtin_amdgcn_raw_buffer_store_b64(u, dsrd, od, 0, 0);
     };
 
+    // V16: one piece = pixel fragment o x channel fragments 2 ip, 2 ip + 1.  Before the swap lane (frow,
+    // fq) holds channels 4 fq .. +4 of both fragments; v_permlane16_swap trades fragment 2 ip's values
+    // of odd lane rows for fragment 2 ip + 1's of even ones, so row fq ends up with the 8 channels
+    // 16 (fq & 1) + 8 (fq >> 1) .. +8 of the fragment pair (rows 0 / 2: fragment 2 ip, rows 1 / 3: 2 ip + 1)
+    auto epi_piece16 = [&](const int tprev, const f32x4 (&ap)[FR][FCO], const int o, const int ip) {
+        const int j = wk + WK * o;
+        const int i0 = 2 * ip;
+        const int m = tprev * TM + (wm * FC + j) * 16 + frow;
+        const int n = n0 + wn * WTN + i0 * 16 + (fq & 1) * 16 + (fq >> 1) * 8;
+        const bool ok = j < FC && m < M && n < cout;
+        const int od = ok ? (m * dcs + n) * 2 : (int)dma::kOob;
+        uint32_t w[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = i0 + h;
+            const f32x4 x = ap[i][o] + f32x4{bias[i][0], bias[i][1], bias[i][2], bias[i][3]};
+            const f32x4 v = silu ? yxh::silu4(x) : x;
+            T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
+            __builtin_memcpy(w[h], t, 8);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const auto r = __builtin_amdgcn_permlane16_swap(w[0][q], w[1][q], false, false);
+            w[0][q] = r[0];
+            w[1][q] = r[1];
+        }
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 u = {w[0][0], w[0][1], w[1][0], w[1][1]};
+        __builtin_amdgcn_raw_buffer_store_b128(u, dsrd, od, 0, 0);
+    };
+
     f32x4 accp[FR][FCO];
-    constexpr int NP = FR * FCO;
+    static_assert(!V16 || FR % 2 == 0, "16-byte epilogue pairs channel fragments");
+    constexpr int NP = V16 ? FR / 2 * FCO : FR * FCO;  // epilogue pieces
+    constexpr int PFR = V16 ? FR / 2 : FR;             // pieces per pixel fragment
+    // K steps between pieces: a 16-byte piece carries two fragments' epilogue, so it rides every other
+    // step while the K loop has room (the 8-byte pieces: every step)
+    constexpr int PSP = V16 && 2 * NP <= WCB ? 2 : 1;
+    auto piece = [&](const int tprev, const f32x4 (&ap)[FR][FCO], const int q) {
+        if constexpr (V16) epi_piece16(tprev, ap, q / PFR, q % PFR);
+        else epi_piece(tprev, ap, q / FR, q % FR);
+    };
     auto tile_step = [&](const int t, const int k, const int tprev, auto epi, auto first) -> int {
         constexpr bool EPI = decltype(epi)::value;
         constexpr bool FIRST = decltype(first)::value;
@@ -187,7 +230,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
 #pragma unroll
                 for (int i = 0; i < FR; ++i) Mma<T>::run(acc[i][j], a[i][s], bf[s % (PD + 1)][j]);
             if constexpr (EPI)
-                if (s < NP) epi_piece(tprev, accp, s / FR, s % FR);
+                if (s % PSP == 0 && s / PSP < NP) piece(tprev, accp, s / PSP);
             if (s + PD < WCB) __builtin_amdgcn_sched_group_barrier(0x100, FC, 0);
 #pragma unroll
             for (int m = 0; m < FR * FC; ++m) {
@@ -197,7 +240,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
         }
         if constexpr (EPI)
 #pragma unroll
-            for (int q = WCB; q < NP; ++q) epi_piece(tprev, accp, q / FR, q % FR);
+            for (int q = (WCB + PSP - 1) / PSP; q < NP; ++q) piece(tprev, accp, q);
 
         if constexpr (WK > 1) {
             char* red = smem + NBUF * HBYTES;  // past every row buffer (NBUF - 1 tiles are in flight)
@@ -242,9 +285,7 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
         next = tile_step(cur, k, prev, std::true_type{}, std::false_type{});
     }
 #pragma unroll
-    for (int o = 0; o < FCO; ++o)
-#pragma unroll
-        for (int i = 0; i < FR; ++i) epi_piece(cur, accp, o, i);
+    for (int q = 0; q < NP; ++q) piece(cur, accp, q);
     dma::wait_vm<0>();  // the zero-filling DMAs of tiles past the end land before the LDS is released
 }
 
@@ -284,8 +325,13 @@ static int launch_ws1(const ConvParams& p, hipStream_t st) {
     const long long ntiles = (M + TM - 1) / TM;
     const int ntn = (p.cout + TN - 1) / TN;
     const int nwork = (int)std::min<long long>(ntiles, std::max(1, p.cus * BPC / ntn));
-    hipLaunchKernelGGL((conv_ws1<T, CIN, TM, TN, WN, WK, WM, BPC, NBUF, UP0>), dim3((unsigned)(nwork * ntn)),
-                       dim3(64 * WN * WK * WM), 0, st, p, (int)ntiles, ntn, nwork, ps, l0, l1);
+    constexpr bool PAIRS = (TN / WN / 16) % 2 == 0;  // channel fragments per wave even: 16-byte stores
+    if (PAIRS && p.vec16)  // (conv.hip: set for the odd tile codes only)
+        hipLaunchKernelGGL((conv_ws1<T, CIN, TM, TN, WN, WK, WM, BPC, NBUF, UP0, PAIRS>), dim3((unsigned)(nwork * ntn)),
+                           dim3(64 * WN * WK * WM), 0, st, p, (int)ntiles, ntn, nwork, ps, l0, l1);
+    else
+        hipLaunchKernelGGL((conv_ws1<T, CIN, TM, TN, WN, WK, WM, BPC, NBUF, UP0, false>), dim3((unsigned)(nwork * ntn)),
+                           dim3(64 * WN * WK * WM), 0, st, p, (int)ntiles, ntn, nwork, ps, l0, l1);
     YXH_CHECK_LAUNCH("conv_ws1 launch");
     return YXH_OK;
 }

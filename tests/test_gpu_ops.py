@@ -1128,18 +1128,27 @@ def test_conv_ws1_1x1(dtype, geom):
     want = ref_conv(torch.cat(parts, 1), conv, bn, "silu")
     out = torch.zeros(B, H, W, cout + 16, dtype=dtype, device=DEV)
     ran = 0
+    # odd codes (round 6): the same tiles with the 16-byte-store epilogue (v_permlane16_swap pairs of channel
+    # fragments): bit-identical to the 8-byte form
     for tid in list(range(201, 211)) + list(range(241, 249)) + [253, 254, 255, 257, 258]:
-        try:
-            y = run_conv(bufs, conv, bn, dtype, out=out, out_coff=8, tile=2 * tid)
-        except NotImplementedError as e:
-            assert "input channels" in str(e), e
-            continue
-        close(y[..., 8:8 + cout].permute(0, 3, 1, 2), want, dtype)
-        assert not y[..., :8].any() and not y[..., 8 + cout:].any()
-        y = y.clone()
-        yf = run_conv(bufs, conv, bn, dtype, out=out, out_coff=8, tile=2 * tid, frag=True)
-        assert torch.equal(yf, y), tid
-        ran += 1
+        y8 = None
+        for code in (2 * tid, 2 * tid + 1):
+            out.zero_()
+            try:
+                y = run_conv(bufs, conv, bn, dtype, out=out, out_coff=8, tile=code)
+            except NotImplementedError as e:
+                assert "input channels" in str(e), e
+                continue
+            close(y[..., 8:8 + cout].permute(0, 3, 1, 2), want, dtype)
+            assert not y[..., :8].any() and not y[..., 8 + cout:].any()
+            y = y.clone()
+            yf = run_conv(bufs, conv, bn, dtype, out=out, out_coff=8, tile=code, frag=True)
+            assert torch.equal(yf, y), code
+            if y8 is None:
+                y8 = y
+            else:
+                assert torch.equal(y, y8), code
+            ran += 1
     assert ran >= 1
 
 

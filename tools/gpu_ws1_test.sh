@@ -1,0 +1,9 @@
+#!/bin/bash
+# GPU box: the 1x1 / 3x3 weight-stationary op tests against a dbg library ($LIB), then stop on failure
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+YOLOX_AMD_LIB=$PWD/$LIB timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -m gpu -x -q --timeout 200 \
+    --timeout-method thread -k "${K:-ws1 or no_activation or pw}" > gpurun_out/ops_$TAG.log 2>&1
+rc=$?
+tail -3 gpurun_out/ops_$TAG.log
+exit $rc
