@@ -660,10 +660,11 @@ int conv2d(const yxh_conv_desc* d, hipStream_t st) {
     const int kstage = 4 * ks * epc;
     p.ncb = (d->cin + kstage - 1) / kstage;
     if (tile > 260) return conv_ws_dispatch(dt, tile - 260 + 60, p, st);
-    // conv_ws1 (tiles 201-210, 241-258): the slab bit selects the 16-byte-store epilogue (conv_ws1.hip V16,
-    // where the destination rows allow it); the autotuner times both codes
+    // conv_ws1 (tiles 201-210, 241-258): the slab bit selects the 16-byte-store epilogue (conv_ws1.hip V16, where
+    // the destination rows allow it; tiles without it refuse the odd code); the autotuner times both codes.  (The
+    // same epilogue in conv_ws measured neutral on the bench and was dropped)
     if ((tile > 240 && tile <= 240 + kNumWs1DeepTiles) || (tile > 200 && tile <= 200 + kNumWs1Tiles))
-        p.vec16 = p.vec16 && ks == 2;
+        p.v16_req = ks == 2;
     if (tile > 240) return conv_ws1_dispatch(dt, tile - 240 + kNumWs1Tiles, p, st);
     if (tile > 220) return conv_ws_dispatch(dt, tile - 220 + 40, p, st);
     if (tile > 214) return dgrad_s2f_dispatch(dt, tile - 214, p, st);

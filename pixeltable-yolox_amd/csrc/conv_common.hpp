@@ -21,6 +21,7 @@ struct ConvParams {
     long long dst_bs;
     int dst_f32, act, dcoff, vec_store, vec_res;
     int vec16;  // dst rows 16-byte aligned and cout a chunk multiple: LDS-staged epilogue
+    int v16_req;  // conv_ws / conv_ws1: the 16-byte-store epilogue was asked for (odd tile code)
     int accum;  // f32 dst += result (YXH_CONV_ACCUMULATE: data-gradient accumulation)
     // image stride == pixels x pixel stride: pixel m lives at m * cs, no (b, pix) split
     // (the integer divides were most of a 1x1 conv's VALU work: tools/gpu_pmc.sh)

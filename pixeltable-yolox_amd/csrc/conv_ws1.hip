@@ -326,7 +326,11 @@ static int launch_ws1(const ConvParams& p, hipStream_t st) {
     const int ntn = (p.cout + TN - 1) / TN;
     const int nwork = (int)std::min<long long>(ntiles, std::max(1, p.cus * BPC / ntn));
     constexpr bool PAIRS = (TN / WN / 16) % 2 == 0;  // channel fragments per wave even: 16-byte stores
-    if (PAIRS && p.vec16)  // (conv.hip: set for the odd tile codes only)
+    if (p.v16_req && !PAIRS) {
+        set_error("conv_ws1 tile has no 16-byte epilogue (an odd number of channel fragments per wave)");
+        return YXH_EUNSUPPORTED;
+    }
+    if (PAIRS && p.v16_req && p.vec16)  // (conv.hip: v16_req = the odd tile codes)
         hipLaunchKernelGGL((conv_ws1<T, CIN, TM, TN, WN, WK, WM, BPC, NBUF, UP0, PAIRS>), dim3((unsigned)(nwork * ntn)),
                            dim3(64 * WN * WK * WM), 0, st, p, (int)ntiles, ntn, nwork, ps, l0, l1);
     else

@@ -1137,7 +1137,7 @@ def test_conv_ws1_1x1(dtype, geom):
             try:
                 y = run_conv(bufs, conv, bn, dtype, out=out, out_coff=8, tile=code)
             except NotImplementedError as e:
-                assert "input channels" in str(e), e
+                assert "input channels" in str(e) or "16-byte epilogue" in str(e), e
                 continue
             close(y[..., 8:8 + cout].permute(0, 3, 1, 2), want, dtype)
             assert not y[..., :8].any() and not y[..., 8 + cout:].any()
