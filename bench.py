@@ -338,9 +338,11 @@ def main_train(args, world, rank):
 
     for _ in range(args.warmup):
         out = step()
-    # YOLOX_AMD_TRAIN_GRAPH=1: the forward + reverse pass replays as hipGraph segments (under DDP the
-    # reducer's bucket all-reduces are issued between the replayed segments, CapturedTrainStep)
-    if args.warmup >= 1 and os.environ.get("YOLOX_AMD_TRAIN_GRAPH", "0") == "1":
+    # the forward + reverse pass replays as hipGraph segments (under DDP the reducer's bucket all-reduces
+    # are issued between the replayed segments, CapturedTrainStep); YOLOX_AMD_TRAIN_GRAPH=0: the eager
+    # step.  Default since round 6: on the GPU boxes of that round the eager step's host issue (16.5-17 ms
+    # per configs[2] step) outran the GPU, captured 534 vs eager 467-475 img/s (configs[4]: 105.6 vs 98.2)
+    if args.warmup >= 1 and os.environ.get("YOLOX_AMD_TRAIN_GRAPH", "1") == "1":
         from yolox_amd.train import CapturedTrainStep
         opt.zero_grad(set_to_none=True)
         cap = CapturedTrainStep(model, imgs, labels, dtype=amp or torch.float32,
@@ -351,6 +353,13 @@ def main_train(args, world, rank):
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     barrier(world)
     torch.cuda.synchronize()
+    # diagnostic (BENCH_HOST_PROFILE=<file>): cProfile of the host side of the timed steps, for the eager
+    # step's issue path (configs[2] is host-issue-bound); the timed numbers of such a run are not reported
+    prof = None
+    if os.environ.get("BENCH_HOST_PROFILE") and rank == 0:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     host_s = 0.0  # time the host spends issuing a step (ctypes launches + tensor bookkeeping)
     for k in range(args.steps):
@@ -359,6 +368,9 @@ def main_train(args, world, rank):
         out = step()
         host_s += time.perf_counter() - h0
         evs[k][1].record(stream)
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(os.environ["BENCH_HOST_PROFILE"])
     torch.cuda.synchronize()
     barrier(world)
     dt = time.perf_counter() - t0
