@@ -1,4 +1,4 @@
-# round 6: headline bench + profile (trace, timeline, reconciled PMC traffic, SQ), then the training
+# headline bench + profile (trace, timeline, reconciled PMC traffic, SQ), then (TRAIN=1) the training
 # configs: configs[2] (yolox_s fp32 bs 8) eager, configs[4] (yolox_x 1280 --fp16 bs 8) eager and captured
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp

@@ -1,4 +1,4 @@
-# round 6: the whole GPU suite + smoke() on the current tree
+# the whole GPU suite + smoke() on the current tree (TAG names the logs)
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
