@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 T=${TAG:-hostprof}
-BENCH_HOST_PROFILE=gpurun_out/host_$T.pstats timeout -k 10 400 python -u bench.py --workload train --steps 10 --warmup 5 \
+YOLOX_AMD_TRAIN_GRAPH=0 BENCH_HOST_PROFILE=gpurun_out/host_$T.pstats timeout -k 10 400 python -u bench.py --workload train --steps 10 --warmup 5 \
     --no-cpu-baseline $ARGS > gpurun_out/host_$T.json 2> gpurun_out/host_$T.err || { tail -5 gpurun_out/host_$T.err; exit 1; }
 python -c "
 import pstats, sys
