@@ -107,7 +107,10 @@ typedef struct {
                             (TN x TM) of the register-staged kernel, id 17-25 the same
                             tiles on the LDS-DMA kernel, id 33-51 the row-tiled 3x3
                             kernel, id 65-70 the persistent streaming 1x1 kernel;
-                            chosen by the planner's on-device autotune                   */
+                            for the weight-stationary 1x1 ids 201-210 / 241-258 the low
+                            bit instead selects the 16-byte-store epilogue (round 6; a
+                            tile without it refuses the odd code); chosen by the
+                            planner's on-device autotune                                 */
     int32_t flags;       /* YXH_CONV_ACCUMULATE: f32 dst += result (gradient accumulation) */
     int32_t grid_cap;    /* 0, or the CUs the persistent tiles (conv_ws / conv_ws1 / conv_pwf) may occupy: a
                             graph lane running beside another lane's work leaves it the rest of the chip */
