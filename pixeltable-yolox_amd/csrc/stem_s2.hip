@@ -293,11 +293,12 @@ __global__ __launch_bounds__(256, 2) void stem_s2(Stem2Params p, int tiles_x, in
                 for (int i = 0; i < 2; ++i) {
                     const f32x4 y =
                         yxh::silu4(acc[i][jj] + f32x4{bias1[i][0], bias1[i][1], bias1[i][2], bias1[i][3]});
-                    T t[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) t[r] = from_f32<T>(valid ? y[r] : 0.0f);
-                    uint2 u;
-                    __builtin_memcpy(&u, t, 8);
+                    // two paired conversions, then the zero padding selected on the packed pairs (a 16-bit +0
+                    // is all-zero bits, as from_f32(0.0f)): selecting before converting made the compiler
+                    // convert each value alone and re-pack the halves (10 VALU per 4 values instead of 4)
+                    uint2 u = pack4<T>(y);
+                    u.x = valid ? u.x : 0u;
+                    u.y = valid ? u.y : 0u;
                     if (pix < kS2NSP) *(uint2*)(simg + (sy * HXP + sx) * PSB + (i * 16 + fq * 4) * 2) = u;
                 }
             }

@@ -47,6 +47,18 @@ __device__ __forceinline__ f32x4 silu4(f32x4 v) {
     return v * r;
 }
 
+// four fp32 values -> four 16-bit values packed in two dwords by two v_cvt_pk_{bf16,f16}_f32 (the same
+// round-to-nearest-even as from_f32; written per element, the compiler sometimes converted each value
+// alone and re-packed the halves with v_perm / shifts)
+template <typename T>
+__device__ __forceinline__ uint2 pack4(f32x4 v) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef T t16x2 __attribute__((ext_vector_type(2)));
+    const t16x2 a = __builtin_convertvector((f32x2{v[0], v[1]}), t16x2);
+    const t16x2 b = __builtin_convertvector((f32x2{v[2], v[3]}), t16x2);
+    return make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
+}
+
 template <bool PRECISE = false>
 __device__ __forceinline__ float apply_act(float v, int act) {
     switch (act) {
