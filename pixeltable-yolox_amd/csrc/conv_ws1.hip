@@ -161,9 +161,9 @@ __global__ __launch_bounds__(64 * WN * WK * WM, BPC) void conv_ws1(ConvParams p,
         for (int h = 0; h < 2; ++h) {
             const int i = i0 + h;
             const f32x4 x = ap[i][o] + f32x4{bias[i][0], bias[i][1], bias[i][2], bias[i][3]};
-            const f32x4 v = silu ? yxh::silu4(x) : x;
-            T t[4] = {from_f32<T>(v[0]), from_f32<T>(v[1]), from_f32<T>(v[2]), from_f32<T>(v[3])};
-            __builtin_memcpy(w[h], t, 8);
+            const uint2 pk = pack4<T>(silu ? yxh::silu4(x) : x);  // two paired conversions
+            w[h][0] = pk.x;
+            w[h][1] = pk.y;
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
