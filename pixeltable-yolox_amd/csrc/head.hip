@@ -189,7 +189,11 @@ __global__ __launch_bounds__(256) void head_pred(yxh_head_desc d) {
 //    the contiguous output rows -- no block barrier after the prologue.
 // Same MFMA order and decode arithmetic as head_pred: bit-identical output
 // (tests/test_gpu_ops.py test_head_pred_fused_level runs both).
-template <typename T, int CIN, int NCF>
+// MODE = yxh_head_desc.train, fixed per instantiation (0: eval decode, 1: training rows -- decoded boxes, raw
+// obj / cls logits, 2: eval raw rows -- raw boxes, sigmoid obj / cls): the decode is branch-free (every lane
+// evaluates its fragment-0 candidates and selects; 32-bit pixel / image arithmetic), where the runtime mode
+// tests and per-lane branches had split it into exec-masked blocks with SGPR spills (round 6)
+template <typename T, int CIN, int NCF, int MODE>
 __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
     constexpr int NW = 8;
     constexpr int KS = CIN / 32;                 // K steps
@@ -205,11 +209,11 @@ __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int frow = lane & 15, fq = lane >> 4;
-    const int C = d.num_classes, hw = d.h * d.w, rowf = 5 + C;
-    const long long M = (long long)d.batch * hw;
-    const long long G = (M + 15) / 16;
-    const long long gstride = (long long)gridDim.x * NW;
-    long long g = (long long)blockIdx.x * NW + wave;
+    const int C = d.num_classes, hw = d.h * d.w, rowf = 5 + C, W = d.w;
+    const int M = d.batch * hw;  // < 2^31 (head_pred_launch)
+    const int G = (M + 15) / 16;
+    const int gstride = (int)gridDim.x * NW;
+    int g = (int)blockIdx.x * NW + wave;
     // ---- weights / biases -> LDS (rows past 5 reg|obj and C cls rows are zero), then VGPRs
     for (int q = tid; q < WROWS * (CIN / 8); q += 64 * NW) {
         const int r = q / (CIN / 8), c = q - (CIN / 8) * (q / (CIN / 8));
@@ -229,10 +233,10 @@ __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
     if (g >= G) return;  // wave-uniform; no block barrier follows
 
     // B operands of group g: [0..KS) reg features, [KS..2KS) cls features of pixel 16 g + frow
-    auto load_b = [&](long long gg, uint4 (&b)[2 * KS]) {
-        long long m = gg * 16 + frow;
+    auto load_b = [&](int gg, uint4 (&b)[2 * KS]) {
+        int m = gg * 16 + frow;
         m = m < M ? m : M - 1;
-        const int bi = (int)(m / hw), pix = (int)(m - (long long)bi * hw);
+        const int bi = m / hw, pix = m - bi * hw;
         const T* pr = (const T*)d.reg.ptr + (long long)bi * d.reg.bstride + (long long)pix * d.reg.cstride + fq * 8;
         const T* pc = (const T*)d.cls.ptr + (long long)bi * d.cls.bstride + (long long)pix * d.cls.cstride + fq * 8;
 #pragma unroll
@@ -256,40 +260,40 @@ __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
 #pragma unroll
             for (int f = 0; f < NF; ++f) Mma<T>::run(acc[f], wr[f][s], f == 0 ? bc[s] : bc[KS + s]);
         // ---- bias + decode -> this wave's staging rows (row = frow, the group's pixel)
-        const long long m0 = g * 16;
-        long long m = m0 + frow;
+        const int m0 = g * 16;
+        int m = m0 + frow;
         m = m < M ? m : M - 1;
-        const int pix = (int)(m - (m / hw) * hw);
-        const int gy = pix / d.w, gx = pix - gy * d.w;
+        const int img = m / hw, pix = m - img * hw;
+        const int gy = pix / W, gx = pix - gy * W;
         float* row = stg + frow * rowf;
         // serving score records (ABI 18): this lane's classes (f - 1) * 16 + fq * 4 + r, in increasing
         // order, scanned as postprocess.hip's filter scans a row (class 0 -- lane fq 0 -- starts the
         // scan even when NaN, every later class replaces only on a strict '>'), from the very values
         // the row gets
         float cbest = -INFINITY, objv = 0.0f;
-        float boxv[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // ch 0-3 (lane fq 0): the decoded box, copied into the record
+        float boxv[4];  // ch 0-3 (lane fq 0): the decoded box, copied into the record
         int cbi = C;
+        // fragment 0: lane row fq 0 holds ch 0-3 (the box), fq 1 ch 4 (obj); every lane evaluates both
+        // candidates of its values and selects (the same arithmetic as the branchy form: bit-identical)
 #pragma unroll
-        for (int f = 0; f < NF; ++f) {
+        for (int r = 0; r < 4; ++r) {
+            const int ch = fq * 4 + r;
+            const float v = acc[0][r] + bl[ch];
+            float bx = v;
+            if constexpr (MODE != 2) bx = r < 2 ? (v + (float)(r == 0 ? gx : gy)) * st : hd_exp(v) * st;
+            const float ob = MODE == 1 ? v : hd_sigmoid(v);
+            boxv[r] = bx;
+            if (r == 0) objv = ob;  // lane row fq 1: ch 4
+            if (ch < 5) row[ch] = ch < 4 ? bx : ob;
+        }
+#pragma unroll
+        for (int f = 1; f < NF; ++f) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int ch = f * 16 + fq * 4 + r;
-                float v = acc[f][r];
-                if (f == 0) {
-                    if (ch < 5) {
-                        v += bl[ch];
-                        if (ch < 4) {
-                            if (d.train != 2) v = ch < 2 ? (v + (float)(ch == 0 ? gx : gy)) * st : hd_exp(v) * st;
-                            boxv[r] = v;
-                        } else {
-                            v = d.train == 1 ? v : hd_sigmoid(v);
-                            objv = v;
-                        }
-                        row[ch] = v;
-                    }
-                } else if (ch - 16 < C) {
-                    v += bl[ch];
-                    const float sv = d.train == 1 ? v : hd_sigmoid(v);
+                const float v = acc[f][r] + bl[ch];
+                const float sv = MODE == 1 ? v : hd_sigmoid(v);
+                if (ch - 16 < C) {
                     row[5 + ch - 16] = sv;
                     if (ch == 16 || sv > cbest) {
                         cbest = sv;
@@ -313,19 +317,18 @@ __global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
                 if (take) { cbest = ob; cbi = oi; }
             }
             const float obj = __shfl(objv, frow + 16);  // ch 4 (obj) lives in lane fq = 1
-            const long long mr = g * 16 + frow;
+            const int mr = m0 + frow;
             if (fq == 0 && mr < M) {
-                const long long img = mr / hw;
-                float4* rec = (float4*)(d.scores + 8 * (img * (d.out_bstride / rowf) + d.a_off + (mr - img * hw)));
+                float4* rec = (float4*)(d.scores + 8 * ((long long)img * (d.out_bstride / rowf) + d.a_off + pix));
                 rec[0] = make_float4(obj * cbest, cbest, (float)cbi, obj);
                 rec[1] = make_float4(boxv[0], boxv[1], boxv[2], boxv[3]);
             }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): every lane's rows are in LDS
         __builtin_amdgcn_wave_barrier();
-        const int n = (int)(M - m0 < 16 ? M - m0 : 16);
+        const int n = M - m0 < 16 ? M - m0 : 16;
         // ---- the group's rows are contiguous in the output (split once at an image boundary)
-        int t0 = 0, bi = (int)(m0 / hw), p0 = (int)(m0 - (long long)bi * hw);
+        int t0 = 0, bi = m0 / hw, p0 = m0 - bi * hw;
         while (t0 < n) {
             const int cnt = min(n - t0, hw - p0);
             float* dst = d.out + (long long)bi * d.out_bstride + (long long)(d.a_off + p0) * rowf;
@@ -379,7 +382,12 @@ int head_pred_launch(const yxh_head_desc* d, hipStream_t st) {
     if (!v1 && rows16 && (d->cin == 64 || d->cin == 128)) {
         const long long groups = (M + 15) / 16;
         const unsigned grid2 = (unsigned)std::min<long long>((groups + 7) / 8, device_cus());  // one 8-wave block per CU
-#define YXH_HEAD2(T, CIN) hipLaunchKernelGGL((head_pred2<T, CIN, 5>), dim3(grid2), dim3(512), 0, st, *d)
+#define YXH_HEAD2(T, CIN)                                                                           \
+    do {                                                                                            \
+        if (d->train == 1) hipLaunchKernelGGL((head_pred2<T, CIN, 5, 1>), dim3(grid2), dim3(512), 0, st, *d); \
+        else if (d->train == 2) hipLaunchKernelGGL((head_pred2<T, CIN, 5, 2>), dim3(grid2), dim3(512), 0, st, *d); \
+        else hipLaunchKernelGGL((head_pred2<T, CIN, 5, 0>), dim3(grid2), dim3(512), 0, st, *d);    \
+    } while (0)
         if (d->dtype == YXH_BF16 && d->cin == 128) YXH_HEAD2(bf16, 128);
         else if (d->dtype == YXH_BF16) YXH_HEAD2(bf16, 64);
         else if (d->dtype == YXH_F16 && d->cin == 128) YXH_HEAD2(f16, 128);
