@@ -197,7 +197,9 @@ class TrainGraph:
         self._scratch_side = torch.empty(0, dtype=torch.uint8, device=self.device)
         self._wpending: list = []
         self._segcap = None  # CapturedTrainStep's segment recorder while it captures
-        self.wgrad_group = max(1, int(os.environ.get("YOLOX_AMD_WGRAD_GROUP", "1")))
+        # weight-gradient convs per side-stream fork (YOLOX_AMD_WGRAD_GROUP; round 6: 3 -- the captured configs[2]
+        # step 535-536 -> 543-546 img/s over three alternating A/Bs (fewer cross-stream edges), configs[4] neutral)
+        self.wgrad_group = max(1, int(os.environ.get("YOLOX_AMD_WGRAD_GROUP", "3")))
         # weight repacks: the first step launches one pack per conv (forward layout) and per
         # data-gradient input slice, recording each as a yxh_pack_job; later steps repack
         # everything in ONE yxh_pack_weights_batch launch at the start of the forward
