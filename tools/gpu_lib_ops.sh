@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU box: the 1x1 / 3x3 weight-stationary op tests against a dbg library ($LIB), then stop on failure
+# GPU box: tests/test_gpu_ops.py (-k $K) against an alternative library build ($LIB, YOLOX_AMD_LIB); non-zero on failure
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 YOLOX_AMD_LIB=$PWD/$LIB timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -m gpu -x -q --timeout 200 \
