@@ -109,6 +109,8 @@ def parse():
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise only the process topology (spawn, rendezvous, barrier, max over ranks) "
                          "with gloo on the CPU; prints one JSON line from rank 0")
+    ap.add_argument("--refine-tiles", action="store_true",
+                    help="after the per-op autotune, re-time close runner-up tiles inside the captured forward")
     ap.add_argument("--layers", action="store_true", help="print a per-op time/roofline table to stderr")
     ap.add_argument("--tune-file", default="", help="JSON tile choices: loaded if present (skips tuning), else written")
     ap.add_argument("--workload", default="infer", choices=["infer", "train"],
@@ -489,6 +491,12 @@ def main():
         engine.load_tune_cache(args.tune_file)
     t_tune = time.perf_counter()
     plan.autotune(verbose=args.layers and rank == 0)
+    if args.refine_tiles:  # second pass: runner-up tiles timed inside the captured forward
+        changed = plan.refine_in_graph(verbose=args.layers and rank == 0)
+        if rank == 0:
+            for (old, new, ma, mb) in changed.values():
+                print(f"refine: tile {old >> 1}/{(old & 1) + 1} -> {new >> 1}/{(new & 1) + 1}: forward "
+                      f"{ma * 1e3:.1f} -> {mb * 1e3:.1f} us", file=sys.stderr)
     t_tune = time.perf_counter() - t_tune
     if args.tune_file and rank == 0 and not os.path.exists(args.tune_file):
         engine.save_tune_cache(args.tune_file)

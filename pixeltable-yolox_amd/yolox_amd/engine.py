@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import statistics
 import sys
 from dataclasses import dataclass, field
 from typing import Optional
@@ -473,6 +474,7 @@ _TUNE_ALL_FAMILIES = os.environ.get("YOLOX_AMD_TUNE_ALL_FAMILIES", "0") == "1"
 # level forked early (YOLOX_AMD_GRAPH=streams) leaves the rest of the chip to the neck it runs beside
 _LANE_CUS = {int(k): int(v) for k, v in (e.split(":") for e in os.environ.get("YOLOX_AMD_LANE_CUS", "").split(",") if e)}
 _TUNE_CACHE: dict = {}
+_TUNE_TIMES: dict = {}  # shape key -> [(isolated ms, tile)] of every applicable candidate, fastest first
 _TUNE_ALL = os.environ.get("YOLOX_AMD_TUNE_ALL", "0") == "1"  # print every variant's time
 
 
@@ -1313,7 +1315,7 @@ class Plan:
                 op.u.conv.tile = _TUNE_CACHE[key]
                 chosen[i] = _TUNE_CACHE[key]
                 continue
-            best = (float("inf"), 0)
+            best, times = (float("inf"), 0), []
             ptr = C.pointer(op)
             cands = (TILE_CANDIDATES if self.dtype == torch.float32 or _TUNE_ALL_FAMILIES else TILE_CANDIDATES_16)
             for tile in cands:
@@ -1338,10 +1340,12 @@ class Plan:
                         t += ev0.elapsed_time(ev1) / reps
                 if _TUNE_ALL:
                     print(f"  op {i} tile {tile >> 1} slabs {(tile & 1) + 1}: {t * 1e3:.1f} us", file=sys.stderr)
+                times.append((t, tile))
                 if t < best[0]:
                     best = (t, tile)
             op.u.conv.tile = best[1]
             _TUNE_CACHE[key] = best[1]
+            _TUNE_TIMES[key] = sorted(times)
             chosen[i] = best[1]
             if verbose:
                 a = rec.args
@@ -1354,6 +1358,72 @@ class Plan:
         if self._graph is not None or self._segments is not None:  # captured graphs hold the old tiles
             self.capture(2 if self._graph_alt is not None else 1)
         return chosen
+
+    def refine_in_graph(self, margin: float = 0.15, alts: int = 2, reps: int = 50, trials: int = 3,
+                        min_gain: float = 0.002, verbose: bool = False) -> dict:
+        """Second tuning pass, inside the captured forward.  autotune() times each conv alone,
+        five times back to back on warm caches; in the forward a launch meets the L2 state its
+        producer left and, on the head lanes, shares the CUs with another level.  For every conv
+        shape (in forward order) whose runner-up tiles timed within ``margin`` of the best alone,
+        the whole forward is replayed with the chosen tile and with each of up to ``alts``
+        runner-ups, ``trials`` alternating A/B rounds of ``reps`` replays each, and a runner-up
+        replaces the choice only if the median forward drops by more than ``min_gain``
+        (a fraction).  Changes go into the per-shape cache like autotune's (save_tune_cache
+        writes them).  Returns {shape key: (old tile, new tile, old ms, new ms)}."""
+        sites = {}  # shape key -> indices of the first chunk's ops with that shape
+        for i, rec in enumerate(self.ctx.ops):
+            if rec.kind == N.OP_CONV and rec.args["groups"] == 1:
+                key = _tune_key(self._ops[i].u.conv)
+                if key in _TUNE_TIMES:
+                    sites.setdefault(key, []).append(i)
+        had_graph = self._graph is not None or self._segments is not None
+        stream = torch.cuda.current_stream(self.device)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+        def set_tile(key, tile):
+            for c in range(self.nchunks):
+                for i in sites[key]:
+                    self._ops[c * self._nops + i].u.conv.tile = tile
+
+        def forward_ms(key, tile):
+            set_tile(key, tile)
+            self.capture(1)
+            for _ in range(3):
+                self.replay()
+            ev0.record(stream)
+            for _ in range(reps):
+                self.replay()
+            ev1.record(stream)
+            ev1.synchronize()
+            return ev0.elapsed_time(ev1) / reps
+
+        changed = {}
+        for key, idx in sites.items():
+            cur = self._ops[idx[0]].u.conv.tile
+            times = _TUNE_TIMES[key]
+            t_cur = next((t for t, tile in times if tile == cur), times[0][0])
+            cands = [tile for t, tile in times if tile != cur and t <= t_cur * (1 + margin)][:alts]
+            for alt in cands:
+                ta, tb = [], []
+                for _ in range(trials):
+                    ta.append(forward_ms(key, cur))
+                    tb.append(forward_ms(key, alt))
+                ma, mb = statistics.median(ta), statistics.median(tb)
+                if verbose:
+                    a = self.ctx.ops[idx[0]].args
+                    print(f"refine k{a['k']}s{a['stride']} {a['cin']}->{a['cout']} @{a['out_h']}x{a['out_w']}: tile "
+                          f"{cur >> 1}/{(cur & 1) + 1} {ma * 1e3:.1f} us vs {alt >> 1}/{(alt & 1) + 1} {mb * 1e3:.1f} us",
+                          file=sys.stderr)
+                if mb < ma * (1 - min_gain):
+                    changed[key] = (changed.get(key, (cur,))[0], alt, ma, mb)
+                    cur = alt
+            set_tile(key, cur)
+            _TUNE_CACHE[key] = cur
+        self._destroy_graphs()
+        torch.cuda.synchronize(self.device)
+        if had_graph:
+            self.capture(1)
+        return changed
 
     # -------------------------------------------------------------- reporting
     def conv_ops(self):

@@ -118,6 +118,45 @@ def test_autotuned_plan_matches_default(golden):
     assert torch.allclose(a, b, rtol=1e-4, atol=1e-4)
 
 
+def test_refine_in_graph_keeps_output_and_cache():
+    """The in-graph refinement pass (bench --refine-tiles): with min_gain < -1 every close runner-up
+    is taken, so the switch path runs for each shape that has one; the plan's conv ops then carry
+    the per-shape cache's tiles, the captured replay equals an eager run, and the output still
+    matches the heuristic plan's up to summation order."""
+    from yolox_amd import _native as N
+    from yolox_amd import engine
+    m = model("yolox_s")
+    from yolox_amd.weights import synthetic_images
+    x = torch.from_numpy(synthetic_images(2, 128, 128, seed=5)).cuda()
+    plan = m.plan_for(2, 128, 128, N.NHWC, torch.uint8)
+    a = plan.run(x).clone()
+    plan.static_input().copy_(x)
+    saved = dict(engine._TUNE_CACHE)
+    try:
+        plan.autotune(reps=1)
+        changed = plan.refine_in_graph(margin=1.0, alts=1, reps=1, trials=1, min_gain=-2.0)
+        _check_refined(plan, changed, engine, x, a)
+    finally:  # the taken runner-ups are arbitrary: later tests tune from the cache as it was
+        engine._TUNE_CACHE.clear()
+        engine._TUNE_CACHE.update(saved)
+
+
+def _check_refined(plan, changed, engine, x, a):
+    assert changed, "no shape had a runner-up tile"
+    assert plan._graph is None and plan._segments is None  # left uncaptured, as it found the plan
+    for _, d in plan.conv_ops():
+        key = engine._tune_key(d)
+        if key in engine._TUNE_TIMES:
+            assert d.tile == engine._TUNE_CACHE[key]
+    for old, new, _, _ in changed.values():
+        assert old != new
+    b = plan.run(x).clone()
+    plan.static_input().copy_(x)
+    c = plan.replay().clone()
+    assert torch.equal(b, c)
+    assert torch.allclose(a, b, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_fused_stem_plan_matches_focus_plan(golden, dtype):
     """The fused Focus+stem op (default) and the two-op path (yxh_focus_pack + conv)
