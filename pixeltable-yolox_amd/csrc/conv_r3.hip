@@ -254,7 +254,7 @@ __device__ __forceinline__ void r3_wait_dyn(int n) {
 #define YXH_W(k) \
     case k: dma::wait_vm<k>(); break;
         YXH_W(1) YXH_W(2) YXH_W(3) YXH_W(4) YXH_W(5) YXH_W(6) YXH_W(7) YXH_W(8) YXH_W(9) YXH_W(10)
-        YXH_W(11) YXH_W(12) YXH_W(13) YXH_W(14) YXH_W(15)
+        YXH_W(11) YXH_W(12) YXH_W(13) YXH_W(14) YXH_W(15) YXH_W(16) YXH_W(17) YXH_W(18) YXH_W(19) YXH_W(20)
 #undef YXH_W
         default: dma::wait_vm<0>(); break;
     }
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void conv_r3h(ConvParams p, int tile
     constexpr int A_PART = A_LOADS % NW, B_PART = B_LOADS % NW;
     constexpr int ABUF = A_LOADS * 1024, BBUF = B_LOADS * 1024;
     constexpr int SMEM = 3 * ABUF + 2 * BBUF;
-    static_assert(A_SLOTS % 64 == 0 && TM % (16 * WM) == 0 && GA + GB <= 15, "tile");
+    static_assert(A_SLOTS % 64 == 0 && TM % (16 * WM) == 0 && GA + GB <= 20, "tile");
     static_assert(SMEM <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -525,6 +525,10 @@ static int r3_dispatch_t(int id, const ConvParams& p, hipStream_t st) {
         case 36: return launch_r3h<T, 1, 16, 16, 128, 8, 2>(p, st);
         case 37: return launch_r3h<T, 1, 32, 16, 64, 16>(p, st);
         case 38: return launch_r3h<T, 1, 16, 8, 64, 8>(p, st);
+        // 20-pixel-wide tiles for 20 x 20 outputs (yolox_l / yolox_x dark5 and PAFPN 512-channel 3x3s: the 32-wide
+        // tiles compute 37.5 % padding there); stride 2: 17 x 41 halo + three 24 KiB weight slots = all 160 KiB
+        case 39: return launch_r3h<T, 2, 20, 8, 128, 4>(p, st);
+        case 40: return launch_r3h<T, 1, 20, 8, 128, 4>(p, st);
         default: set_error("conv_r3 tile id %d", id); return YXH_EINVAL;
     }
 }

@@ -463,7 +463,7 @@ class OutBuffer:
 # (yoloxhip.h yxh_conv_desc.tile); for the weight-stationary 1x1 conv_ws1 (201-210, 241-258) the slab bit
 # selects the 16-byte-store epilogue instead (round 6)
 TILE_CANDIDATES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + list(range(33, 52))
-                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 151)] + [2 * i for i in range(161, 197)] + [2 * i + k for i in range(201, 211) for k in (0, 1)] + [2 * i for i in range(221, 237)] + [2 * i + k for i in range(241, 259) for k in (0, 1)] + [2 * i for i in range(261, 281)]
+                   + list(range(65, 71)) for k in (0, 1)] + [2 * 81, 2 * 82] + [2 * i for i in range(97, 105)] + [2 * i for i in range(113, 153)] + [2 * i for i in range(161, 197)] + [2 * i + k for i in range(201, 211) for k in (0, 1)] + [2 * i for i in range(221, 237)] + [2 * i + k for i in range(241, 259) for k in (0, 1)] + [2 * i for i in range(261, 281)]
 # 16-bit plans: the families that win on MI355X (profiles/r03/final/tune_r3fa_*.json: yolox_s picks only
 # conv_pwf / conv_ws / conv_ws1; yolox_l fp16 also conv_igemm and conv_r3 once or twice); the LDS-DMA
 # conv_glds, row-tiled conv_rows and the round-1 pointwise kernels never do and are tried only with

@@ -20,7 +20,7 @@ SHAPES = [(1, 160, 32, 32), (1, 80, 64, 64), (1, 40, 128, 128), (1, 20, 256, 256
           (2, 160, 64, 128), (2, 80, 128, 256), (2, 40, 256, 512), (2, 80, 128, 128), (2, 40, 256, 256)]
 if os.environ.get("WS_SHAPES"):  # e.g. "1,80,128,128;1,40,128,128"
     SHAPES = [tuple(int(v) for v in sh.split(",")) for sh in os.environ["WS_SHAPES"].split(";")]
-OLD = [2 * i for i in range(113, 151)]
+OLD = [2 * i for i in range(113, 153)]
 NEW = [2 * i for i in range(161, 191)]
 TILES = [int(t) for t in sys.argv[1:]] or OLD + NEW
 
