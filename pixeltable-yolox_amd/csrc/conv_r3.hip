@@ -546,6 +546,8 @@ static int r3h_dispatch_f32(int id, const ConvParams& p, hipStream_t st) {
         case 32: return launch_r3h<float, 1, 32, 8, 32, 8>(p, st);
         case 33: return launch_r3h<float, 2, 8, 8, 64, 4>(p, st);
         case 38: return launch_r3h<float, 1, 16, 8, 64, 8>(p, st);
+        case 39: return launch_r3h<float, 2, 20, 8, 128, 4>(p, st);
+        case 40: return launch_r3h<float, 1, 20, 8, 128, 4>(p, st);
         default: set_error("conv_r3 tile id %d is built for bf16/f16 only", id); return YXH_EUNSUPPORTED;
     }
 }

@@ -143,7 +143,7 @@ _BASE_TILES = [2 * i + k for i in list(range(1, 10)) + list(range(17, 26)) + lis
 CONV_TUNE_TILES = _BASE_TILES + ([] if os.environ.get("YOLOX_AMD_TRAIN_TILES16") == "base" else
                                  [2 * i for i in list(range(97, 105)) + list(range(161, 191)) + list(range(201, 211))
                                   + list(range(261, 290)) + list(range(217, 221))])
-CONV_TUNE_TILES_F32 = _BASE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38)] + [2 * i for i in range(211, 217)]
+CONV_TUNE_TILES_F32 = _BASE_TILES + [2 * (112 + i) for i in (29, 30, 31, 32, 33, 38, 39, 40)] + [2 * i for i in range(211, 217)]
 WGRAD_TUNE_TILES = list(range(1, 11)) + list(range(11, 17)) + list(range(17, 25)) + list(range(25, 31))
 _TRAIN_TILES: dict = {}
 # YOLOX_AMD_TUNE_CHECK_DET=1 (tests): every applicable candidate also runs twice into a zeroed sink and

@@ -697,7 +697,7 @@ def test_conv_r3h_fp32_accumulate(s):
     base = torch.randn(want_conv.shape, generator=torch.Generator().manual_seed(13))
     out = nhwc(base, torch.float32).contiguous()
     ran = 0
-    for tid in (141, 142, 143, 144, 145, 150):
+    for tid in (141, 142, 143, 144, 145, 150, 151, 152):
         out.copy_(nhwc(base, torch.float32))
         try:
             run_conv([(nhwc(x, torch.float32), 0, 64, 0)], conv, bn, torch.float32, act="none", out=out, tile=2 * tid,
