@@ -589,7 +589,7 @@ typedef struct {
  * train = 1: obj/cls stay logits (get_output_and_grid, :213-231); train = 2 (ABI 16): the
  * eval rows without the box decode (decode_in_inference = False, :208-211): reg raw, obj/cls
  * sigmoid.
- * scores (ABI 18, NULL = none; eval decode rows (train = 0) of the 64 / 128-channel 16-bit levels
+ * scores (ABI 18, NULL = none; eval decode rows (train = 0) of the 64 / 128 / 256-channel 16-bit levels
  * only): per anchor 8 floats {obj * max class, max class, its index, obj, cx, cy, w, h} -- the fp32
  * values utils.postprocess's filter computes from the row (boxes.py:46-48: first maximum, obj *
  * conf) and the row's box, from the same registers -- at [image][a_off + pixel], image stride

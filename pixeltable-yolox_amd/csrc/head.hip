@@ -193,9 +193,13 @@ __global__ __launch_bounds__(256) void head_pred(yxh_head_desc d) {
 // obj / cls logits, 2: eval raw rows -- raw boxes, sigmoid obj / cls): the decode is branch-free (every lane
 // evaluates its fragment-0 candidates and selects; 32-bit pixel / image arithmetic), where the runtime mode
 // tests and per-lane branches had split it into exec-masked blocks with SGPR spills (round 6)
+// 8 waves per block (two per SIMD) for 64 / 128 channels; 4 for 256 (yolox_l: its 6 x 8 weight fragments and the
+// two groups of 16 feature operands need ~350 registers, one wave per SIMD)
+constexpr int head2_waves(int cin) { return cin >= 256 ? 4 : 8; }
+
 template <typename T, int CIN, int NCF, int MODE>
-__global__ __launch_bounds__(512) void head_pred2(yxh_head_desc d) {
-    constexpr int NW = 8;
+__global__ __launch_bounds__(64 * head2_waves(CIN)) void head_pred2(yxh_head_desc d) {
+    constexpr int NW = head2_waves(CIN);
     constexpr int KS = CIN / 32;                 // K steps
     constexpr int NF = 1 + NCF;                  // output fragments: reg|obj, then cls
     constexpr int WROWS = NF * 16;
@@ -375,22 +379,25 @@ int head_pred_launch(const yxh_head_desc* d, hipStream_t st) {
     const bool rows16 = ((uintptr_t)d->reg.ptr % 16) == 0 && ((uintptr_t)d->cls.ptr % 16) == 0 &&
                         d->reg.cstride % 8 == 0 && d->cls.cstride % 8 == 0 && d->reg.bstride % 8 == 0 &&
                         d->cls.bstride % 8 == 0;
-    YXH_CHECK_ARG(!d->scores || (!v1 && rows16 && (d->cin == 64 || d->cin == 128) && d->train == 0 &&
+    YXH_CHECK_ARG(!d->scores || (!v1 && rows16 && (d->cin == 64 || d->cin == 128 || d->cin == 256) && d->train == 0 &&
                                  ((uintptr_t)d->scores % 16) == 0 && d->out_bstride % (5 + d->num_classes) == 0),
-                  "head_pred: score records need the head_pred2 path (eval decode rows, 64 / 128 16-bit channels, "
+                  "head_pred: score records need the head_pred2 path (eval decode rows, 64 / 128 / 256 16-bit channels, "
                   "16-byte rows) and a 16-byte aligned buffer");
-    if (!v1 && rows16 && (d->cin == 64 || d->cin == 128)) {
+    if (!v1 && rows16 && (d->cin == 64 || d->cin == 128 || d->cin == 256)) {
         const long long groups = (M + 15) / 16;
-        const unsigned grid2 = (unsigned)std::min<long long>((groups + 7) / 8, device_cus());  // one 8-wave block per CU
-#define YXH_HEAD2(T, CIN)                                                                           \
-    do {                                                                                            \
-        if (d->train == 1) hipLaunchKernelGGL((head_pred2<T, CIN, 5, 1>), dim3(grid2), dim3(512), 0, st, *d); \
-        else if (d->train == 2) hipLaunchKernelGGL((head_pred2<T, CIN, 5, 2>), dim3(grid2), dim3(512), 0, st, *d); \
-        else hipLaunchKernelGGL((head_pred2<T, CIN, 5, 0>), dim3(grid2), dim3(512), 0, st, *d);    \
+#define YXH_HEAD2(T, CIN)                                                                                        \
+    do {                                                                                                         \
+        constexpr int nw = head2_waves(CIN);                                                                     \
+        const unsigned grid2 = (unsigned)std::min<long long>((groups + nw - 1) / nw, device_cus()); /* a block per CU */ \
+        if (d->train == 1) hipLaunchKernelGGL((head_pred2<T, CIN, 5, 1>), dim3(grid2), dim3(64 * nw), 0, st, *d);     \
+        else if (d->train == 2) hipLaunchKernelGGL((head_pred2<T, CIN, 5, 2>), dim3(grid2), dim3(64 * nw), 0, st, *d); \
+        else hipLaunchKernelGGL((head_pred2<T, CIN, 5, 0>), dim3(grid2), dim3(64 * nw), 0, st, *d);                \
     } while (0)
         if (d->dtype == YXH_BF16 && d->cin == 128) YXH_HEAD2(bf16, 128);
+        else if (d->dtype == YXH_BF16 && d->cin == 256) YXH_HEAD2(bf16, 256);
         else if (d->dtype == YXH_BF16) YXH_HEAD2(bf16, 64);
         else if (d->dtype == YXH_F16 && d->cin == 128) YXH_HEAD2(f16, 128);
+        else if (d->dtype == YXH_F16 && d->cin == 256) YXH_HEAD2(f16, 256);
         else if (d->dtype == YXH_F16) YXH_HEAD2(f16, 64);
         else {
             set_error("head_pred: dtype %d not built", d->dtype);

@@ -1160,14 +1160,14 @@ class Plan:
         ``postprocess_device(..., scores=)`` filters instead of the rows (32 instead of 340 bytes read
         per anchor).  The records belong to the forward that wrote the output
         rows: the next forward overwrites them.  Eval decode plans whose every level is one
-        head_pred launch over 64 / 128 16-bit channels only; returns None (nothing enabled)
+        head_pred launch over 64 / 128 / 256 16-bit channels only; returns None (nothing enabled)
         otherwise.  Call before capture()."""
         if self._graph is not None or self._graph_alt is not None:
             raise RuntimeError("enable_scores() before capture()")
         heads = [r for r in self.ctx.ops if r.kind == N.OP_HEAD]
         other = [r for r in self.ctx.ops if r.kind == N.OP_CONV and (r.args["dst_f32"] or r.args.get("head_post"))]
         if (self.stage != "full" or not heads or other or self.ctx.dtype == torch.float32
-                or any(r.args["cin"] not in (64, 128) or r.args["train"] != PlanCtx.HEAD_EVAL for r in heads)):
+                or any(r.args["cin"] not in (64, 128, 256) or r.args["train"] != PlanCtx.HEAD_EVAL for r in heads)):
             return None
         if self.scores is None:
             self.scores = torch.zeros(self.batch, self.anchors, 8, dtype=torch.float32, device=self.device)

@@ -1201,12 +1201,12 @@ def test_conv_ws_residual_and_strided_dst():
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("cin,h,w,train", [(128, 8, 12, 0), (64, 20, 20, 0), (256, 4, 8, 1), (128, 10, 10, 1),
-                                           (128, 6, 6, 2), (64, 12, 8, 1)])
+                                           (128, 6, 6, 2), (64, 12, 8, 1), (256, 10, 10, 0), (256, 6, 6, 2)])
 def test_head_pred_fused_level(dtype, cin, h, w, train, monkeypatch):
     """yxh_head_pred: reg/obj/cls 1x1 preds + cat + sigmoid + decode of one level into
     rows [a_off, a_off + h*w) of a [B, A, 85] output, vs torch fp32 on the same (rounded)
     operands; other rows untouched.  Features are channel slices of wider buffers.  train = 2:
-    decode_in_inference = False (reg raw, obj / cls sigmoid).  For 64 / 128 channels the
+    decode_in_inference = False (reg raw, obj / cls sigmoid).  For 64 / 128 / 256 channels the
     per-wave head_pred2 runs, bit-identical to the tile kernel (YXH_HEAD_V1=1) -- 10 x 10 and
     6 x 6 levels put 16-pixel groups across image boundaries."""
     import ctypes as Cc

@@ -193,8 +193,9 @@ def test_mask_passes_match_one_pass(oracle, budget):
         lib.yxh_set_nms_mask_budget(0)
 
 
-@pytest.mark.parametrize("size,batch", [(320, 4), (640, 2)])
-def test_scored_filter_from_head_records(oracle, size, batch):
+@pytest.mark.parametrize("name,dtype,size,batch", [("yolox_s", torch.bfloat16, 320, 4), ("yolox_s", torch.bfloat16, 640, 2),
+                                                    ("yolox_l", torch.float16, 320, 2)])  # yolox_l: 256-channel head
+def test_scored_filter_from_head_records(oracle, name, dtype, size, batch):
     """Plan.enable_scores (ABI 18): the head launches also write per-anchor records {obj * max class,
     max class, class index, obj, cx, cy, w, h}; (1) the output rows are bit-identical to a plan without records,
     (2) every record equals the filter's own arithmetic on its row (first maximum, obj * conf in fp32),
@@ -205,12 +206,12 @@ def test_scored_filter_from_head_records(oracle, size, batch):
     from yolox_amd.models import YoloxModule
     from yolox_amd.utils.boxes import postprocess_device
     from yolox_amd.weights import synthetic_images
-    m = YoloxModule.synthetic("yolox_s", seed=0, device="cuda", dtype=torch.bfloat16)
+    m = YoloxModule.synthetic(name, seed=0, device="cuda", dtype=dtype)
     x = torch.from_numpy(synthetic_images(batch, size, size, seed=21)).cuda()
-    plain = Plan(m, batch, size, size, torch.bfloat16, "cuda", N.NHWC, torch.uint8)
+    plain = Plan(m, batch, size, size, dtype, "cuda", N.NHWC, torch.uint8)
     plain.static_input().copy_(x)
     want_rows = plain.replay().clone()
-    p = Plan(m, batch, size, size, torch.bfloat16, "cuda", N.NHWC, torch.uint8)
+    p = Plan(m, batch, size, size, dtype, "cuda", N.NHWC, torch.uint8)
     scores = p.enable_scores()
     assert scores is not None and tuple(scores.shape) == (batch, p.anchors, 8)
     p.static_input().copy_(x)
