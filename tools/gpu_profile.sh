@@ -33,8 +33,8 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
     > gpurun_out/pmc_${TAG}_SQ2.log 2>&1 || exit 1
 python tools/forward_timeline.py gpurun_out/prof_$TAG/run_kernel_trace.csv > gpurun_out/timeline_$TAG.txt || exit 1
 # HBM bytes of exactly the 4 timed forwards of the PMC passes, launch list reconciled with the trace
-python tools/traffic.py gpurun_out/pmc_$TAG gpurun_out/traffic_$TAG.json --replays 4 \
-    --timeline gpurun_out/timeline_$TAG.txt $TRAFFIC_ARGS || exit 1
+python tools/traffic.py gpurun_out/pmc_$TAG gpurun_out/traffic_$TAG.json $TRAFFIC_ARGS --replays 4 \
+    --timeline gpurun_out/timeline_$TAG.txt || exit 1
 python tools/mfma_util.py gpurun_out/pmc_${TAG}_SQ/run_counter_collection.csv --last 3 \
     --stalls gpurun_out/pmc_${TAG}_SQ2/run_counter_collection.csv --json gpurun_out/mfma_util_$TAG.json \
     > gpurun_out/mfma_util_$TAG.txt || exit 1
